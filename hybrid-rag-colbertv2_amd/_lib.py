@@ -1,0 +1,77 @@
+"""ctypes binding of libcolbert_mi355x.so (the C ABI in include/colbert_mi355x.h).
+
+There is no CPU fallback: if the library is missing or no HIP device is
+present, every compute entry point raises.  ctypes releases the GIL for the
+duration of each foreign call.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libcolbert_mi355x.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "colbert_mi355x.h")
+
+DTYPE_BF16 = 1
+DTYPE_F32 = 2
+SCORER_MAXSIM = 0
+SCORER_REF_MEANPOOL_COSINE = 1
+SCORERS = {"maxsim": SCORER_MAXSIM, "ref_meanpool_cosine": SCORER_REF_MEANPOOL_COSINE}
+ERR_EINVAL, ERR_EUNSUPPORTED, ERR_EHIP, ERR_ESTATE = -1, -2, -3, -4
+
+_p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+_SIGS = {
+    "cbv2_abi_version": (ctypes.c_int, []),
+    "cbv2_last_error": (ctypes.c_char_p, []),
+    "cbv2_index_create": (ctypes.c_int, [ctypes.c_int, _p, _i32, _i64, _i32, _i32, _p, _i64,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_index_destroy": (ctypes.c_int, [_p]),
+    "cbv2_index_build_means": (ctypes.c_int, [_p, _p, _i32, _p, _p]),
+    "cbv2_score": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _p, _i64, _p]),
+    "cbv2_search_workspace_bytes": (_sz, [_p, _i32]),
+    "cbv2_search": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p]),
+    "cbv2_rerank": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _p, _p, _p]),
+    "cbv2_select_topk": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
+    "cbv2_topk_rows": (ctypes.c_int, [_p, _i32, _i64, _i64, _i32, _i64, _p, _p, _p]),
+    "cbv2_merge_topk": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p]),
+    "cbv2_rrf_fuse": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _p]),
+}
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER):
+    """Every function the public header declares (used by the export test)."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(cbv2_\w+)\s*\(", text, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class Cbv2Error(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"cbv2 error {code}: {msg}")
+        self.code = code
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = lib().cbv2_last_error().decode(errors="replace")
+        if rc == ERR_EINVAL:
+            raise ValueError(msg)
+        raise Cbv2Error(rc, msg)
+    return rc

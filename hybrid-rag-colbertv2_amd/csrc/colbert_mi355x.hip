@@ -1,0 +1,893 @@
+// colbert_mi355x.hip — MI355X (gfx950 / CDNA4) kernels + C ABI for the ColBERT
+// late-interaction retrieval path.  See include/colbert_mi355x.h for the
+// contract and DESIGN.md for the roofline of each kernel.
+//
+// Kernels
+//   maxsim_scan_kernel   S[b,i] = sum_{q<lq} max_{t<len_i} <Q[b,q], D_i[t]>  (bf16 MFMA,
+//                        fp32 accumulate).  Replaces _maxsim_score (local_rag_complete.py:802-831)
+//                        in its north-star (true MaxSim) form.  Query-stationary: each
+//                        workgroup keeps 16 queries' fragments in VGPRs and streams a
+//                        contiguous doc chunk HBM -> LDS (global_load_lds, XOR-swizzled,
+//                        double-buffered); every doc tile is read once per workgroup.
+//   topk_rows_kernel     torch.topk (local_rag_complete.py:767): exact radix select on
+//                        order-preserving score bits, ties by lower doc index, bitonic sort.
+//   rerank_kernel        rerank (local_rag_complete.py:779-800) on precomputed tiles:
+//                        gather candidate docs by id straight into VGPRs, MaxSim, rank.
+//   select_small_kernel  argsort + [:k] (local_rag_complete.py:789-792) of a short row.
+//   merge_topk_kernel    cross-shard merge of sorted per-shard top-k lists.
+//   meanpool_*           the reference's literal arithmetic (mean-pool + cosine,
+//                        local_rag_complete.py:821-829) with doc means built once.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+#include <stdio.h>
+#include <string.h>
+
+#include "colbert_mi355x.h"
+
+namespace {
+
+constexpr int kDim = 128;                         // embedding dim (Jina-ColBERT-v2)
+constexpr int kLd = 128;                          // token slots per doc
+constexpr int kLqMax = 32;                        // query tokens per MFMA column block
+constexpr int kRowBytes = kDim * 2;               // 256 B per bf16 token row
+constexpr int kDocBytes = kLd * kRowBytes;        // 32 KiB per doc tile
+constexpr int kTopkMax = 1024;                    // largest k any selection supports
+constexpr int kSmallMax = 1024;                   // longest row for select_small / rerank C
+constexpr int kMergeMax = 8192;                   // G * k limit of the merge kernel
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+__device__ __forceinline__ float neg_inf() { return -__builtin_inff(); }
+
+// Order-preserving map float -> uint32 (larger float <=> larger uint).
+__device__ __forceinline__ uint32_t f2u(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float u2f(uint32_t u) {
+  u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  return __uint_as_float(u);
+}
+// Ranking key: score descending, then lower index first.
+__device__ __forceinline__ uint64_t rank_key(float s, uint32_t idx) {
+  return ((uint64_t)f2u(s) << 32) | (uint32_t)(~idx);
+}
+
+__device__ __forceinline__ float max16(const f32x16& a) {
+  float m0 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+  float m1 = fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]));
+  float m2 = fmaxf(fmaxf(a[8], a[9]), fmaxf(a[10], a[11]));
+  float m3 = fmaxf(fmaxf(a[12], a[13]), fmaxf(a[14], a[15]));
+  return fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+}
+
+// Accumulator init for a partially valid 32-token block: 0 for doc rows < dl,
+// -inf for padding rows.  Rows held by this lane for a 32x32x16 MFMA:
+// row(reg) = row0 + (reg&3) + 8*(reg>>2), row0 = 32*blk + 4*h.
+__device__ __forceinline__ f32x16 row_mask_init(int row0, int dl) {
+  f32x16 a;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) a[reg] = (row0 + (reg & 3) + 8 * (reg >> 2) < dl) ? 0.0f : neg_inf();
+  return a;
+}
+
+// Sum over the 32 query-token columns after folding the two row halves.
+// Every lane ends with the identical value (xor butterfly of commutative adds).
+__device__ __forceinline__ float col_reduce(float m, int r, int lq) {
+  float v = fmaxf(m, __shfl_xor(m, 32));
+  v = (r < lq) ? v : 0.0f;
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 1);
+  return v;
+}
+
+// B-operand fragments of one query for v_mfma_f32_32x32x16_bf16.  Lane l
+// (r = l&31 query token, h = l>>5) holds, for k-step s, dims 64h+8s .. 64h+8s+7
+// of token r.  The doc A-operand uses the same permutation of the 128 dims, so
+// the 8 k-steps still sum every dim exactly once.
+__device__ __forceinline__ void load_qfrag(const uint16_t* __restrict__ Q, int qi, int B, int lq,
+                                           int lane, bf16x8 (&qf)[8]) {
+  const int r = lane & 31, h = lane >> 5;
+  const bool ok = (qi < B) && (r < lq);
+  const u32x4* src = reinterpret_cast<const u32x4*>(Q + ((size_t)(ok ? qi : 0) * lq + (ok ? r : 0)) * kDim + 64 * h);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    u32x4 v = ok ? src[s] : u32x4{0u, 0u, 0u, 0u};
+    qf[s] = __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MaxSim scan.  Grid = n_qgroups * n_chunks workgroups of WAVES waves; each
+// wave owns QW queries.  Doc tiles: LDS image [128 tokens][16 slots of 16 B],
+// slot p of token t holding logical slot p ^ (t & 15) (conflict-free
+// ds_read_b128 for the A-fragment pattern; filled by lane-linear LDS-DMA with
+// the XOR applied to the per-lane SOURCE address).
+// ---------------------------------------------------------------------------
+template <int WAVES, int QW>
+__global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
+    int64_t chunk_docs) {
+  constexpr int QPB = WAVES * QW;
+  constexpr int kPieces = kDocBytes / 1024;       // 1-KiB LDS-DMA pieces per doc
+  constexpr int kPiecesPerWave = kPieces / WAVES;
+  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * kDocBytes];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+
+  // XCD-aware, bijective block -> (query group, chunk): the blocks dealt to one
+  // XCD (b % 8) cover consecutive linear ids, query group fastest, so all query
+  // groups of a chunk stream the same docs through the same L2 at once.
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int g = lin % nq_groups;
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;  // uniform over the workgroup
+  const int nd = (int)(d_end - d_begin);
+
+  bf16x8 qf[QW][8];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag(Q, g * QPB + wave * QW + q, B, lq, lane, qf[q]);
+
+  // LDS-DMA source offsets of this lane's pieces (same for every doc).
+  uint32_t src_off[kPiecesPerWave];
+#pragma unroll
+  for (int j = 0; j < kPiecesPerWave; ++j) {
+    const int piece = wave * kPiecesPerWave + j;
+    const int t = 4 * piece + (lane >> 4);
+    const int p = lane & 15;
+    src_off[j] = t * kRowBytes + 16 * (p ^ (t & 15));
+  }
+  auto issue = [&](int i, int buf) {
+    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kDocBytes;
+#pragma unroll
+    for (int j = 0; j < kPiecesPerWave; ++j) {
+      const int piece = wave * kPiecesPerWave + j;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(dbase + src_off[j]),
+                                       (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16, 0, 0);
+    }
+  };
+
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+
+  issue(0, 0);
+  for (int i = 0; i < nd; ++i) {
+    // doc i landed (own pieces) -> barrier (everyone's pieces; everyone done with i-1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i + 1 < nd) issue(i + 1, (i + 1) & 1);
+
+    const uint8_t* buf = smem + (i & 1) * kDocBytes;
+    int dl = doclens[d_begin + i];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    float m[QW];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) m[q] = neg_inf();
+#pragma unroll
+    for (int c = 0; c < kLd / 32; ++c) {
+      if (dl > 32 * c) {
+        bf16x8 af[8];
+        const uint8_t* row = buf + (32 * c + r) * kRowBytes;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+          af[s] = *reinterpret_cast<const bf16x8*>(row + 16 * ((8 * h + s) ^ (r & 15)));
+        // Padding rows (t >= dl) start their accumulation at -inf, so they can
+        // never win the max: masking costs nothing on full blocks.
+        const f32x16 init = (dl >= 32 * c + 32) ? f32x16{} : row_mask_init(32 * c + 4 * h, dl);
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          f32x16 acc = init;
+#pragma unroll
+          for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], qf[q][s], acc, 0, 0, 0);
+          m[q] = fmaxf(m[q], max16(acc));
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = col_reduce(m[q], r, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = g * QPB + wave * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row top-k: exact radix select (11/11/10-bit digits of the order-preserving
+// score key; if the k-th score is tied, a second radix select over ~index picks
+// the lowest indices), then a bitonic sort of the k winners in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kTkThreads = 1024;
+
+// Wave 0 finds bin b with count(bins > b) < kleft <= count(bins >= b).
+__device__ void find_bin(const uint32_t* hist, int nb, uint32_t kleft, uint32_t* s_bin,
+                         uint32_t* s_above, uint32_t* s_bincount) {
+  const int lane = threadIdx.x & 63;
+  const int per = nb / 64;
+  uint32_t tot = 0;
+  for (int j = 0; j < per; ++j) tot += hist[lane * per + j];
+  uint32_t incl = tot;  // inclusive suffix sum over lanes >= lane
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t t = __shfl_down(incl, off);
+    if (lane + off < 64) incl += t;
+  }
+  const uint32_t above = incl - tot;
+  const bool mine = (above < kleft) && (kleft <= incl);
+  if (mine) {
+    uint32_t cum = above;
+    for (int j = per - 1; j >= 0; --j) {
+      const uint32_t c = hist[lane * per + j];
+      if (cum + c >= kleft) {
+        *s_bin = lane * per + j;
+        *s_above = cum;
+        *s_bincount = c;
+        break;
+      }
+      cum += c;
+    }
+  }
+}
+
+__device__ void bitonic_desc(uint64_t* keys, int P) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint64_t a = keys[i], b = keys[j];
+          const bool desc = (i & size) == 0;
+          if (desc ? (a < b) : (a > b)) {
+            keys[i] = b;
+            keys[j] = a;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __restrict__ scores, int64_t n,
+                                                               int64_t ld, int k, int64_t id_base,
+                                                               float* __restrict__ out_s,
+                                                               int32_t* __restrict__ out_i) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint64_t sel[kTopkMax];
+  __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const float* x = scores + (size_t)blockIdx.x * ld;
+  const int kk = (int)((int64_t)k < n ? k : n);
+
+  if (kk == n) {
+    for (int i = tid; i < kk; i += kTkThreads) sel[i] = rank_key(x[i], (uint32_t)i);
+  } else {
+    const int shifts[3] = {21, 10, 0};
+    const int bits[3] = {11, 11, 10};
+    uint32_t prefix = 0, mask = 0, kleft = (uint32_t)kk, last_count = 0;
+    for (int p = 0; p < 3; ++p) {
+      const int nb = 1 << bits[p];
+      for (int b = tid; b < nb; b += kTkThreads) hist[b] = 0;
+      __syncthreads();
+      for (int64_t i = tid; i < n; i += kTkThreads) {
+        const uint32_t u = f2u(x[i]);
+        if ((u & mask) == prefix) atomicAdd(&hist[(u >> shifts[p]) & (nb - 1)], 1u);
+      }
+      __syncthreads();
+      if (wave == 0) find_bin(hist, nb, kleft, &s_bin, &s_above, &s_bincount);
+      __syncthreads();
+      kleft -= s_above;
+      prefix |= s_bin << shifts[p];
+      mask |= (uint32_t)(nb - 1) << shifts[p];
+      last_count = s_bincount;
+      __syncthreads();
+    }
+    const uint32_t ustar = prefix;
+    uint32_t id_thr = 0xffffffffu;  // ties at ustar with index <= id_thr are taken
+    if (kleft < last_count) {
+      uint32_t iprefix = 0, imask = 0, kl2 = kleft;
+      for (int p = 0; p < 3; ++p) {
+        const int nb = 1 << bits[p];
+        for (int b = tid; b < nb; b += kTkThreads) hist[b] = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < n; i += kTkThreads) {
+          const uint32_t key2 = ~(uint32_t)i;
+          if (f2u(x[i]) == ustar && (key2 & imask) == iprefix)
+            atomicAdd(&hist[(key2 >> shifts[p]) & (nb - 1)], 1u);
+        }
+        __syncthreads();
+        if (wave == 0) find_bin(hist, nb, kl2, &s_bin, &s_above, &s_bincount);
+        __syncthreads();
+        kl2 -= s_above;
+        iprefix |= s_bin << shifts[p];
+        imask |= (uint32_t)(nb - 1) << shifts[p];
+        __syncthreads();
+      }
+      id_thr = ~iprefix;
+    }
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += kTkThreads) {
+      const uint32_t u = f2u(x[i]);
+      if (u > ustar || (u == ustar && (uint32_t)i <= id_thr)) {
+        const uint32_t pos = atomicAdd(&s_cnt, 1u);
+        if (pos < (uint32_t)kTopkMax) sel[pos] = ((uint64_t)u << 32) | (uint32_t)(~(uint32_t)i);
+      }
+    }
+  }
+  __syncthreads();
+  int P = 1;
+  while (P < kk) P <<= 1;
+  for (int i = kk + tid; i < P; i += kTkThreads) sel[i] = 0;
+  bitonic_desc(sel, P);
+  for (int j = tid; j < k; j += kTkThreads) {
+    float s = neg_inf();
+    int32_t id = -1;
+    if (j < kk) {
+      const uint64_t key = sel[j];
+      s = u2f((uint32_t)(key >> 32));
+      id = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+    }
+    out_s[(size_t)blockIdx.x * k + j] = s;
+    out_i[(size_t)blockIdx.x * k + j] = id;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small-row selection (rank counting; rows of C <= 1024).
+// ---------------------------------------------------------------------------
+__device__ void select_from_lds(const float* sc, const uint64_t* keys, int C, int k, const int32_t* ids_row,
+                                float* out_s, int32_t* out_i, int32_t* out_p) {
+  for (int t = threadIdx.x; t < C; t += blockDim.x) {
+    const uint64_t kt = keys[t];
+    int rank = 0;
+    for (int j = 0; j < C; ++j) rank += (keys[j] > kt);
+    if (rank < k) {
+      out_s[rank] = sc[t];
+      if (out_i) out_i[rank] = ids_row ? ids_row[t] : t;
+      if (out_p) out_p[rank] = t;
+    }
+  }
+  for (int j = C + threadIdx.x; j < k; j += blockDim.x) {
+    out_s[j] = neg_inf();
+    if (out_i) out_i[j] = -1;
+    if (out_p) out_p[j] = -1;
+  }
+}
+
+__global__ __launch_bounds__(256) void select_small_kernel(const float* __restrict__ scores,
+                                                           const int32_t* __restrict__ ids, int C, int k,
+                                                           float* __restrict__ out_s,
+                                                           int32_t* __restrict__ out_i,
+                                                           int32_t* __restrict__ out_p) {
+  __shared__ float sc[kSmallMax];
+  __shared__ uint64_t keys[kSmallMax];
+  const size_t b = blockIdx.x;
+  for (int t = threadIdx.x; t < C; t += blockDim.x) {
+    sc[t] = scores[b * C + t];
+    keys[t] = rank_key(sc[t], (uint32_t)t);
+  }
+  __syncthreads();
+  select_from_lds(sc, keys, C, k, ids ? ids + b * C : nullptr, out_s + b * k, out_i ? out_i + b * k : nullptr,
+                  out_p ? out_p + b * k : nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// Rerank: one workgroup per query; each wave gathers whole candidate docs
+// (32 KiB, contiguous) straight into VGPRs and scores them with the same MFMA
+// tiling as the scan; then rank-select top-k in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kRrWaves = 8;
+__global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
+    const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, int k,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i, int32_t* __restrict__ out_p) {
+  __shared__ float sc[kSmallMax];
+  __shared__ uint64_t keys[kSmallMax];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.x;
+  bf16x8 qf[8];
+  load_qfrag(Q, b, b + 1, lq, lane, qf);
+  const int32_t* crow = cand + (size_t)b * C;
+  for (int c = wave; c < C; c += kRrWaves) {
+    const int32_t id = crow[c];
+    const int64_t loc = (int64_t)id - id_base;
+    float v = neg_inf();
+    if (id >= 0 && loc >= 0 && loc < n) {
+      int dl = doclens[loc];
+      dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+      const uint8_t* dbase = tokens + (size_t)loc * kDocBytes;
+      bf16x8 af[4][8];
+#pragma unroll
+      for (int blk = 0; blk < 4; ++blk) {
+        if (dl > 32 * blk) {
+          const u32x4* src = reinterpret_cast<const u32x4*>(dbase + (32 * blk + r) * kRowBytes + 128 * h);
+#pragma unroll
+          for (int s = 0; s < 8; ++s) af[blk][s] = __builtin_bit_cast(bf16x8, src[s]);
+        }
+      }
+      float m = neg_inf();
+#pragma unroll
+      for (int blk = 0; blk < 4; ++blk) {
+        if (dl > 32 * blk) {
+          f32x16 acc = (dl >= 32 * blk + 32) ? f32x16{} : row_mask_init(32 * blk + 4 * h, dl);
+#pragma unroll
+          for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[blk][s], qf[s], acc, 0, 0, 0);
+          m = fmaxf(m, max16(acc));
+        }
+      }
+      v = col_reduce(m, r, lq);
+    }
+    if (lane == 0) sc[c] = v;
+  }
+  __syncthreads();
+  if (k == 0) {
+    for (int t = threadIdx.x; t < C; t += blockDim.x) out_s[(size_t)b * C + t] = sc[t];
+    return;
+  }
+  for (int t = threadIdx.x; t < C; t += blockDim.x) keys[t] = rank_key(sc[t], (uint32_t)t);
+  __syncthreads();
+  select_from_lds(sc, keys, C, k, crow, out_s + (size_t)b * k, out_i + (size_t)b * k,
+                  out_p ? out_p + (size_t)b * k : nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// Merge G sorted per-shard lists: rank = own position + #greater keys in every
+// other list (binary search); ids are unique across shards so ranks are too.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void merge_topk_kernel(const float* __restrict__ in_s,
+                                                         const int32_t* __restrict__ in_i, int G, int B,
+                                                         int k, float* __restrict__ out_s,
+                                                         int32_t* __restrict__ out_i) {
+  __shared__ uint64_t keys[kMergeMax];
+  __shared__ int nvalid[64];
+  const int b = blockIdx.x;
+  for (int t = threadIdx.x; t < G * k; t += blockDim.x) {
+    const int g = t / k, j = t % k;
+    const size_t src = ((size_t)g * B + b) * k + j;
+    const int32_t id = in_i[src];
+    keys[t] = id >= 0 ? rank_key(in_s[src], (uint32_t)id) : 0ull;
+  }
+  if (threadIdx.x < G) {
+    int cnt = 0;
+    const size_t base = ((size_t)threadIdx.x * B + b) * k;
+    while (cnt < k && in_i[base + cnt] >= 0) ++cnt;
+    nvalid[threadIdx.x] = cnt;
+  }
+  __syncthreads();
+  int total = 0;
+  for (int g = 0; g < G; ++g) total += nvalid[g];
+  for (int t = threadIdx.x; t < G * k; t += blockDim.x) {
+    const int g = t / k, j = t % k;
+    if (j >= nvalid[g]) continue;
+    const uint64_t key = keys[t];
+    int rank = j;
+    for (int g2 = 0; g2 < G; ++g2) {
+      if (g2 == g) continue;
+      const uint64_t* L = keys + g2 * k;
+      int lo = 0, hi = nvalid[g2];  // count of entries > key (list sorted descending)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (L[mid] > key) lo = mid + 1; else hi = mid;
+      }
+      rank += lo;
+    }
+    if (rank < k) {
+      out_s[(size_t)b * k + rank] = u2f((uint32_t)(key >> 32));
+      out_i[(size_t)b * k + rank] = (int32_t)(~(uint32_t)key);
+    }
+  }
+  for (int j = total + threadIdx.x; j < k; j += blockDim.x) {
+    out_s[(size_t)b * k + j] = neg_inf();
+    out_i[(size_t)b * k + j] = -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Literal reference scorer: cosine(mean_q, mean_d) as torch computes it
+// (x / max(||x||, 1e-8), then sum of products).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void meanpool_build_kernel(const float* __restrict__ tok, int ld_src,
+                                                             const int32_t* __restrict__ doclens,
+                                                             float* __restrict__ means) {
+  __shared__ float red[2];
+  const size_t doc = blockIdx.x;
+  const int d = threadIdx.x;
+  int dl = doclens[doc];
+  dl = dl < 0 ? 0 : (dl > ld_src ? ld_src : dl);
+  float s = 0.0f;
+  for (int t = 0; t < dl; ++t) s += tok[(doc * ld_src + t) * kDim + d];
+  const float mean = dl > 0 ? s / (float)dl : 0.0f;
+  float sq = mean * mean;
+  for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  const float nrm = sqrtf(red[0] + red[1]);
+  means[doc * kDim + d] = mean / fmaxf(nrm, 1e-8f);
+}
+
+constexpr int kMpDocs = 64, kMpQ = 16;
+__global__ __launch_bounds__(256) void meanpool_scores_kernel(const float* __restrict__ means, int64_t n,
+                                                              const float* __restrict__ Q, int B, int lq,
+                                                              float* __restrict__ out, int64_t ld_out) {
+  __shared__ float qn[kMpQ][kDim];
+  __shared__ float dm[kMpDocs][kDim + 1];
+  const int tid = threadIdx.x;
+  const int64_t doc0 = (int64_t)blockIdx.x * kMpDocs;
+  const int q0 = blockIdx.y * kMpQ;
+  {  // normalised query means: 16 threads per query, 8 dims each
+    const int qq = tid >> 4, part = tid & 15;
+    const int qi = q0 + qq;
+    float mv[8];
+    float sq = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.0f;
+      if (qi < B)
+        for (int t = 0; t < lq; ++t) s += Q[((size_t)qi * lq + t) * kDim + part * 8 + j];
+      mv[j] = s / (float)lq;
+      sq += mv[j] * mv[j];
+    }
+    for (int off = 8; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+    const float inv = 1.0f / fmaxf(sqrtf(sq), 1e-8f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qn[qq][part * 8 + j] = mv[j] * inv;
+  }
+  for (int e = tid; e < kMpDocs * kDim; e += 256) {
+    const int dd = e / kDim, c = e % kDim;
+    dm[dd][c] = (doc0 + dd < n) ? means[(size_t)(doc0 + dd) * kDim + c] : 0.0f;
+  }
+  __syncthreads();
+  const int dd = tid & 63;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int qq = (tid >> 6) * 4 + j;
+    float s = 0.0f;
+    for (int c = 0; c < kDim; ++c) s += qn[qq][c] * dm[dd][c];
+    if (q0 + qq < B && doc0 + dd < n) out[(size_t)(q0 + qq) * ld_out + doc0 + dd] = s;
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+struct cbv2_index {
+  int device;
+  const uint8_t* tokens;
+  int64_t n;
+  int32_t ld, d;
+  const int32_t* doclens;
+  int64_t id_base;
+  const float* doc_means;
+};
+
+namespace {
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define CBV2_HIP(call)                                                                    \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) return fail(CBV2_EHIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+#define CBV2_REQUIRE(cond, ...) \
+  do {                          \
+    if (!(cond)) return fail(CBV2_EINVAL, __VA_ARGS__); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) { ok = false; return; }
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) ok = false;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int cu_count(int dev) {
+  static int cache[64] = {0};
+  if (dev >= 0 && dev < 64 && cache[dev]) return cache[dev];
+  int v = 256;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+  if (dev >= 0 && dev < 64) cache[dev] = v;
+  return v;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CBV2_EHIP, "%s launch: %s", what, hipGetErrorString(e));
+  return CBV2_OK;
+}
+
+constexpr int kScanWaves = 4, kScanQW = 4, kScanQPB = kScanWaves * kScanQW;
+
+int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
+                hipStream_t st) {
+  if (ix->n == 0) return CBV2_OK;
+  const int nq_groups = (B + kScanQPB - 1) / kScanQPB;
+  const int64_t target = 2LL * cu_count(ix->device);  // two resident workgroups per CU
+  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  if (n_chunks < 1) n_chunks = 1;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t grid = (int64_t)nq_groups * n_chunks;
+  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  hipLaunchKernelGGL((maxsim_scan_kernel<kScanWaves, kScanQW>), dim3((unsigned)grid), dim3(kScanWaves * 64), 0,
+                     st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs);
+  return launch_check("maxsim_scan_kernel");
+}
+
+int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+  if (ix->n == 0) return CBV2_OK;
+  dim3 grid((unsigned)((ix->n + kMpDocs - 1) / kMpDocs), (unsigned)((B + kMpQ - 1) / kMpQ));
+  hipLaunchKernelGGL(meanpool_scores_kernel, grid, dim3(256), 0, st, ix->doc_means, ix->n, Q, B, lq, out, ld_out);
+  return launch_check("meanpool_scores_kernel");
+}
+
+int check_query(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B, int32_t lq) {
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  CBV2_REQUIRE(Q != nullptr, "null query pointer");
+  CBV2_REQUIRE(B >= 1, "B must be >= 1 (got %d)", B);
+  CBV2_REQUIRE(lq >= 1, "lq must be >= 1 (got %d)", lq);
+  CBV2_REQUIRE(aligned16(Q), "query pointer must be 16-byte aligned");
+  if (scorer == CBV2_SCORER_MAXSIM) {
+    CBV2_REQUIRE(q_dtype == CBV2_DTYPE_BF16, "maxsim scorer takes bf16 queries");
+    CBV2_REQUIRE(lq <= kLqMax, "maxsim takes at most %d query tokens (got %d)", kLqMax, lq);
+  } else if (scorer == CBV2_SCORER_REF_MEANPOOL_COSINE) {
+    CBV2_REQUIRE(q_dtype == CBV2_DTYPE_F32, "ref_meanpool_cosine scorer takes f32 queries");
+    if (ix->doc_means == nullptr) return fail(CBV2_ESTATE, "doc means not built (cbv2_index_build_means)");
+  } else {
+    return fail(CBV2_EINVAL, "unknown scorer %d", scorer);
+  }
+  return CBV2_OK;
+}
+
+int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t lq, float* out,
+               int64_t ld_out, hipStream_t st) {
+  if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st);
+  return scan_meanpool(ix, (const float*)Q, B, lq, out, ld_out, st);
+}
+
+int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, float* out_s,
+              int32_t* out_i, hipStream_t st) {
+  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
+                     out_s, out_i);
+  return launch_check("topk_rows_kernel");
+}
+}  // namespace
+
+extern "C" {
+
+int cbv2_abi_version(void) { return CBV2_ABI_VERSION; }
+
+const char* cbv2_last_error(void) { return g_err; }
+
+int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, int32_t ld, int32_t d,
+                      const int32_t* doclens, int64_t id_base, cbv2_index** out) {
+  CBV2_REQUIRE(out != nullptr, "null output handle pointer");
+  *out = nullptr;
+  CBV2_REQUIRE(n >= 0 && n <= 0x7fffffffLL, "n out of range (%lld)", (long long)n);
+  CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "global ids must fit int32");
+  if (dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "index dtype %d not built (bf16 only)", dtype);
+  if (ld != kLd || d != kDim)
+    return fail(CBV2_EUNSUPPORTED, "index geometry ld=%d d=%d not built (ld=128, d=128)", ld, d);
+  if (n > 0) {
+    CBV2_REQUIRE(tokens != nullptr && doclens != nullptr, "null tokens/doclens");
+    CBV2_REQUIRE(aligned16(tokens), "tokens must be 16-byte aligned");
+  }
+  int ndev = 0;
+  CBV2_HIP(hipGetDeviceCount(&ndev));
+  CBV2_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
+  cbv2_index* ix = new cbv2_index{device, (const uint8_t*)tokens, n, ld, d, doclens, id_base, nullptr};
+  *out = ix;
+  return CBV2_OK;
+}
+
+int cbv2_index_destroy(cbv2_index* index) {
+  delete index;
+  return CBV2_OK;
+}
+
+int cbv2_index_build_means(cbv2_index* ix, const float* tokens_f32, int32_t ld_src, float* doc_means,
+                           void* stream) {
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  CBV2_REQUIRE(ld_src >= 1, "ld_src must be >= 1");
+  CBV2_REQUIRE(ix->n == 0 || (tokens_f32 && doc_means), "null tokens_f32/doc_means");
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  if (ix->n > 0) {
+    hipLaunchKernelGGL(meanpool_build_kernel, dim3((unsigned)ix->n), dim3(128), 0, (hipStream_t)stream,
+                       tokens_f32, ld_src, ix->doclens, doc_means);
+    int rc = launch_check("meanpool_build_kernel");
+    if (rc) return rc;
+  }
+  ix->doc_means = doc_means;
+  return CBV2_OK;
+}
+
+int cbv2_score(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+               float* out, int64_t ld_out, void* stream) {
+  int rc = check_query(ix, scorer, Q, q_dtype, B, lq);
+  if (rc) return rc;
+  CBV2_REQUIRE(ix->n == 0 || out != nullptr, "null output");
+  CBV2_REQUIRE(ld_out >= ix->n, "ld_out (%lld) < n (%lld)", (long long)ld_out, (long long)ix->n);
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  return score_impl(ix, scorer, Q, B, lq, out, ld_out, (hipStream_t)stream);
+}
+
+size_t cbv2_search_workspace_bytes(const cbv2_index* ix, int32_t B) {
+  if (!ix || B < 1) return 0;
+  return (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
+}
+
+int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                int32_t k, void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids,
+                void* stream) {
+  int rc = check_query(ix, scorer, Q, q_dtype, B, lq);
+  if (rc) return rc;
+  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(out_scores && out_ids, "null outputs");
+  const size_t need = cbv2_search_workspace_bytes(ix, B);
+  CBV2_REQUIRE(workspace != nullptr && workspace_bytes >= need, "workspace too small (%zu < %zu)",
+               workspace_bytes, need);
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  rc = score_impl(ix, scorer, Q, B, lq, ws, ix->n, st);
+  if (rc) return rc;
+  return topk_impl(ws, B, ix->n, ix->n, k, ix->id_base, out_scores, out_ids, st);
+}
+
+int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
+                float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+  int rc = check_query(ix, CBV2_SCORER_MAXSIM, Q, CBV2_DTYPE_BF16, B, lq);
+  if (rc) return rc;
+  CBV2_REQUIRE(cand != nullptr, "null candidates");
+  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
+  CBV2_REQUIRE(k >= 0 && k <= kTopkMax, "k must be in [0, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(out_scores != nullptr, "null out_scores");
+  CBV2_REQUIRE(k == 0 || out_ids != nullptr, "null out_ids");
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)B), dim3(kRrWaves * 64), 0, (hipStream_t)stream, ix->tokens,
+                     ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids,
+                     out_pos);
+  return launch_check("rerank_kernel");
+}
+
+int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t C, int32_t k, float* out_scores,
+                     int32_t* out_ids, int32_t* out_pos, void* stream) {
+  CBV2_REQUIRE(scores && out_scores, "null scores/out_scores");
+  CBV2_REQUIRE(B >= 1, "B must be >= 1");
+  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
+  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, scores, ids, C, k,
+                     out_scores, out_ids, out_pos);
+  return launch_check("select_small_kernel");
+}
+
+int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base,
+                   float* out_scores, int32_t* out_ids, void* stream) {
+  CBV2_REQUIRE(scores && out_scores && out_ids, "null pointer");
+  CBV2_REQUIRE(B >= 1, "B must be >= 1");
+  CBV2_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "n out of range");
+  CBV2_REQUIRE(ld >= n, "ld < n");
+  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "ids must fit int32");
+  return topk_impl(scores, B, n, ld, k, id_base, out_scores, out_ids, (hipStream_t)stream);
+}
+
+int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
+                    float* out_scores, int32_t* out_ids, void* stream) {
+  CBV2_REQUIRE(in_scores && in_ids && out_scores && out_ids, "null pointer");
+  CBV2_REQUIRE(G >= 1 && G <= 64, "G must be in [1, 64]");
+  CBV2_REQUIRE(B >= 1, "B must be >= 1");
+  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d]", kTopkMax);
+  CBV2_REQUIRE((int64_t)G * k <= kMergeMax, "G*k must be <= %d", kMergeMax);
+  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores, in_ids, G,
+                     B, k, out_scores, out_ids);
+  return launch_check("merge_topk_kernel");
+}
+
+// Host-side reciprocal rank fusion (HOST pointers).  Restates
+// HybridRetriever._reciprocal_rank_fusion (local_rag_complete.py:960-978):
+// score[id] += 1.0 / (rrf_k + rank) over the BM25 list, then the ColBERT list
+// (rank 1-based, float64, same operation order as the Python), then a STABLE
+// sort by score descending, so ties keep first-insertion order.  ids < 0 are
+// padding and skipped.  Writes the first C fused ids/scores per query (-1 / 0
+// padded); out_count (nullable) receives the number of distinct ids.
+int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_ids, int32_t kc, int32_t B,
+                  int32_t rrf_k, int32_t C, int32_t* out_ids, double* out_scores, int32_t* out_count) {
+  CBV2_REQUIRE(B >= 1 && C >= 1 && kb >= 0 && kc >= 0, "bad sizes");
+  CBV2_REQUIRE((kb == 0 || bm25_ids) && (kc == 0 || colbert_ids) && out_ids, "null pointer");
+  std::vector<int32_t> ids;
+  std::vector<double> sc;
+  std::vector<int> order;
+  ids.reserve(kb + kc);
+  sc.reserve(kb + kc);
+  for (int32_t b = 0; b < B; ++b) {
+    ids.clear();
+    sc.clear();
+    auto add = [&](int32_t id, int32_t rank) {
+      const double inc = 1.0 / (double)(rrf_k + rank);
+      for (size_t j = 0; j < ids.size(); ++j)
+        if (ids[j] == id) { sc[j] = sc[j] + inc; return; }
+      ids.push_back(id);
+      sc.push_back(0.0 + inc);
+    };
+    for (int32_t r = 0; r < kb; ++r) {
+      const int32_t id = bm25_ids[(size_t)b * kb + r];
+      if (id >= 0) add(id, r + 1);
+    }
+    for (int32_t r = 0; r < kc; ++r) {
+      const int32_t id = colbert_ids[(size_t)b * kc + r];
+      if (id >= 0) add(id, r + 1);
+    }
+    order.resize(ids.size());
+    for (size_t j = 0; j < ids.size(); ++j) order[j] = (int)j;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return sc[a] > sc[c]; });
+    for (int32_t j = 0; j < C; ++j) {
+      const bool ok = j < (int32_t)order.size();
+      out_ids[(size_t)b * C + j] = ok ? ids[order[j]] : -1;
+      if (out_scores) out_scores[(size_t)b * C + j] = ok ? sc[order[j]] : 0.0;
+    }
+    if (out_count) out_count[b] = (int32_t)ids.size();
+  }
+  return CBV2_OK;
+}
+
+}  // extern "C"

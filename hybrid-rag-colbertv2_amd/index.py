@@ -1,0 +1,263 @@
+"""HBM-resident ColBERT index shard and its device calls.
+
+Replaces the reference's ``self.corpus_embeddings`` tensor
+(local_rag_complete.py:725, 735-739, 751-752), which holds whatever
+``SentenceTransformer.encode`` returned, fp32, on "mps"/"cpu".  Here a shard
+is a contiguous id range ``[id_base, id_base + n)`` of the corpus laid out for
+the MI355X scan kernel:
+
+    tokens   bf16 [n, 128, 128]  (32 KiB per doc, rows >= doclen are padding)
+    doclens  int32 [n]
+    means    f32  [n, 128]       (optional: literal-reference scorer only)
+
+All compute goes through libcolbert_mi355x.so (``_lib``); the tensors are
+owned here and borrowed by the C handle.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, List, Optional, Sequence, Tuple, Union
+
+import torch
+
+from . import _lib
+
+LD = 128
+DIM = 128
+LQ_MAX = 32
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_cuda(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a ROCm device tensor (got {t.device})")
+
+
+def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
+                ld: int = LD) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Token matrices -> (bf16 [n, ld, 128] padded with zeros, int32 doclens [n]).
+
+    Accepts a dense ``[n, L, D]`` tensor (every doc has L tokens, as the
+    reference's stacked encode output), a pooled ``[n, D]`` tensor (one token
+    per doc: the shape ``encode`` returns by default), or a list of ``[L_i, D]``.
+    """
+    if isinstance(embs, torch.Tensor):
+        if embs.dim() == 2:
+            embs = embs.unsqueeze(1)
+        if embs.dim() != 3:
+            raise ValueError(f"expected [n, L, {DIM}] or [n, {DIM}] embeddings, got {tuple(embs.shape)}")
+        n, L, D = embs.shape
+        if D != DIM or L > ld:
+            raise ValueError(f"doc embeddings must be [n, L<={ld}, {DIM}] (got {tuple(embs.shape)})")
+        tokens = torch.zeros((n, ld, DIM), dtype=torch.bfloat16, device=device)
+        tokens[:, :L] = embs.to(device=device, dtype=torch.bfloat16)
+        doclens = torch.full((n,), L, dtype=torch.int32, device=device)
+        return tokens, doclens
+    embs = list(embs)
+    n = len(embs)
+    tokens = torch.zeros((n, ld, DIM), dtype=torch.bfloat16, device=device)
+    lens = []
+    for i, e in enumerate(embs):
+        e = e if e.dim() == 2 else e.unsqueeze(0)
+        if e.shape[-1] != DIM or e.shape[0] > ld:
+            raise ValueError(f"doc {i}: expected [L<={ld}, {DIM}] tokens, got {tuple(e.shape)}")
+        tokens[i, : e.shape[0]] = e.to(device=device, dtype=torch.bfloat16)
+        lens.append(e.shape[0])
+    doclens = torch.tensor(lens, dtype=torch.int32, device=device)
+    return tokens, doclens
+
+
+class ColbertIndex:
+    """One shard of the corpus resident in HBM, with a C handle borrowing it."""
+
+    def __init__(self, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0):
+        _require_cuda(tokens, "tokens")
+        _require_cuda(doclens, "doclens")
+        if tokens.dtype != torch.bfloat16 or tokens.dim() != 3 or tuple(tokens.shape[1:]) != (LD, DIM):
+            raise ValueError(f"tokens must be bf16 [n, {LD}, {DIM}] (got {tokens.dtype} {tuple(tokens.shape)})")
+        if doclens.dtype != torch.int32 or doclens.shape != (tokens.shape[0],):
+            raise ValueError("doclens must be int32 [n]")
+        self.tokens = tokens.contiguous()
+        self.doclens = doclens.contiguous()
+        self.device = tokens.device
+        self.n = int(tokens.shape[0])
+        self.id_base = int(id_base)
+        self.means: Optional[torch.Tensor] = None
+        self._ws: Optional[torch.Tensor] = None
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().cbv2_index_create(
+            self.device.index if self.device.index is not None else torch.cuda.current_device(),
+            self.tokens.data_ptr(), _lib.DTYPE_BF16, self.n, LD, DIM, self.doclens.data_ptr(),
+            self.id_base, ctypes.byref(h)))
+        self._h = h
+
+    @classmethod
+    def from_embeddings(cls, embs, device="cuda", id_base: int = 0, build_means: bool = False):
+        device = torch.device(device)
+        tokens, doclens = pack_tokens(embs, device)
+        ix = cls(tokens, doclens, id_base=id_base)
+        if build_means:
+            if isinstance(embs, torch.Tensor):
+                f32 = embs if embs.dim() == 3 else embs.unsqueeze(1)
+                f32 = f32.to(device=device, dtype=torch.float32).contiguous()
+            else:
+                f32 = torch.zeros((ix.n, LD, DIM), dtype=torch.float32, device=device)
+                for i, e in enumerate(embs):
+                    e = e if e.dim() == 2 else e.unsqueeze(0)
+                    f32[i, : e.shape[0]] = e.to(device=device, dtype=torch.float32)
+            ix.build_means(f32)
+        return ix
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().cbv2_index_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.n
+
+    # ----------------------------------------------------------------- build
+    def build_means(self, tokens_f32: torch.Tensor):
+        """Per-doc normalised token means for the literal reference scorer."""
+        _require_cuda(tokens_f32, "tokens_f32")
+        if tokens_f32.dtype != torch.float32 or tokens_f32.dim() != 3 or tokens_f32.shape[0] != self.n \
+                or tokens_f32.shape[2] != DIM:
+            raise ValueError(f"tokens_f32 must be f32 [n, L, {DIM}]")
+        tokens_f32 = tokens_f32.contiguous()
+        means = torch.empty((self.n, DIM), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().cbv2_index_build_means(self._h, tokens_f32.data_ptr(), tokens_f32.shape[1],
+                                                     means.data_ptr(), _stream_ptr(self.device)))
+        self.means = means
+        self._means_src = tokens_f32  # kept alive until the kernel has run
+        torch.cuda.current_stream(self.device).synchronize()
+        self._means_src = None
+
+    # ----------------------------------------------------------------- query prep
+    def _prep_query(self, Q: torch.Tensor, scorer: str) -> Tuple[torch.Tensor, int]:
+        if Q.dim() == 2:
+            Q = Q.unsqueeze(0)
+        if Q.dim() != 3 or Q.shape[2] != DIM:
+            raise ValueError(f"queries must be [B, lq, {DIM}] (got {tuple(Q.shape)})")
+        Q = Q.to(self.device)
+        if scorer == "maxsim":
+            return Q.to(torch.bfloat16).contiguous(), _lib.DTYPE_BF16
+        return Q.to(torch.float32).contiguous(), _lib.DTYPE_F32
+
+    def _scorer(self, scorer: str) -> int:
+        try:
+            return _lib.SCORERS[scorer]
+        except KeyError:
+            raise ValueError(f"unknown scorer {scorer!r}; expected one of {sorted(_lib.SCORERS)}") from None
+
+    # ----------------------------------------------------------------- compute
+    def score(self, Q: torch.Tensor, scorer: str = "maxsim") -> torch.Tensor:
+        """f32 [B, n] scores of every doc of the shard (the reference's _maxsim_score)."""
+        sid = self._scorer(scorer)
+        Qd, qdt = self._prep_query(Q, scorer)
+        B, lq = int(Qd.shape[0]), int(Qd.shape[1])
+        out = torch.empty((B, max(self.n, 1)), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().cbv2_score(self._h, sid, Qd.data_ptr(), qdt, B, lq, out.data_ptr(),
+                                         out.shape[1], _stream_ptr(self.device)))
+        return out[:, : self.n]
+
+    def search(self, Q: torch.Tensor, k: int, scorer: str = "maxsim") -> Tuple[torch.Tensor, torch.Tensor]:
+        """Top-k over the shard: (f32 [B, k] scores, int32 [B, k] global ids), -inf/-1 padded."""
+        sid = self._scorer(scorer)
+        Qd, qdt = self._prep_query(Q, scorer)
+        B, lq = int(Qd.shape[0]), int(Qd.shape[1])
+        L = _lib.lib()
+        need = int(L.cbv2_search_workspace_bytes(self._h, B))
+        if self._ws is None or self._ws.numel() * 4 < need:
+            self._ws = torch.empty(((need + 3) // 4,), dtype=torch.float32, device=self.device)
+        out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+        out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        _lib.check(L.cbv2_search(self._h, sid, Qd.data_ptr(), qdt, B, lq, int(k), self._ws.data_ptr(),
+                                 self._ws.numel() * 4, out_s.data_ptr(), out_i.data_ptr(),
+                                 _stream_ptr(self.device)))
+        return out_s, out_i
+
+    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+        """Gather candidates by global id and MaxSim-rank them.
+
+        k > 0: (scores [B, k], ids [B, k], positions [B, k]); k == 0: raw scores [B, C].
+        """
+        Qd, _ = self._prep_query(Q, "maxsim")
+        cand = cand.to(device=self.device, dtype=torch.int32).contiguous()
+        if cand.dim() == 1:
+            cand = cand.unsqueeze(0)
+        B, C = int(cand.shape[0]), int(cand.shape[1])
+        if Qd.shape[0] != B:
+            raise ValueError(f"{Qd.shape[0]} queries but {B} candidate rows")
+        if k == 0:
+            out_s = torch.empty((B, C), dtype=torch.float32, device=self.device)
+            _lib.check(_lib.lib().cbv2_rerank(self._h, Qd.data_ptr(), B, int(Qd.shape[1]), cand.data_ptr(), C, 0,
+                                              out_s.data_ptr(), None, None, _stream_ptr(self.device)))
+            return out_s
+        out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+        out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        out_p = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        _lib.check(_lib.lib().cbv2_rerank(self._h, Qd.data_ptr(), B, int(Qd.shape[1]), cand.data_ptr(), C, int(k),
+                                          out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(),
+                                          _stream_ptr(self.device)))
+        return out_s, out_i, out_p
+
+
+# --------------------------------------------------------------------- free functions
+def select_topk(scores: torch.Tensor, k: int, ids: Optional[torch.Tensor] = None):
+    """Top-k of each row of a short [B, C] matrix (C <= 1024); ties -> lower position."""
+    _require_cuda(scores, "scores")
+    scores = scores.to(torch.float32).contiguous()
+    if scores.dim() == 1:
+        scores = scores.unsqueeze(0)
+    B, C = scores.shape
+    dev = scores.device
+    if ids is not None:
+        ids = ids.to(device=dev, dtype=torch.int32).contiguous()
+    out_s = torch.empty((B, k), dtype=torch.float32, device=dev)
+    out_i = torch.empty((B, k), dtype=torch.int32, device=dev)
+    out_p = torch.empty((B, k), dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().cbv2_select_topk(scores.data_ptr(), ids.data_ptr() if ids is not None else None, B, C,
+                                           int(k), out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(),
+                                           _stream_ptr(dev)))
+    return out_s, out_i, out_p
+
+
+def topk_rows(scores: torch.Tensor, k: int, id_base: int = 0):
+    """Top-k of each row of a [B, n] score matrix (exact; ties -> lower index)."""
+    _require_cuda(scores, "scores")
+    if scores.dim() == 1:
+        scores = scores.unsqueeze(0)
+    scores = scores.to(torch.float32)
+    if scores.stride(1) != 1:
+        scores = scores.contiguous()
+    B, n = scores.shape
+    dev = scores.device
+    out_s = torch.empty((B, k), dtype=torch.float32, device=dev)
+    out_i = torch.empty((B, k), dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().cbv2_topk_rows(scores.data_ptr(), B, n, scores.stride(0), int(k), int(id_base),
+                                         out_s.data_ptr(), out_i.data_ptr(), _stream_ptr(dev)))
+    return out_s, out_i
+
+
+def merge_topk(scores: torch.Tensor, ids: torch.Tensor, k: int):
+    """Merge [G, B, k] sorted per-shard lists into the global [B, k]."""
+    _require_cuda(scores, "scores")
+    scores = scores.to(torch.float32).contiguous()
+    ids = ids.to(device=scores.device, dtype=torch.int32).contiguous()
+    G, B, kk = scores.shape
+    if kk != k:
+        raise ValueError("per-shard lists must have length k")
+    out_s = torch.empty((B, k), dtype=torch.float32, device=scores.device)
+    out_i = torch.empty((B, k), dtype=torch.int32, device=scores.device)
+    _lib.check(_lib.lib().cbv2_merge_topk(scores.data_ptr(), ids.data_ptr(), G, B, int(k), out_s.data_ptr(),
+                                          out_i.data_ptr(), _stream_ptr(scores.device)))
+    return out_s, out_i

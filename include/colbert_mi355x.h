@@ -1,0 +1,147 @@
+/*
+ * colbert_mi355x.h — C ABI of libcolbert_mi355x.so, the MI355X (gfx950) ColBERT
+ * late-interaction scoring path.
+ *
+ * The reference (techmum21p/hybrid-rag-ColBERTv2) has no FFI: its seam is the
+ * Python object `DualIndexer.colbert_retriever` (local_rag_complete.py:844)
+ * called as `.search(query=, k=)` (:954) and `.rerank(query=, documents=, k=)`
+ * (:999).  Each entry point below replaces one piece of arithmetic behind that
+ * seam; the Python package (hybrid-rag-colbertv2_amd/) binds them with ctypes
+ * and keeps the reference's method names and result dicts.
+ *
+ * Conventions
+ *  - Every pointer argument except `cbv2_index*` is a DEVICE pointer owned by
+ *    the caller (torch tensors in the Python layer), except in the host-only
+ *    helper cbv2_rrf_fuse, which takes HOST pointers.  Nothing is allocated or
+ *    freed inside a compute call, so calls are hipGraph-capturable.
+ *  - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy default
+ *    stream).  One index handle belongs to one device.
+ *  - Return 0 on success, a negative CBV2_E* code on error; the message is in
+ *    the thread-local `cbv2_last_error()`.  Arguments are validated on the host
+ *    BEFORE any launch: a call that returns an error has launched nothing.
+ *  - Ranking ties are broken deterministically: score descending, then the
+ *    lower index in the scored list (doc id for search, candidate position for
+ *    rerank).  The reference's torch.topk / argsort (local_rag_complete.py:767,
+ *    :789) leave tie order unspecified; this is the defined refinement.
+ *
+ * Index layout in HBM (see DESIGN.md "Data layout"):
+ *    tokens   bf16 [n][ld = 128][d = 128], row-major, 16-byte aligned;
+ *             rows t >= doclens[i] of doc i are padding and never score.
+ *    doclens  int32 [n], 0 <= doclens[i] <= 128.
+ *    Local doc i has global id  id_base + i  (contiguous shard of the corpus).
+ */
+#ifndef COLBERT_MI355X_H
+#define COLBERT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBV2_ABI_VERSION 1
+
+/* dtypes */
+#define CBV2_DTYPE_BF16 1
+#define CBV2_DTYPE_F32 2
+
+/* scorers */
+#define CBV2_SCORER_MAXSIM 0              /* sum_i max_j <q_i, d_j>            */
+#define CBV2_SCORER_REF_MEANPOOL_COSINE 1 /* cos(mean_i q_i, mean_j d_j)       */
+
+/* error codes */
+#define CBV2_OK 0
+#define CBV2_EINVAL -1       /* bad argument (shape, null pointer, range)       */
+#define CBV2_EUNSUPPORTED -2 /* valid but not built (e.g. ld != 128)             */
+#define CBV2_EHIP -3         /* a HIP runtime call failed                        */
+#define CBV2_ESTATE -4       /* handle not ready (e.g. meanpool means not built) */
+
+typedef struct cbv2_index cbv2_index;
+
+/* Library / error reporting ------------------------------------------------ */
+int cbv2_abi_version(void);
+const char* cbv2_last_error(void);
+
+/* Index handle --------------------------------------------------------------
+ * Replaces the tensor the reference keeps in `self.corpus_embeddings`
+ * (local_rag_complete.py:735-739 index(), :751-752 load()).  The handle
+ * BORROWS `tokens`, `doclens` (and later `doc_means`): the caller keeps them
+ * alive until cbv2_index_destroy.  `device` is the HIP device ordinal.      */
+int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, int32_t ld,
+                      int32_t d, const int32_t* doclens, int64_t id_base, cbv2_index** out);
+int cbv2_index_destroy(cbv2_index* index);
+
+/* Literal-reference scorer support: build the L2-normalised per-doc token means
+ * the reference recomputes on every call (local_rag_complete.py:822,825-829)
+ * ONCE, from the fp32 encoder output `tokens_f32` [n][ld_src][d].
+ * `doc_means` is a caller-owned f32 [n][d] buffer the handle borrows.        */
+int cbv2_index_build_means(cbv2_index* index, const float* tokens_f32, int32_t ld_src,
+                           float* doc_means, void* stream);
+
+/* Scoring -------------------------------------------------------------------
+ * cbv2_score — JinaColBERTRetriever._maxsim_score (local_rag_complete.py:802-831)
+ * for a batch of B queries against every doc of the index:
+ *    out[b * ld_out + i] = score(Q[b], doc i)     (i = local index)
+ *  scorer MAXSIM:              Q bf16 [B][lq][128], 1 <= lq <= 32.
+ *  scorer REF_MEANPOOL_COSINE: Q f32  [B][lq][128], any lq >= 1 (means must
+ *                              be built).                                    */
+int cbv2_score(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B,
+               int32_t lq, float* out, int64_t ld_out, void* stream);
+
+/* cbv2_search — JinaColBERTRetriever.search (local_rag_complete.py:755-777):
+ * score every doc, then top-k (torch.topk at :767) with the deterministic tie
+ * rule.  Writes out_scores f32 [B][k] and out_ids int32 [B][k] (GLOBAL ids =
+ * id_base + local index), best first; slots past min(k, n) hold -inf / -1.
+ * `workspace` must hold cbv2_search_workspace_bytes(index, B) bytes.        */
+size_t cbv2_search_workspace_bytes(const cbv2_index* index, int32_t B);
+int cbv2_search(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B,
+                int32_t lq, int32_t k, void* workspace, size_t workspace_bytes,
+                float* out_scores, int32_t* out_ids, void* stream);
+
+/* cbv2_rerank — JinaColBERTRetriever.rerank (local_rag_complete.py:779-800)
+ * without re-encoding: the C candidate docs of each query are GATHERED from
+ * the HBM index by global id (cand int32 [B][C]; ids outside this shard or < 0
+ * score -inf) and MaxSim-scored against Q (bf16 [B][lq][128]).
+ *  k > 0:  out_scores [B][k], out_ids [B][k] (global ids), out_pos [B][k]
+ *          (candidate position = the reference's `result_index`), best first.
+ *  k == 0: out_scores [B][C] receives the raw candidate scores (for the
+ *          sharded path: all-reduce(max) across shards, then cbv2_select_topk). */
+int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const int32_t* cand,
+                int32_t C, int32_t k, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                void* stream);
+
+/* Selection -----------------------------------------------------------------
+ * cbv2_select_topk — top-k of each row of a small score matrix (rows of
+ * C <= 1024 entries: rerank after the cross-shard all-reduce).  ids (nullable)
+ * [B][C] maps positions to doc ids (NULL: id = position).  Ties: lower
+ * position first.  out_pos (nullable) receives positions.                   */
+int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t C, int32_t k,
+                     float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
+
+/* cbv2_topk_rows — top-k of each row of a large score matrix scores[b*ld + i],
+ * i < n (radix select, then bitonic sort).  ids written = id_base + i.      */
+int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k,
+                   int64_t id_base, float* out_scores, int32_t* out_ids, void* stream);
+
+/* cbv2_merge_topk — merge G per-shard sorted top-k lists ([G][B][k] scores and
+ * global ids, e.g. after an RCCL all-gather) into the global top-k [B][k].
+ * Entries with id < 0 are padding.                                          */
+int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B,
+                    int32_t k, float* out_scores, int32_t* out_ids, void* stream);
+
+/* Host fusion (HOST pointers, no GPU) --------------------------------------
+ * cbv2_rrf_fuse — HybridRetriever._reciprocal_rank_fusion
+ * (local_rag_complete.py:960-978) for B queries at once, followed by the
+ * `[:50]` cut of :916 (C = 50): float64 1/(rrf_k + rank) sums in the
+ * reference's order and a stable sort, so results and tie order are identical
+ * to the Python.  bm25_ids [B][kb], colbert_ids [B][kc] (ids < 0 = padding);
+ * out_ids [B][C] (-1 padded), out_scores [B][C] (nullable), out_count [B]
+ * (nullable) = distinct ids per query.                                     */
+int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_ids, int32_t kc, int32_t B,
+                  int32_t rrf_k, int32_t C, int32_t* out_ids, double* out_scores, int32_t* out_count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COLBERT_MI355X_H */

@@ -1,0 +1,219 @@
+"""CPU ORACLE for the ColBERT retrieval hot path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / the timed CPU baseline.  The product
+(hybrid-rag-colbertv2_amd/) never calls it: it has no CPU fallback.
+
+Each function restates the reference's arithmetic in numpy, citing the
+reference line it follows (LRC = /root/reference/local_rag_complete.py):
+
+  meanpool_cosine   LRC:814-831  _maxsim_score as written (mean-pool + cosine,
+                                 torch's x/max(||x||,eps) form of cosine_similarity)
+  maxsim            the north-star contract the reference's docstring describes
+                    (LRC:807-812): S = sum_q max_t <q, d_t>, padded rows excluded
+  topk              LRC:767 torch.topk, with the tie rule made explicit:
+                    score desc, then lower index
+  rerank_select     LRC:789-798 argsort(desc)[:k] + 1-based rank, same tie rule
+  rrf               LRC:960-978 reciprocal rank fusion, float64, stable sort
+  merge_topk        cross-shard merge (no reference counterpart; exact by the
+                    same tie rule)
+
+Pinning: meanpool_cosine, rrf and the search/rerank
+dict pipeline are checked against golden vectors produced by the reference's
+own functions (tests/golden/gen_golden.py, AST-extracted from LRC).  maxsim is
+pinned (a) at one doc token, where the reference's ranking equals MaxSim's
+(tests/golden/single_token.npz), and (b) by exact-rational known answers on
+the k/16 grid (tests/golden/exact_grid.npz).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ------------------------------------------------------------------ bf16 helpers
+def to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """float32 -> bf16 bit patterns, round-to-nearest-even (torch's .to(bfloat16))."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return r.astype(np.uint16)
+
+
+def from_bf16_bits(b: np.ndarray) -> np.ndarray:
+    return (np.asarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def bf16_round(x: np.ndarray) -> np.ndarray:
+    return from_bf16_bits(to_bf16_bits(x))
+
+
+# ------------------------------------------------------------------ scorers
+def maxsim(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray | None = None) -> np.ndarray:
+    """True MaxSim, float64: Q [B, lq, D], docs [N, L, D] -> [B, N].
+
+    Rows t >= doclens[n] never score; an empty doc scores -inf.
+    """
+    Q = np.asarray(Q, dtype=np.float64)
+    if Q.ndim == 2:
+        Q = Q[None]
+    docs = np.asarray(docs, dtype=np.float64)
+    N, L, _ = docs.shape
+    if doclens is None:
+        doclens = np.full(N, L, np.int64)
+    valid = np.arange(L)[None, :] < np.asarray(doclens)[:, None]            # [N, L]
+    out = np.empty((Q.shape[0], N), np.float64)
+    for b in range(Q.shape[0]):
+        sim = np.einsum("nld,qd->nlq", docs, Q[b], optimize=True)           # [N, L, lq]
+        sim = np.where(valid[:, :, None], sim, -np.inf)
+        out[b] = sim.max(axis=1).sum(axis=1)
+    return out
+
+
+def meanpool_cosine(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray | None = None,
+                    eps: float = 1e-8) -> np.ndarray:
+    """LRC:814-831: cosine(mean_t q_t, mean_t d_t) -> [B, N] (float64).
+
+    The reference averages every stored row; with doclens, the first doclens[n]
+    rows are the stored rows.  Cosine as torch computes it: each vector divided
+    by max(||v||, eps), then the sum of products.
+    """
+    Q = np.asarray(Q, dtype=np.float64)
+    if Q.ndim == 2:
+        Q = Q[None]
+    docs = np.asarray(docs, dtype=np.float64)
+    N, L, _ = docs.shape
+    if doclens is None:
+        doclens = np.full(N, L, np.int64)
+    doclens = np.asarray(doclens)
+    valid = (np.arange(L)[None, :] < doclens[:, None]).astype(np.float64)
+    dsum = np.einsum("nld,nl->nd", docs, valid)
+    dmean = dsum / np.maximum(doclens, 1)[:, None]
+    dmean[doclens == 0] = 0.0
+    qmean = Q.mean(axis=1)
+    dn = dmean / np.maximum(np.linalg.norm(dmean, axis=1, keepdims=True), eps)
+    qn = qmean / np.maximum(np.linalg.norm(qmean, axis=1, keepdims=True), eps)
+    return qn @ dn.T
+
+
+# ------------------------------------------------------------------ selection
+def topk(scores: np.ndarray, k: int, id_base: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """LRC:767 with ties -> lower index.  [B, N] -> (scores [B, k], ids [B, k]); pads -inf / -1."""
+    s = np.atleast_2d(np.asarray(scores))
+    B, N = s.shape
+    kk = min(k, N)
+    out_s = np.full((B, k), -np.inf, np.float64)
+    out_i = np.full((B, k), -1, np.int64)
+    idx = np.arange(N)
+    for b in range(B):
+        order = np.lexsort((idx, -s[b].astype(np.float64)))[:kk]
+        out_s[b, :kk] = s[b, order]
+        out_i[b, :kk] = order + id_base
+    return out_s, out_i
+
+
+def rerank_select(scores: np.ndarray, k: int):
+    """LRC:789-798: positions sorted by score desc (ties: lower position), [:k], 1-based ranks."""
+    s = np.asarray(scores, dtype=np.float64)
+    order = np.lexsort((np.arange(len(s)), -s))[:k]
+    return [(int(p), float(s[p]), r + 1) for r, p in enumerate(order)]
+
+
+def rerank(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray, cand: np.ndarray, k: int, id_base: int = 0):
+    """MaxSim of each query's candidate ids (global), then top-k by (score desc, position asc).
+
+    Returns (scores [B, k], ids [B, k], positions [B, k]); out-of-shard / negative ids score -inf.
+    """
+    Q = np.asarray(Q, np.float64)
+    cand = np.atleast_2d(np.asarray(cand, np.int64))
+    B, C = cand.shape
+    N = docs.shape[0]
+    out_s = np.full((B, k), -np.inf)
+    out_i = np.full((B, k), -1, np.int64)
+    out_p = np.full((B, k), -1, np.int64)
+    for b in range(B):
+        sc = np.full(C, -np.inf)
+        for c in range(C):
+            loc = cand[b, c] - id_base
+            if cand[b, c] >= 0 and 0 <= loc < N:
+                sc[c] = maxsim(Q[b:b + 1], docs[loc:loc + 1], doclens[loc:loc + 1])[0, 0]
+        order = np.lexsort((np.arange(C), -sc))[:k]
+        m = len(order)
+        out_s[b, :m] = sc[order]
+        out_i[b, :m] = cand[b, order]
+        out_p[b, :m] = order
+    return out_s, out_i, out_p
+
+
+def merge_topk(scores: np.ndarray, ids: np.ndarray, k: int):
+    """[G, B, k] per-shard lists -> global [B, k]; padding ids < 0 ignored."""
+    G, B, _ = scores.shape
+    out_s = np.full((B, k), -np.inf)
+    out_i = np.full((B, k), -1, np.int64)
+    for b in range(B):
+        s = scores[:, b].reshape(-1).astype(np.float64)
+        i = ids[:, b].reshape(-1).astype(np.int64)
+        keep = i >= 0
+        s, i = s[keep], i[keep]
+        order = np.lexsort((i, -s))[:k]
+        out_s[b, :len(order)] = s[order]
+        out_i[b, :len(order)] = i[order]
+    return out_s, out_i
+
+
+# ------------------------------------------------------------------ fusion
+def rrf(bm25_ids: Sequence[int], colbert_ids: Sequence[int], k: int = 60) -> List[Tuple[int, float]]:
+    """LRC:960-978: score[id] += 1/(k + rank) over the BM25 list, then the ColBERT
+    list (rank 1-based); Python float64; sorted(..., reverse=True) is stable, so
+    equal scores keep first-insertion order."""
+    scores = {}
+    for rank, cid in enumerate(bm25_ids, 1):
+        scores[cid] = scores.get(cid, 0) + (1 / (k + rank))
+    for rank, cid in enumerate(colbert_ids, 1):
+        scores[cid] = scores.get(cid, 0) + (1 / (k + rank))
+    return sorted(scores.items(), key=lambda x: x[1], reverse=True)
+
+
+# ------------------------------------------------------------------ C restatement
+_CLIB = None
+C_LIB_PATH = os.path.join(HERE, "_build", "libcbv2_oracle.so")
+
+
+def c_lib():
+    """ctypes handle to oracle/cbv2_oracle.c (built by __graft_entry__.build())."""
+    global _CLIB
+    if _CLIB is None:
+        if not os.path.exists(C_LIB_PATH):
+            raise RuntimeError(f"{C_LIB_PATH} missing: build it with `make -C oracle`")
+        L = ctypes.CDLL(C_LIB_PATH)
+        L.oracle_maxsim_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_topk.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        _CLIB = L
+    return _CLIB
+
+
+def c_maxsim_bf16(q_bits: np.ndarray, doc_bits: np.ndarray, doclens: np.ndarray) -> np.ndarray:
+    """C restatement of maxsim on bf16 bit patterns: q [B, lq, 128], docs [N, L, 128] -> f64 [B, N]."""
+    q_bits = np.ascontiguousarray(q_bits, np.uint16)
+    doc_bits = np.ascontiguousarray(doc_bits, np.uint16)
+    doclens = np.ascontiguousarray(doclens, np.int32)
+    B, lq, D = q_bits.shape
+    N, L, _ = doc_bits.shape
+    assert D == 128
+    out = np.empty((B, N), np.float64)
+    c_lib().oracle_maxsim_bf16(q_bits.ctypes.data, B, lq, doc_bits.ctypes.data, doclens.ctypes.data, N, L,
+                               out.ctypes.data)
+    return out
+
+
+def c_topk(scores_row: np.ndarray, k: int) -> np.ndarray:
+    s = np.ascontiguousarray(scores_row, np.float64)
+    ids = np.empty(k, np.int64)
+    vals = np.empty(k, np.float64)
+    c_lib().oracle_topk(s.ctypes.data, len(s), k, vals.ctypes.data, ids.ctypes.data)
+    return ids
