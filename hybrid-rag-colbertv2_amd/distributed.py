@@ -1,0 +1,83 @@
+"""Multi-GPU path: the corpus sharded by contiguous id range, one process per GPU.
+
+No reference counterpart (the reference is single-process); this
+is the §8(e) design:
+
+  stage 2  every rank scans its shard (HIP scan + top-k) -> [B, k] (score,
+           global id) -> ONE all-gather over RCCL/xGMI of the packed pairs
+           [G, B, k, 2] -> HIP merge with the (score desc, id asc) rule.
+           Every rank ends with the identical global top-k.
+  stage 3  every rank scores the candidates it owns (-inf for the rest) ->
+           all-reduce(MAX) over [B, C] -> HIP top-k select.  Each id is owned by
+           exactly one shard, so MAX picks the owner's score.
+
+Messages are tiny (B=256, k=100: 200 KiB per rank), so the exchange is
+latency-bound; it is one collective per stage.  torch.distributed's "nccl"
+backend IS RCCL on ROCm.  The same code runs on "gloo" for CPU tests, where
+the caller injects CPU ``local``/``ops`` objects (tests only).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [begin, end) of global ids owned by ``rank`` (sizes differ by <= 1)."""
+    base, rem = divmod(n_total, world)
+    begin = rank * base + min(rank, rem)
+    return begin, begin + base + (1 if rank < rem else 0)
+
+
+class _DeviceOps:
+    """HIP merge / select (libcolbert_mi355x.so)."""
+
+    @staticmethod
+    def merge(S: torch.Tensor, I: torch.Tensor, k: int):
+        from .index import merge_topk
+        return merge_topk(S, I, k)
+
+    @staticmethod
+    def select(scores: torch.Tensor, k: int, ids: torch.Tensor):
+        from .index import select_topk
+        return select_topk(scores, k, ids=ids)
+
+
+class ShardedSearcher:
+    """Global search / rerank over a corpus whose shards live on the ranks of ``group``.
+
+    ``local`` is this rank's shard (a ``ColbertIndex``: ``search(Q, k)`` and
+    ``rerank(Q, cand, 0)``); ``ops`` provides ``merge`` and ``select``.
+    """
+
+    def __init__(self, local, group: Optional[dist.ProcessGroup] = None, ops=None):
+        self.local = local
+        self.group = group
+        self.ops = ops if ops is not None else _DeviceOps()
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        else:
+            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
+        return out
+
+    def search(self, Q: torch.Tensor, k: int):
+        s, i = self.local.search(Q, k)
+        if self.world == 1:
+            return s, i
+        packed = torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1)  # [B, k, 2]
+        allp = self._all_gather(packed)                                                    # [G, B, k, 2]
+        S = allp[..., 0].contiguous().view(torch.float32)
+        I = allp[..., 1].contiguous()
+        return self.ops.merge(S, I, k)
+
+    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+        raw = self.local.rerank(Q, cand, 0)                                                # [B, C]
+        if self.world > 1:
+            dist.all_reduce(raw, op=dist.ReduceOp.MAX, group=self.group)
+        return self.ops.select(raw, k, ids=cand)

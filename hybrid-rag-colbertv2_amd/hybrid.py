@@ -1,0 +1,249 @@
+"""DualIndexer and HybridRetriever — drop-in for local_rag_complete.py:838-1014.
+
+The three-stage flow is the reference's (LRC:894-935): host BM25 top-100,
+ColBERT top-100 (HIP scan + top-k), reciprocal rank fusion (host, exact
+float64 semantics), ``[:50]`` candidates, ColBERT rerank top-10.  The result
+dicts are the reference's (LRC:1004-1013).
+
+MI355X changes:
+  * ``_fetch_chunks_from_db`` reads a ``ChunkStore`` (id -> chunk dict) with
+    ids equal to index positions; the reference's SQLite lookup treats
+    0-based index positions as 1-based primary keys (LRC:984).
+  * ``_colbert_rerank`` gathers the candidates' precomputed token tiles from
+    HBM by id (``rerank_ids``) instead of re-encoding their texts, and reuses
+    the stage-2 query embedding (the reference encodes the query twice).
+  * ``retrieve_batch`` runs the same three stages for a batch of query
+    embeddings with one device round trip per stage.
+LRC = local_rag_complete.py
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .bm25 import HostBM25
+from .config import RAGConfig
+from .retriever import JinaColBERTRetriever
+
+
+# ---------------------------------------------------------------------- fusion
+def rrf_fuse(bm25_ids: np.ndarray, colbert_ids: np.ndarray, rrf_k: int = 60, C: int = 50,
+             return_scores: bool = False):
+    """Batched LRC:960-978 + ``[:C]`` (LRC:916) in native host code.
+
+    bm25_ids [B, kb], colbert_ids [B, kc] int (negative = padding) ->
+    fused ids [B, C] int32 (-1 padded) [, float64 scores [B, C], counts [B]].
+    """
+    bm = np.ascontiguousarray(np.atleast_2d(bm25_ids), dtype=np.int32)
+    cb = np.ascontiguousarray(np.atleast_2d(colbert_ids), dtype=np.int32)
+    B = max(bm.shape[0], cb.shape[0])
+    if bm.shape[0] != B:
+        bm = np.ascontiguousarray(np.broadcast_to(bm, (B, bm.shape[1])))
+    if cb.shape[0] != B:
+        cb = np.ascontiguousarray(np.broadcast_to(cb, (B, cb.shape[1])))
+    out = np.empty((B, C), np.int32)
+    sc = np.empty((B, C), np.float64)
+    cnt = np.empty(B, np.int32)
+    _lib.check(_lib.lib().cbv2_rrf_fuse(bm.ctypes.data if bm.size else None, bm.shape[1],
+                                        cb.ctypes.data if cb.size else None, cb.shape[1], B, int(rrf_k), C,
+                                        out.ctypes.data, sc.ctypes.data, cnt.ctypes.data))
+    return (out, sc, cnt) if return_scores else out
+
+
+# ---------------------------------------------------------------------- chunk store
+class ChunkStore:
+    """In-memory id -> chunk table (replaces the SQLAlchemy ``Chunk`` lookups, LRC:980-994)."""
+
+    def __init__(self, chunks: Optional[Sequence[Dict]] = None):
+        self._rows = {}
+        for i, c in enumerate(chunks or []):
+            self.add(c.get("chunk_id", c.get("id", i)), c)
+
+    def add(self, chunk_id: int, chunk: Dict) -> None:
+        self._rows[int(chunk_id)] = {
+            "chunk_id": int(chunk_id),
+            "text": chunk.get("text", ""),
+            "document_id": chunk.get("document_id"),
+            "heading_path": chunk.get("heading_path", ""),
+            "has_images": chunk.get("has_images", False),
+            "metadata": chunk.get("metadata") or {},
+        }
+
+    @classmethod
+    def from_corpus(cls, corpus: Sequence[str]) -> "ChunkStore":
+        return cls([{"chunk_id": i, "text": t} for i, t in enumerate(corpus)])
+
+    def get(self, chunk_id: int) -> Optional[Dict]:
+        return self._rows.get(int(chunk_id))
+
+    def __len__(self):
+        return len(self._rows)
+
+
+# ---------------------------------------------------------------------- indexer
+class DualIndexer:
+    """LRC:838-879: holds the BM25 and ColBERT retrievers (the drop-in seam)."""
+
+    def __init__(self, config: RAGConfig, encoder=None):
+        self.config = config
+        self.bm25_retriever: Optional[HostBM25] = None
+        self.colbert_retriever = JinaColBERTRetriever(config, encoder=encoder)
+
+    def build_bm25_index(self, corpus: List[str]) -> None:
+        print("\n[BM25s] Building lexical search index...", end=" ")
+        start = time.time()
+        self.bm25_retriever = HostBM25()
+        self.bm25_retriever.index(self.bm25_retriever.tokenize(corpus))
+        self.bm25_retriever.save(self.config.bm25_index_path)
+        print(f"✓ {time.time() - start:.2f}s")
+
+    def build_colbert_index(self, corpus: List[str]) -> None:
+        print("\n[ColBERT] Building semantic search index...")
+        start = time.time()
+        self.colbert_retriever.index(corpus)
+        print(f"  ✓ {time.time() - start:.2f}s")
+
+    def load_indexes(self) -> None:
+        self.bm25_retriever = HostBM25.load(self.config.bm25_index_path)
+        self.colbert_retriever.load()
+
+
+# ---------------------------------------------------------------------- hybrid
+class HybridRetriever:
+    """Three-stage retrieval: BM25 + ColBERT + ColBERT reranking (LRC:886-1014)."""
+
+    def __init__(self, config: RAGConfig, indexer: DualIndexer, db_session=None, verbose: bool = True):
+        self.config = config
+        self.indexer = indexer
+        self.db_session = db_session
+        self.verbose = verbose
+
+    def _log(self, msg: str):
+        if self.verbose:
+            print(msg)
+
+    def retrieve(self, query: str, top_k_final: int = None) -> List[Dict]:
+        """LRC:894-935, same stages, cut-offs and per-stage timing prints."""
+        if top_k_final is None:
+            top_k_final = self.config.final_top_k
+        self._log("\n🔍 Retrieving relevant chunks...")
+
+        start = time.time()
+        bm25_results = self._bm25_search(query, k=self.config.bm25_top_k)
+        bm25_time = time.time() - start
+        self._log(f"   • BM25s: {bm25_time:.3f}s")
+
+        start = time.time()
+        q_emb = self.indexer.colbert_retriever._encode_query(query)
+        colbert_results = self._colbert_search(q_emb, k=self.config.colbert_top_k)
+        colbert_time = time.time() - start
+        self._log(f"   • ColBERT: {colbert_time:.3f}s")
+
+        start = time.time()
+        fused_results = self._reciprocal_rank_fusion(bm25_results, colbert_results, k=self.config.rrf_k)
+        candidates = fused_results[: self.config.fused_candidates]
+        fusion_time = time.time() - start
+        self._log(f"   • Fusion: {fusion_time:.3f}s")
+
+        start = time.time()
+        candidate_chunks = self._fetch_chunks_from_db([r["chunk_id"] for r in candidates])
+        fetch_time = time.time() - start
+        self._log(f"   • Fetch: {fetch_time:.3f}s")
+
+        start = time.time()
+        reranked_results = self._colbert_rerank(q_emb, candidate_chunks, top_k=top_k_final)
+        rerank_time = time.time() - start
+        self._log(f"   • Rerank: {rerank_time:.3f}s")
+
+        total = bm25_time + colbert_time + fusion_time + fetch_time + rerank_time
+        self._log(f"   ✓ Total retrieval: {total:.3f}s")
+        return reranked_results
+
+    def _bm25_search(self, query: str, k: int) -> List[Dict]:
+        """LRC:937-950 against the host BM25."""
+        bm = self.indexer.bm25_retriever
+        if bm is None:
+            return []
+        results, scores = bm.retrieve(bm.tokenize(query), k=k)
+        return [{"chunk_id": int(results[0][i]), "score": float(scores[0][i]), "source": "bm25"}
+                for i in range(len(results[0])) if results[0][i] >= 0]
+
+    def _colbert_search(self, query, k: int) -> List[Dict]:
+        """LRC:952-958."""
+        results = self.indexer.colbert_retriever.search(query=query, k=k)
+        return [{"chunk_id": r["document_id"], "score": r["score"], "source": "colbert"} for r in results]
+
+    def _reciprocal_rank_fusion(self, bm25_results: List[Dict], colbert_results: List[Dict],
+                                k: int = 60) -> List[Dict]:
+        """LRC:960-978 (native, same float64 arithmetic and stable tie order)."""
+        bm = np.array([[r["chunk_id"] for r in bm25_results]], np.int32).reshape(1, -1)
+        cb = np.array([[r["chunk_id"] for r in colbert_results]], np.int32).reshape(1, -1)
+        C = max(1, bm.shape[1] + cb.shape[1])
+        ids, sc, cnt = rrf_fuse(bm, cb, rrf_k=k, C=C, return_scores=True)
+        n = int(cnt[0])
+        return [{"chunk_id": int(ids[0, j]), "rrf_score": float(sc[0, j])} for j in range(n)]
+
+    def _fetch_chunks_from_db(self, chunk_ids: List[int]) -> List[Dict]:
+        """LRC:980-994 against a ChunkStore (0-based ids = index positions)."""
+        store = self.db_session
+        if store is None:
+            corpus = self.indexer.colbert_retriever.corpus or []
+            return [{"chunk_id": int(i), "text": corpus[i] if i < len(corpus) else "", "document_id": None,
+                     "heading_path": "", "has_images": False, "metadata": {}} for i in chunk_ids]
+        out = []
+        for cid in chunk_ids:
+            c = store.get(cid)
+            if c:
+                out.append(dict(c))
+        return out
+
+    def _colbert_rerank(self, query, chunks: List[Dict], top_k: int) -> List[Dict]:
+        """LRC:996-1014; scores gathered tiles by chunk id (no re-encode)."""
+        if not chunks:
+            return []
+        retr = self.indexer.colbert_retriever
+        if retr.scorer == "maxsim" and not isinstance(query, str):
+            q = query if query.dim() == 3 else query.unsqueeze(0)
+            cand = torch.tensor([[c["chunk_id"] for c in chunks]], dtype=torch.int32, device=retr.device)
+            kk = min(top_k, len(chunks))
+            scores, _, pos = retr.rerank_ids(q, cand, kk)
+            reranked = [{"result_index": int(p), "score": float(s), "rank": r + 1}
+                        for r, (s, p) in enumerate(zip(scores[0].tolist(), pos[0].tolist()))]
+        else:
+            documents = [c["text"] for c in chunks]
+            reranked = retr.rerank(query=query, documents=documents, k=top_k)
+        final = []
+        for result in reranked:
+            original = chunks[result["result_index"]]
+            final.append({
+                "chunk_id": original["chunk_id"],
+                "text": original["text"],
+                "document_id": original["document_id"],
+                "heading_path": original.get("heading_path", ""),
+                "has_images": original.get("has_images", False),
+                "metadata": original["metadata"],
+                "score": result["score"],
+                "rank": result["rank"],
+            })
+        return final
+
+    # ------------------------------------------------------------------ batched path
+    def retrieve_batch(self, Q: torch.Tensor, bm25_ids: np.ndarray, top_k_final: Optional[int] = None):
+        """All three stages for B query embeddings at once (the benchmark step).
+
+        Q [B, lq, D] device; bm25_ids [B, kb] host int (stage-1 output) ->
+        device (scores [B, k], global ids [B, k]).
+        """
+        k_final = top_k_final or self.config.final_top_k
+        retr = self.indexer.colbert_retriever
+        _, ids = retr.search_embeddings(Q, self.config.colbert_top_k)
+        ids_h = ids.cpu().numpy()
+        cand = rrf_fuse(bm25_ids, ids_h, rrf_k=self.config.rrf_k, C=self.config.fused_candidates)
+        cand_d = torch.from_numpy(cand).pin_memory().to(retr.device, non_blocking=True)
+        s, i, _ = retr.rerank_ids(Q, cand_d, k_final)
+        return s, i

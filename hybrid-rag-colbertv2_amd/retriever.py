@@ -1,0 +1,134 @@
+"""JinaColBERTRetriever — drop-in for local_rag_complete.py:715-831.
+
+Same constructor, methods and result dicts as the reference; the corpus
+embeddings live in HBM as a ``ColbertIndex`` and every score / top-k /
+rerank runs in the HIP kernels of libcolbert_mi355x.so.
+
+Differences from the reference, all deliberate:
+  * ``scorer``: "maxsim" (default) computes true ColBERT MaxSim, which the
+    reference's docstring promises (LRC:807-812) but its code does not;
+    "ref_meanpool_cosine" reproduces the code as written (LRC:821-829).
+  * Ties in top-k / argsort are broken by lower index (the reference's
+    torch.topk / argsort order is unspecified).
+  * ``search`` works for pooled ([D]) query embeddings as a one-token query;
+    the reference raises IndexError there.
+  * Added batch entry points for the MI355X path: ``search_embeddings`` and
+    ``rerank_ids`` (rerank by gathering precomputed doc tiles by id instead of
+    re-encoding 50 chunk texts per query).
+LRC = local_rag_complete.py
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence, Union
+
+import torch
+
+from .config import RAGConfig
+from .encoder import load_local_encoder
+from .index import ColbertIndex, select_topk
+
+
+class JinaColBERTRetriever:
+    """ColBERT retrieval over an HBM-resident token index (LRC:715-831)."""
+
+    def __init__(self, config: RAGConfig, encoder=None):
+        self.config = config
+        dev = config.device if str(config.device).startswith("cuda") else "cuda"
+        self.device = torch.device(dev)
+        # LRC:720-724 loads the encoder by hub name; here it must be supplied or local.
+        self.model = encoder if encoder is not None else load_local_encoder(config.embedding_model, dev)
+        self.corpus_embeddings: Optional[ColbertIndex] = None
+        self.corpus: Optional[List[str]] = None
+
+    @property
+    def scorer(self) -> str:
+        return getattr(self.config, "scorer", "maxsim")
+
+    # ------------------------------------------------------------ index / load
+    def _build(self, embeddings) -> ColbertIndex:
+        return ColbertIndex.from_embeddings(embeddings, device=self.device,
+                                            build_means=(self.scorer == "ref_meanpool_cosine"))
+
+    def index(self, corpus: List[str]) -> None:
+        """LRC:728-746: encode the corpus, keep it in HBM, save index.pt."""
+        self.corpus = corpus
+        print(f"  Encoding {len(corpus)} documents...")
+        embeddings = self.model.encode(corpus, show_progress_bar=True, convert_to_tensor=True)
+        self.corpus_embeddings = self._build(embeddings)
+        os.makedirs(self.config.colbert_index_path, exist_ok=True)
+        saved = embeddings.cpu() if isinstance(embeddings, torch.Tensor) else [e.cpu() for e in embeddings]
+        torch.save({"embeddings": saved, "corpus": corpus},
+                   os.path.join(self.config.colbert_index_path, "index.pt"))
+
+    def load(self) -> None:
+        """LRC:748-753 (reads the reference's own index.pt format; never unpickles code)."""
+        index_file = os.path.join(self.config.colbert_index_path, "index.pt")
+        data = torch.load(index_file, map_location="cpu", weights_only=True)
+        self.corpus_embeddings = self._build(data["embeddings"])
+        self.corpus = data["corpus"]
+
+    def index_embeddings(self, embeddings, corpus: Optional[List[str]] = None) -> None:
+        """Install precomputed token embeddings (dense [N, L, D], pooled [N, D] or a list)."""
+        self.corpus_embeddings = self._build(embeddings)
+        self.corpus = corpus
+
+    # ------------------------------------------------------------ encoding
+    def _encode_query(self, query: Union[str, torch.Tensor]) -> torch.Tensor:
+        q = query if isinstance(query, torch.Tensor) else self.model.encode(query, convert_to_tensor=True)
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        return q
+
+    # ------------------------------------------------------------ search
+    def search(self, query: str, k: int = 10) -> List[Dict]:
+        """LRC:755-777: [{'document_id', 'score', 'text'}] best first."""
+        ix = self.corpus_embeddings
+        if ix is None:
+            raise RuntimeError("no index: call index() or load() first")
+        q = self._encode_query(query)
+        kk = min(k, len(ix))
+        if kk <= 0:
+            return []
+        scores, ids = ix.search(q.unsqueeze(0), kk, scorer=self.scorer)
+        scores, ids = scores[0].tolist(), ids[0].tolist()  # one D2H copy each
+        return [{"document_id": int(i), "score": float(s), "text": self.corpus[i] if self.corpus else None}
+                for s, i in zip(scores, ids)]
+
+    def search_embeddings(self, Q: torch.Tensor, k: int):
+        """Batched stage 2: Q [B, lq, D] -> device (scores [B, k], global ids [B, k])."""
+        return self.corpus_embeddings.search(Q, k, scorer=self.scorer)
+
+    # ------------------------------------------------------------ rerank
+    def rerank(self, query: str, documents: List[str], k: int = 10) -> List[Dict]:
+        """LRC:779-800: re-encode query and documents, score, sort, top-k with 1-based rank."""
+        if not documents:
+            return []
+        q = self._encode_query(query)
+        d = self.model.encode(documents, convert_to_tensor=True)
+        tmp = self._build(d)
+        kk = min(k, len(documents))
+        if self.scorer == "maxsim":
+            cand = torch.arange(len(documents), dtype=torch.int32, device=self.device).unsqueeze(0)
+            scores, _, pos = tmp.rerank(q.unsqueeze(0), cand, kk)
+        else:
+            raw = tmp.score(q.unsqueeze(0), scorer=self.scorer)
+            scores, _, pos = select_topk(raw, kk)
+        scores, pos = scores[0].tolist(), pos[0].tolist()
+        return [{"result_index": int(p), "score": float(s), "rank": r + 1, "text": documents[p]}
+                for r, (s, p) in enumerate(zip(scores, pos))]
+
+    def rerank_ids(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+        """Batched stage 3 on precomputed tiles: -> device (scores, global ids, positions) [B, k]."""
+        if self.scorer != "maxsim":
+            raise ValueError("rerank_ids gathers token tiles and scores with MaxSim; use rerank() "
+                             "for the ref_meanpool_cosine scorer")
+        return self.corpus_embeddings.rerank(Q, cand, k)
+
+    # ------------------------------------------------------------ scorer
+    def _maxsim_score(self, query_embedding: torch.Tensor, doc_embeddings: torch.Tensor) -> torch.Tensor:
+        """LRC:802-831 shape semantics: 2-D inputs gain a leading batch dim; returns .squeeze()."""
+        q = query_embedding.unsqueeze(0) if query_embedding.dim() == 2 else query_embedding
+        d = doc_embeddings.unsqueeze(0) if doc_embeddings.dim() == 2 else doc_embeddings
+        tmp = self._build(d)
+        return tmp.score(q, scorer=self.scorer).squeeze()

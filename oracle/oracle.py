@@ -53,20 +53,22 @@ def bf16_round(x: np.ndarray) -> np.ndarray:
 
 
 # ------------------------------------------------------------------ scorers
-def maxsim(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray | None = None) -> np.ndarray:
-    """True MaxSim, float64: Q [B, lq, D], docs [N, L, D] -> [B, N].
+def maxsim(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray | None = None,
+           dtype=np.float64) -> np.ndarray:
+    """True MaxSim: Q [B, lq, D], docs [N, L, D] -> [B, N] (float64 by default;
+    dtype=np.float32 is the reference's own CPU arithmetic, used as the timed baseline).
 
     Rows t >= doclens[n] never score; an empty doc scores -inf.
     """
-    Q = np.asarray(Q, dtype=np.float64)
+    Q = np.asarray(Q, dtype=dtype)
     if Q.ndim == 2:
         Q = Q[None]
-    docs = np.asarray(docs, dtype=np.float64)
+    docs = np.asarray(docs, dtype=dtype)
     N, L, _ = docs.shape
     if doclens is None:
         doclens = np.full(N, L, np.int64)
     valid = np.arange(L)[None, :] < np.asarray(doclens)[:, None]            # [N, L]
-    out = np.empty((Q.shape[0], N), np.float64)
+    out = np.empty((Q.shape[0], N), dtype)
     for b in range(Q.shape[0]):
         sim = np.einsum("nld,qd->nlq", docs, Q[b], optimize=True)           # [N, L, lq]
         sim = np.where(valid[:, :, None], sim, -np.inf)
