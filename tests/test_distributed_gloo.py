@@ -1,0 +1,110 @@
+"""CPU, world_size 2 (gloo): the sharded search / rerank protocol of
+hybrid-rag-colbertv2_amd/distributed.py (all-gather of packed (score, id)
+pairs + merge; all-reduce MAX of candidate scores + select) equals the
+unsharded oracle.  The per-shard compute is injected as oracle-backed CPU
+objects (test-only); on the GPU box the same class drives the HIP kernels
+over RCCL (tests/test_gpu_api.py).
+"""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as orc
+
+
+class OracleShard:
+    def __init__(self, Q, docs, doclens, begin):
+        self.docs, self.doclens, self.begin = docs, doclens, begin
+
+    def search(self, Q, k):
+        s = orc.maxsim(Q.numpy(), self.docs, self.doclens)
+        vs, ids = orc.topk(s, k, id_base=self.begin)
+        return torch.from_numpy(vs.astype(np.float32)), torch.from_numpy(ids.astype(np.int32))
+
+    def rerank(self, Q, cand, k):
+        assert k == 0
+        c = cand.numpy()
+        out = np.full(c.shape, -np.inf, np.float32)
+        for b in range(c.shape[0]):
+            for j in range(c.shape[1]):
+                loc = c[b, j] - self.begin
+                if c[b, j] >= 0 and 0 <= loc < len(self.docs):
+                    out[b, j] = orc.maxsim(Q[b:b + 1].numpy(), self.docs[loc:loc + 1], self.doclens[loc:loc + 1])[0, 0]
+        return torch.from_numpy(out)
+
+
+class OracleOps:
+    @staticmethod
+    def merge(S, I, k):
+        s, i = orc.merge_topk(S.numpy(), I.numpy(), k)
+        return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(i.astype(np.int32))
+
+    @staticmethod
+    def select(scores, k, ids):
+        sc = scores.numpy()
+        out_s = np.full((sc.shape[0], k), -np.inf, np.float32)
+        out_i = np.full((sc.shape[0], k), -1, np.int32)
+        out_p = np.full((sc.shape[0], k), -1, np.int32)
+        for b in range(sc.shape[0]):
+            for r, (p, s, _) in enumerate(orc.rerank_select(sc[b], k)):
+                out_s[b, r], out_i[b, r], out_p[b, r] = s, ids[b, p], p
+        return torch.from_numpy(out_s), torch.from_numpy(out_i), torch.from_numpy(out_p)
+
+
+def _data():
+    rng = np.random.default_rng(7)
+    N, B = 301, 3
+    docs = orc.bf16_round(rng.standard_normal((N, 16, 128)).astype(np.float32))
+    doclens = rng.integers(0, 17, size=N)
+    Q = torch.from_numpy(orc.bf16_round(rng.standard_normal((B, 32, 128)).astype(np.float32)))
+    cand = rng.integers(-1, N, size=(B, 20)).astype(np.int32)
+    return Q, docs, doclens, cand
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range
+        Q, docs, doclens, cand = _data()
+        a, b = shard_range(len(docs), rank, world)
+        ss = ShardedSearcher(OracleShard(Q, docs[a:b], doclens[a:b], a), ops=OracleOps())
+        s, i = ss.search(Q, 40)
+        rs, ri, rp = ss.rerank(Q, torch.from_numpy(cand), 7)
+        q.put((rank, s.numpy(), i.numpy(), rs.numpy(), ri.numpy(), rp.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_sharded_protocol_world2_equals_unsharded():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Q, docs, doclens, cand = _data()
+    full = orc.maxsim(Q.numpy(), docs, doclens)
+    es, ei = orc.topk(full, 40)
+    rs, ri, rp = orc.rerank(Q.numpy(), docs, doclens, cand, 7)
+    for _, s, i, gs, gi, gp in res:        # every rank holds the identical global answer
+        assert np.array_equal(i, ei)
+        np.testing.assert_allclose(s, es, atol=1e-5)
+        assert np.array_equal(gp, rp) and np.array_equal(gi, ri)
+        np.testing.assert_allclose(gs, rs, atol=1e-5)

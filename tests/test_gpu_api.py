@@ -1,0 +1,168 @@
+"""GPU: the drop-in Python API (JinaColBERTRetriever / DualIndexer /
+HybridRetriever) on the HIP kernels reproduces the reference's recorded
+outputs (config 1, literal scorer) and the oracle's (maxsim scorer)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from hybrid_rag_colbertv2_amd import FakeEncoder, RAGConfig
+from hybrid_rag_colbertv2_amd.hybrid import ChunkStore, DualIndexer, HybridRetriever
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+TOY = json.load(open(os.path.join(GOLDEN, "toy_c1.json")))
+
+
+class RecordedBM25:
+    """Stage-1 stand-in replaying the BM25 lists recorded with the golden run."""
+
+    def __init__(self):
+        self.lists = {q: bm for q, bm in zip(TOY["queries"], TOY["bm25"])}
+
+    def tokenize(self, q):
+        return q
+
+    def retrieve(self, q, k):
+        bm = self.lists[q]
+        return np.array([bm["ids"][:k]]), np.array([bm["scores"][:k]])
+
+
+def _system(tmp_path, scorer):
+    cfg = RAGConfig(scorer=scorer, colbert_index_path=str(tmp_path / "colbert"),
+                    bm25_index_path=str(tmp_path / "bm25"))
+    ind = DualIndexer(cfg, encoder=FakeEncoder(**TOY["encoder"]))
+    ind.colbert_retriever.index(TOY["corpus"])
+    ind.bm25_retriever = RecordedBM25()
+    store = ChunkStore([{"chunk_id": c["id"], "text": t, "document_id": c["document_id"],
+                         "heading_path": c["heading_path"], "has_images": c["has_images"],
+                         "metadata": json.loads(c["metadata"]) if c["metadata"] else {}}
+                        for c, t in zip(TOY["chunks"], TOY["corpus"])])
+    return cfg, ind, HybridRetriever(cfg, ind, store, verbose=False)
+
+
+def test_c1_literal_search_rerank_retrieve_match_reference(dev, tmp_path):
+    cfg, ind, hyb = _system(tmp_path, "ref_meanpool_cosine")
+    r = ind.colbert_retriever
+    for i, q in enumerate(TOY["queries"]):
+        got = r.search(q, k=10)
+        assert [g["document_id"] for g in got] == [x["document_id"] for x in TOY["search"][i]]
+        np.testing.assert_allclose([g["score"] for g in got], [x["score"] for x in TOY["search"][i]], atol=1e-5)
+        assert got[0]["text"] == TOY["corpus"][got[0]["document_id"]]
+        rr = r.rerank(q, TOY["corpus"][0:50:3], k=5)
+        ref = TOY["rerank"][i]["results"]
+        assert [(x["result_index"], x["rank"]) for x in rr] == [(x["result_index"], x["rank"]) for x in ref]
+        np.testing.assert_allclose([x["score"] for x in rr], [x["score"] for x in ref], atol=1e-5)
+        fin = hyb.retrieve(q)
+        ref = TOY["retrieve"][i]
+        assert [f["chunk_id"] for f in fin] == [x["chunk_id"] for x in ref]
+        for f, x in zip(fin, ref):
+            assert f["text"] == TOY["corpus"][f["chunk_id"]]
+            assert {k: v for k, v in f.items() if k not in ("score", "text")} == \
+                {k: v for k, v in x.items() if k != "score"}
+            assert abs(f["score"] - x["score"]) < 1e-5
+
+
+def test_literal_maxsim_score_shapes_match_reference(dev, tmp_path):
+    cfg = RAGConfig(scorer="ref_meanpool_cosine")
+    from hybrid_rag_colbertv2_amd.retriever import JinaColBERTRetriever
+    r = JinaColBERTRetriever(cfg, encoder=FakeEncoder())
+    z = np.load(os.path.join(GOLDEN, "literal_maxsim.npz"))
+    for case in "abc":
+        got = r._maxsim_score(torch.from_numpy(z[f"{case}_q"]), torch.from_numpy(z[f"{case}_docs"]))
+        assert tuple(got.shape) == z[f"{case}_scores"].shape
+        np.testing.assert_allclose(got.cpu().numpy(), z[f"{case}_scores"], atol=1e-5)
+
+
+def test_maxsim_pipeline_matches_oracle(dev, tmp_path):
+    cfg, ind, hyb = _system(tmp_path, "maxsim")
+    enc = FakeEncoder(**TOY["encoder"])
+    docs = orc.bf16_round(enc.encode(TOY["corpus"], convert_to_tensor=False))
+    for i, q in enumerate(TOY["queries"]):
+        qe = orc.bf16_round(enc.encode(q, convert_to_tensor=False))
+        s = orc.maxsim(qe, docs)
+        es, ei = orc.topk(s, 10)
+        got = ind.colbert_retriever.search(q, k=10)
+        assert [g["document_id"] for g in got] == list(ei[0])
+        np.testing.assert_allclose([g["score"] for g in got], es[0], atol=1e-3)
+        fused = orc.rrf(TOY["bm25"][i]["ids"], list(orc.topk(s, 100)[1][0]))[:50]
+        cand = [c for c, _ in fused]
+        order = orc.rerank_select(s[0, cand], 10)
+        fin = hyb.retrieve(q)
+        assert [f["chunk_id"] for f in fin] == [cand[p] for p, _, _ in order]
+        assert [f["rank"] for f in fin] == list(range(1, len(fin) + 1))
+
+
+def test_index_save_load_roundtrip_and_reference_format(dev, tmp_path):
+    cfg, ind, _ = _system(tmp_path, "maxsim")
+    r = ind.colbert_retriever
+    before = r.search(TOY["queries"][0], k=7)
+    r.corpus_embeddings = None
+    r.load()
+    assert r.search(TOY["queries"][0], k=7) == before
+    # a file in the reference's own layout: {'embeddings': fp32 [N, L, D], 'corpus': [...]}
+    enc = FakeEncoder(maxlen=20)
+    emb = enc.encode(TOY["corpus"][:9], convert_to_tensor=True)
+    os.makedirs(tmp_path / "ref", exist_ok=True)
+    torch.save({"embeddings": emb, "corpus": TOY["corpus"][:9]}, tmp_path / "ref" / "index.pt")
+    cfg2 = RAGConfig(colbert_index_path=str(tmp_path / "ref"))
+    from hybrid_rag_colbertv2_amd.retriever import JinaColBERTRetriever
+    r2 = JinaColBERTRetriever(cfg2, encoder=enc)
+    r2.load()
+    res = r2.search(TOY["queries"][1], k=20)
+    assert len(res) == 9 and res[0]["text"] in TOY["corpus"][:9]
+
+
+def test_pooled_query_and_docs_work(dev):
+    """Pooled [D] encodings (SentenceTransformer's default) are 1-token inputs here."""
+    from hybrid_rag_colbertv2_amd.retriever import JinaColBERTRetriever
+
+    class Pooled:
+        def encode(self, x, convert_to_tensor=True, **_):
+            e = FakeEncoder(maxlen=1).encode(x, convert_to_tensor=True)
+            return e[..., 0, :] if isinstance(x, list) else e[0]
+
+    r = JinaColBERTRetriever(RAGConfig(), encoder=Pooled())
+    r.index_embeddings(Pooled().encode(TOY["corpus"]), TOY["corpus"])
+    res = r.search(TOY["corpus"][4], k=3)
+    assert res[0]["document_id"] == 4
+
+
+def test_retrieve_batch_equals_single(dev, tmp_path):
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    B, N = 8, 3000
+    Qf = synth.make_queries(B)
+    planted = synth.planted_ids(B, N, 10)
+    tokens, doclens = synth.make_shard(0, N, Qf, planted, dev)
+    bm = synth.bm25_lists(B, N, planted)
+    cfg = RAGConfig()
+    ind = DualIndexer(cfg, encoder=FakeEncoder())
+    ind.colbert_retriever.corpus_embeddings = ColbertIndex(tokens, doclens)
+    hyb = HybridRetriever(cfg, ind, None, verbose=False)
+    Q = Qf.to(dev, torch.bfloat16)
+    s, i = hyb.retrieve_batch(Q, bm)
+    for b in range(B):
+        assert set(i[b].tolist()) == set(planted[b].tolist())
+        s1, i1 = hyb.retrieve_batch(Q[b:b + 1], bm[b:b + 1])
+        assert torch.equal(i1[0], i[b]) and torch.equal(s1[0], s[b])
+
+
+def test_sharded_searcher_single_process(dev):
+    from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    g = torch.Generator().manual_seed(0)
+    docs = torch.randn(500, 128, 128, generator=g).bfloat16()
+    ix = ColbertIndex(docs.to(dev), torch.full((500,), 128, dtype=torch.int32, device=dev))
+    Q = torch.randn(3, 32, 128, generator=g).bfloat16().to(dev)
+    ss = ShardedSearcher(ix)
+    a = ss.search(Q, 10)
+    b = ix.search(Q, 10)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    cand = a[1][:, :5].contiguous()
+    r1 = ss.rerank(Q, cand, 3)
+    r2 = ix.rerank(Q, cand, 3)
+    assert all(torch.equal(x, y) for x, y in zip(r1, r2))

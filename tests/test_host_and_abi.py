@@ -1,0 +1,106 @@
+"""CPU: the C-ABI library loads and exports every declared symbol; argument
+validation fails before any launch; host-side logic (native RRF, BM25 stand-in,
+sharding, synthetic corpus helpers) is exact."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from hybrid_rag_colbertv2_amd import _lib
+from oracle import oracle as orc
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libcolbert_mi355x.so not built")
+    return _lib.lib()
+
+
+def test_library_exports_every_header_symbol(L):
+    syms = _lib.header_symbols()
+    assert len(syms) >= 13
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib._SIGS), "ctypes signatures out of sync with the header"
+    assert L.cbv2_abi_version() == 1
+
+
+def test_validation_errors_without_gpu(L):
+    h = ctypes.c_void_p()
+    assert L.cbv2_index_create(0, None, 7, 10, 128, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
+    assert b"dtype" in L.cbv2_last_error()
+    assert L.cbv2_index_create(0, None, 1, 10, 64, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
+    assert L.cbv2_index_create(0, None, 1, -1, 128, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EINVAL
+    assert L.cbv2_index_create(0, None, 1, 10, 128, 128, None, 0, None) == _lib.ERR_EINVAL
+    assert L.cbv2_topk_rows(None, 1, 10, 10, 5, 0, None, None, None) == _lib.ERR_EINVAL
+    assert L.cbv2_select_topk(ctypes.c_void_p(16), None, 1, 10, 0, ctypes.c_void_p(16), None, None, None) \
+        == _lib.ERR_EINVAL
+    assert L.cbv2_merge_topk(ctypes.c_void_p(16), ctypes.c_void_p(16), 65, 1, 10, ctypes.c_void_p(16),
+                             ctypes.c_void_p(16), None) == _lib.ERR_EINVAL
+    assert L.cbv2_score(None, 0, None, 1, 1, 32, None, 0, None) == _lib.ERR_EINVAL
+    with pytest.raises(ValueError):
+        _lib.check(_lib.ERR_EINVAL)
+
+
+def test_native_rrf_matches_reference_golden(L):
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+    for case in json.load(open(os.path.join(GOLDEN, "rrf_ties.json"))):
+        bm = np.array(case["bm25"], np.int32).reshape(1, -1)
+        cb = np.array(case["colbert"], np.int32).reshape(1, -1)
+        ids, sc, cnt = rrf_fuse(bm, cb, C=200, return_scores=True)
+        n = int(cnt[0])
+        assert [(int(i), float(s)) for i, s in zip(ids[0, :n], sc[0, :n])] == \
+            [(f["chunk_id"], f["rrf_score"]) for f in case["fused"]]
+        assert (ids[0, n:] == -1).all()
+
+
+def test_native_rrf_batch_equals_python(L):
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+    rng = np.random.default_rng(0)
+    B = 64
+    bm = rng.integers(0, 300, size=(B, 100)).astype(np.int32)
+    cb = rng.integers(0, 300, size=(B, 100)).astype(np.int32)
+    cb[:, 90:] = -1
+    ids = rrf_fuse(bm, cb, C=50)
+    for b in range(B):
+        exp = [i for i, _ in orc.rrf(list(bm[b]), [x for x in cb[b] if x >= 0])][:50]
+        assert list(ids[b, : len(exp)]) == exp
+
+
+def test_host_bm25_basic(tmp_path):
+    from hybrid_rag_colbertv2_amd.bm25 import HostBM25
+    corpus = ["the cat sat on the mat", "dogs chase cats", "a bird in the hand", "cats and dogs and cats"]
+    bm = HostBM25()
+    bm.index(bm.tokenize(corpus))
+    ids, sc = bm.retrieve(bm.tokenize("cats"), k=3)
+    assert ids[0][0] == 3 and sc[0][0] > sc[0][1] > 0
+    bm.save(str(tmp_path))
+    bm2 = HostBM25.load(str(tmp_path))
+    ids2, sc2 = bm2.retrieve(bm2.tokenize("cats"), k=3)
+    assert np.array_equal(ids, ids2) and np.allclose(sc, sc2)
+
+
+def test_shard_range_partitions():
+    from hybrid_rag_colbertv2_amd.distributed import shard_range
+    for n in (0, 1, 7, 1000, 1_000_001):
+        for w in (1, 2, 3, 8):
+            r = [shard_range(n, k, w) for k in range(w)]
+            assert r[0][0] == 0 and r[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+            assert max(e - s for s, e in r) - min(e - s for s, e in r) <= 1
+
+
+def test_synth_helpers():
+    from hybrid_rag_colbertv2_amd import synth
+    p = synth.planted_ids(16, 5000, 10)
+    assert len(np.unique(p)) == p.size
+    bm = synth.bm25_lists(16, 5000, p, k=100)
+    assert bm.shape == (16, 100)
+    for b in range(16):
+        assert set(p[b, :5]) <= set(bm[b])
+    q = synth.make_queries(4)
+    assert np.allclose(q.norm(dim=-1).numpy(), 1.0, atol=1e-5)
