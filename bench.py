@@ -210,7 +210,7 @@ def main():
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
                        "parallelism": f"corpus sharded x{world}" + (" (RCCL all-gather + all-reduce)" if world > 1 else "")},
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
-            "roofline": {"bound": "mfma", "kernel": "maxsim_scan_kernel", "achieved": round(achieved, 2),
+            "roofline": {"bound": "mfma", "kernel": "maxsim_scan16_kernel<8,4>", "achieved": round(achieved, 2),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                          "traffic": traffic, "avg_ms": round(scan_avg, 3)},
             "cpu_baseline": cpu,

@@ -42,6 +42,7 @@ constexpr int kMergeMax = 8192;                   // G * k limit of the merge ke
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
@@ -93,6 +94,34 @@ __device__ __forceinline__ float col_reduce(float m, int r, int lq) {
   return v;
 }
 
+// Cross-lane helpers without LDS traffic (gfx950): v_permlane32_swap /
+// v_permlane16_swap exchange half-waves / 16-lane rows; DPP row ops do the rest.
+__device__ __forceinline__ float fold32_max(float v) {  // max over lanes l, l^32
+  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+__device__ __forceinline__ float fold16_max(float v) {  // max over lanes l, l^16 (rows 0<->1, 2<->3)
+  const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+__device__ __forceinline__ float fold16_add(float v) {  // sum over lanes l, l^16 row pairs
+  const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(t[0]) + __uint_as_float(t[1]);
+}
+__device__ __forceinline__ float dpp_row_sum16(float v) {  // sum over each 16-lane row, in every lane
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, true));  // row_mirror
+  return v;
+}
+// 32x32 epilogue, DPP form: same result set as col_reduce, no ds_bpermute.
+__device__ __forceinline__ float col_reduce_dpp(float m, int r, int lq) {
+  float v = fold32_max(m);
+  v = (r < lq) ? v : 0.0f;
+  return fold16_add(dpp_row_sum16(v));
+}
+
 // B-operand fragments of one query for v_mfma_f32_32x32x16_bf16.  Lane l
 // (r = l&31 query token, h = l>>5) holds, for k-step s, dims 64h+8s .. 64h+8s+7
 // of token r.  The doc A-operand uses the same permutation of the 128 dims, so
@@ -116,7 +145,7 @@ __device__ __forceinline__ void load_qfrag(const uint16_t* __restrict__ Q, int q
 // ds_read_b128 for the A-fragment pattern; filled by lane-linear LDS-DMA with
 // the XOR applied to the per-lane SOURCE address).
 // ---------------------------------------------------------------------------
-template <int WAVES, int QW>
+template <int WAVES, int QW, bool DPP>
 __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -208,7 +237,204 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_kernel(
     }
 #pragma unroll
     for (int q = 0; q < QW; ++q) {
-      const float v = col_reduce(m[q], r, lq);
+      const float v = DPP ? col_reduce_dpp(m[q], r, lq) : col_reduce(m[q], r, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = g * QPB + wave * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MaxSim scan on v_mfma_f32_16x16x32_bf16.  Per (query, doc): 8 doc row tiles
+// (16 tokens) x 2 query column tiles (16 tokens) x 4 k-steps (32 dims) = 64
+// MFMAs.  Lane l: c = l&15, g = l>>4.  A (doc): token 16*rt + c, dims
+// 32g + 8s .. +7 of k-step s;  B (query): token 16*ct + c, same dims.  C/D:
+// column c (query token), rows 4g + reg (doc tokens).  Accumulators are 4
+// registers, so the A fragments of the NEXT row tile are read from LDS while
+// the current tile's MFMAs run (16 VGPRs per tile, double-buffered).
+// LDS image: 16-B slot p of token t holds logical slot p ^ swz16(t), which is
+// conflict-free for this fragment pattern in every ds_read_b128 lane group.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int swz16(int t) { return ((t & 1) << 3) | (t & 2) | ((t >> 2) & 1); }
+
+__device__ __forceinline__ void load_qfrag16(const uint16_t* __restrict__ Q, int qi, int B, int lq, int lane,
+                                             bf16x8 (&qf)[2][4]) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int tok = 16 * ct + c;
+    const bool ok = (qi < B) && (tok < lq);
+    const u32x4* src = reinterpret_cast<const u32x4*>(Q + ((size_t)(ok ? qi : 0) * lq + (ok ? tok : 0)) * kDim + 32 * g);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u32x4 v = ok ? src[s] : u32x4{0u, 0u, 0u, 0u};
+      qf[ct][s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+}
+
+// A fragments of row tile rt from the swizzled LDS image.
+__device__ __forceinline__ void lds_afrag16(const uint8_t* buf, int rt, int lane, bf16x8 (&a)[4]) {
+  const int c = lane & 15, g = lane >> 4;
+  const int t = 16 * rt + c;
+  const uint8_t* row = buf + t * kRowBytes;
+  const int sw = swz16(t);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) a[s] = *reinterpret_cast<const bf16x8*>(row + 16 * ((4 * g + s) ^ sw));
+}
+
+// A fragments of row tile rt straight from global memory (rerank gather).
+__device__ __forceinline__ void gbl_afrag16(const uint8_t* doc, int rt, int lane, bf16x8 (&a)[4]) {
+  const int c = lane & 15, g = lane >> 4;
+  const u32x4* src = reinterpret_cast<const u32x4*>(doc + (16 * rt + c) * kRowBytes + 64 * g);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) a[s] = __builtin_bit_cast(bf16x8, src[s]);
+}
+
+__device__ __forceinline__ f32x4 row_mask_init16(int row0, int dl) {
+  f32x4 a;
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) a[reg] = (row0 + reg < dl) ? 0.0f : neg_inf();
+  return a;
+}
+
+// One row tile against QW queries: m[q][ct] = max(m, max over this lane's 4 rows).
+template <int QW>
+__device__ __forceinline__ void tile16(const bf16x8 (&a)[4], const bf16x8 (&qf)[QW][2][4], const f32x4& init,
+                                       float (&m)[QW][2]) {
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      f32x4 acc = init;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], qf[q][ct][s], acc, 0, 0, 0);
+      m[q][ct] = fmaxf(fmaxf(m[q][ct], fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
+    }
+  }
+}
+
+// Per-(query, doc) epilogue of the 16x16 tiling: max over the 4 row groups,
+// then sum over the lq query tokens (2 column tiles x 16 lanes).
+__device__ __forceinline__ float reduce16(float m0, float m1, int lane, int lq) {
+  const int c = lane & 15;
+  m0 = fold16_max(fold32_max(m0));
+  m1 = fold16_max(fold32_max(m1));
+  const float v = (c < lq ? m0 : 0.0f) + (16 + c < lq ? m1 : 0.0f);
+  return dpp_row_sum16(v);
+}
+
+// Full (query, doc) MaxSim for the 16x16 tiling; FRAG(rt, a) loads row tile rt.
+template <int QW, typename Frag>
+__device__ __forceinline__ void doc16(Frag frag, const bf16x8 (&qf)[QW][2][4], int dl, int lane, float (&m)[QW][2]) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+  if (dl >= kLd) {
+    // Full doc (the common case): straight-line, so hipcc counts the LDS reads
+    // exactly and the next tile's fragments load under the current tile's MFMAs.
+    bf16x8 a0[4], a1[4];
+    frag(0, a0);
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; rt += 2) {
+      frag(rt + 1, a1);
+      tile16<QW>(a0, qf, f32x4{}, m);
+      if (rt + 2 < kLd / 16) frag(rt + 2, a0);
+      tile16<QW>(a1, qf, f32x4{}, m);
+    }
+    return;
+  }
+  const int nrt = (dl + 15) >> 4;
+  bf16x8 a0[4], a1[4];
+  if (nrt > 0) frag(0, a0);
+#pragma unroll
+  for (int rt = 0; rt < kLd / 16; rt += 2) {
+    if (rt < nrt) {
+      if (rt + 1 < nrt) frag(rt + 1, a1);
+      const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+      tile16<QW>(a0, qf, init, m);
+    }
+    if (rt + 1 < nrt) {
+      if (rt + 2 < nrt) frag(rt + 2, a0);
+      const f32x4 init = (dl >= 16 * rt + 32) ? f32x4{} : row_mask_init16(16 * rt + 16 + 4 * g, dl);
+      tile16<QW>(a1, qf, init, m);
+    }
+  }
+}
+
+template <int WAVES, int QW, int OCC = 2>
+__global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
+    int64_t chunk_docs) {
+  constexpr int QPB = WAVES * QW;
+  constexpr int kPieces = kDocBytes / 1024;
+  constexpr int kPiecesPerWave = kPieces / WAVES;
+  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * kDocBytes];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int g = lin % nq_groups;
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;
+  const int nd = (int)(d_end - d_begin);
+
+  bf16x8 qf[QW][2][4];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag16(Q, g * QPB + wave * QW + q, B, lq, lane, qf[q]);
+
+  uint32_t src_off[kPiecesPerWave];
+#pragma unroll
+  for (int j = 0; j < kPiecesPerWave; ++j) {
+    const int piece = wave * kPiecesPerWave + j;
+    const int t = 4 * piece + (lane >> 4);
+    src_off[j] = t * kRowBytes + 16 * ((lane & 15) ^ swz16(t));
+  }
+  auto issue = [&](int i, int buf) {
+    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kDocBytes;
+#pragma unroll
+    for (int j = 0; j < kPiecesPerWave; ++j) {
+      const int piece = wave * kPiecesPerWave + j;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(dbase + src_off[j]),
+                                       (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16, 0, 0);
+    }
+  };
+
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+
+  issue(0, 0);
+  for (int i = 0; i < nd; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i + 1 < nd) issue(i + 1, (i + 1) & 1);
+
+    const uint8_t* buf = smem + (i & 1) * kDocBytes;
+    int dl = doclens[d_begin + i];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    float m[QW][2];
+    doc16<QW>([&](int rt, bf16x8 (&a)[4]) { lds_afrag16(buf, rt, lane, a); }, qf, dl, lane, m);
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
       sc[q] = (lane == (i & 63)) ? v : sc[q];
     }
     if ((i & 63) == 63 || i == nd - 1) {
@@ -419,10 +645,10 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
   __shared__ uint64_t keys[kSmallMax];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, h = lane >> 5;
   const int b = blockIdx.x;
-  bf16x8 qf[8];
-  load_qfrag(Q, b, b + 1, lq, lane, qf);
+  bf16x8 qf[1][2][4];
+  load_qfrag16(Q, b, b + 1, lq, lane, qf[0]);
+  const int g = lane >> 4;
   const int32_t* crow = cand + (size_t)b * C;
   for (int c = wave; c < C; c += kRrWaves) {
     const int32_t id = crow[c];
@@ -432,26 +658,20 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
       int dl = doclens[loc];
       dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
       const uint8_t* dbase = tokens + (size_t)loc * kDocBytes;
-      bf16x8 af[4][8];
+      // the whole doc in flight at once (32 KiB per wave), then the scan's math
+      bf16x8 af[kLd / 16][4];
 #pragma unroll
-      for (int blk = 0; blk < 4; ++blk) {
-        if (dl > 32 * blk) {
-          const u32x4* src = reinterpret_cast<const u32x4*>(dbase + (32 * blk + r) * kRowBytes + 128 * h);
+      for (int rt = 0; rt < kLd / 16; ++rt)
+        if (16 * rt < dl) gbl_afrag16(dbase, rt, lane, af[rt]);
+      float m[1][2] = {{neg_inf(), neg_inf()}};
 #pragma unroll
-          for (int s = 0; s < 8; ++s) af[blk][s] = __builtin_bit_cast(bf16x8, src[s]);
+      for (int rt = 0; rt < kLd / 16; ++rt) {
+        if (16 * rt < dl) {
+          const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+          tile16<1>(af[rt], qf, init, m);
         }
       }
-      float m = neg_inf();
-#pragma unroll
-      for (int blk = 0; blk < 4; ++blk) {
-        if (dl > 32 * blk) {
-          f32x16 acc = (dl >= 32 * blk + 32) ? f32x16{} : row_mask_init(32 * blk + 4 * h, dl);
-#pragma unroll
-          for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[blk][s], qf[s], acc, 0, 0, 0);
-          m = fmaxf(m, max16(acc));
-        }
-      }
-      v = col_reduce(m, r, lq);
+      v = reduce16(m[0][0], m[0][1], lane, lq);
     }
     if (lane == 0) sc[c] = v;
   }
@@ -650,13 +870,23 @@ int launch_check(const char* what) {
   return CBV2_OK;
 }
 
-constexpr int kScanWaves = 4, kScanQW = 4, kScanQPB = kScanWaves * kScanQW;
+// Scan variants (tools/scan_lab.py A/Bs them in one process; the default is
+// the fastest measured).  id: kernel, waves/workgroup, queries/wave.
+enum ScanVariant {
+  kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
+  kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8
+};
+// Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
+// 1: 58.3 %, 2: 61.7 %, 3: 65.3 %, 4: 59.4 %, 5: 52.0 %, 6: 61.2 %, 8: 54.8 %
+// of the bf16 dense peak.  rerank_kernel uses the same 16x16 math as 2/3/5-8.
+constexpr int kDefaultScan = kScan16W8;
 
-int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
-                hipStream_t st) {
-  if (ix->n == 0) return CBV2_OK;
-  const int nq_groups = (B + kScanQPB - 1) / kScanQPB;
-  const int64_t target = 2LL * cu_count(ix->device);  // two resident workgroups per CU
+template <int WAVES, int QW, int PER_CU, typename Kern>
+int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
+                hipStream_t st, const char* name) {
+  constexpr int QPB = WAVES * QW;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int64_t target = (int64_t)PER_CU * cu_count(ix->device);  // resident workgroups
   int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
   if (n_chunks < 1) n_chunks = 1;
   if (n_chunks > ix->n) n_chunks = ix->n;
@@ -664,9 +894,36 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = (int64_t)nq_groups * n_chunks;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_kernel<kScanWaves, kScanQW>), dim3((unsigned)grid), dim3(kScanWaves * 64), 0,
-                     st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs);
-  return launch_check("maxsim_scan_kernel");
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens, ix->n, Q, B, lq,
+                     out, ld_out, chunk_docs);
+  return launch_check(name);
+}
+
+int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
+                int variant = kDefaultScan) {
+  if (ix->n == 0) return CBV2_OK;
+  switch (variant) {
+    case kScan32Shfl:
+      return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
+    case kScan32Dpp:
+      return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, true>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
+    case kScan16W4:
+      return launch_scan<4, 4, 2>(maxsim_scan16_kernel<4, 4>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    case kScan16W8:
+      return launch_scan<8, 4, 1>(maxsim_scan16_kernel<8, 4>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    case kScan32DppW8:
+      return launch_scan<8, 4, 1>(maxsim_scan_kernel<8, 4, true>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
+    case kScan16W4Q8:
+      return launch_scan<4, 8, 1>(maxsim_scan16_kernel<4, 8, 1>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    case kScan16W8Q2:
+      return launch_scan<8, 2, 1>(maxsim_scan16_kernel<8, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    case kScan16W8Q3:
+      return launch_scan<8, 3, 1>(maxsim_scan16_kernel<8, 3>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    case kScan16W4Q2:
+      return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    default:
+      return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
+  }
 }
 
 int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
