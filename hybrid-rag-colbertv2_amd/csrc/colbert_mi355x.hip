@@ -450,6 +450,72 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Small-batch scan (B <= 2 per query group): HBM-bound, so no LDS staging —
+// every wave owns a contiguous doc range and streams each doc (32 KiB, 128 B
+// per lane per row tile) straight into VGPRs; 8 waves per CU keep ~256 KiB in
+// flight per CU.  Same tile order, masking and epilogue as doc16, so scores are
+// bit-identical to the LDS kernel's and the rerank kernel's.
+// ---------------------------------------------------------------------------
+template <int QW>
+__global__ __launch_bounds__(256, 2) void maxsim_scan_direct_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
+    int64_t chunk_docs) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t lin = (int64_t)blockIdx.x * 4 + wave;      // one doc chunk per wave
+  const int qg = (int)(lin % nq_groups);
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;  // uniform over the wave; no block-level sync below
+  const int nd = (int)(d_end - d_begin);
+
+  bf16x8 qf[QW][2][4];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QW + q, B, lq, lane, qf[q]);
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+
+  for (int i = 0; i < nd; ++i) {
+    int dl = doclens[d_begin + i];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kDocBytes;
+    bf16x8 af[kLd / 16][4];
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt)
+      if (16 * rt < dl) gbl_afrag16(dbase, rt, lane, af[rt]);
+    float m[QW][2];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt) {
+      if (16 * rt < dl) {
+        const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+        tile16<QW>(af[rt], qf, init, m);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = qg * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Row top-k: exact radix select (11/11/10-bit digits of the order-preserving
 // score key; if the k-th score is tied, a second radix select over ~index picks
 // the lowest indices), then a bitonic sort of the k winners in LDS.
@@ -874,12 +940,18 @@ int launch_check(const char* what) {
 // the fastest measured).  id: kernel, waves/workgroup, queries/wave.
 enum ScanVariant {
   kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
-  kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8
+  kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
+  kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
 // 1: 58.3 %, 2: 61.7 %, 3: 65.3 %, 4: 59.4 %, 5: 52.0 %, 6: 61.2 %, 8: 54.8 %
 // of the bf16 dense peak.  rerank_kernel uses the same 16x16 math as 2/3/5-8.
-constexpr int kDefaultScan = kScan16W8;
+constexpr int kDefaultScan = kScanAuto;
+// Auto dispatch (measured, 1M docs, tools/scan_lab.py): B<=8 direct scan
+// (B=1: 5.0 ms = 6.5 TB/s of doc bytes; B=8: 13.7 ms vs 18.4 ms for the LDS
+// kernel), B<=16 the 16-query LDS kernel, larger B the 32-query LDS kernel.
+constexpr int kDirectMaxB = 8;
+constexpr int kSmallLdsMaxB = 16;
 
 template <int WAVES, int QW, int PER_CU, typename Kern>
 int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
@@ -899,10 +971,33 @@ int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, flo
   return launch_check(name);
 }
 
+template <int QW>
+int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t target_waves = 8LL * cu_count(ix->device);  // 2 waves per SIMD
+  int64_t n_chunks = (target_waves + nq_groups - 1) / nq_groups;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  if (n_chunks < 1) n_chunks = 1;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t waves = (int64_t)nq_groups * n_chunks;
+  const int64_t grid = (waves + 3) / 4;
+  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  hipLaunchKernelGGL(maxsim_scan_direct_kernel<QW>, dim3((unsigned)grid), dim3(256), 0, st, ix->tokens, ix->doclens,
+                     ix->n, Q, B, lq, out, ld_out, chunk_docs);
+  return launch_check("maxsim_scan_direct_kernel");
+}
+
 int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                 int variant = kDefaultScan) {
   if (ix->n == 0) return CBV2_OK;
+  if (variant == kScanAuto)
+    variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2) : (B <= kSmallLdsMaxB ? kScan16W4 : kScan16W8);
   switch (variant) {
+    case kScanDirectQ1:
+      return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
+    case kScanDirectQ2:
+      return launch_direct<2>(ix, Q, B, lq, out, ld_out, st);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:

@@ -254,3 +254,16 @@ def test_errors_raise_without_launch(dev):
         ix.score(Q.to(dev), scorer="nope")
     with pytest.raises(Exception):
         ix.score(Q.to(dev).float(), scorer="ref_meanpool_cosine")  # means not built
+
+
+def test_small_batch_scan_bit_identical_to_batched(dev):
+    """B<=4 runs the direct (HBM-streaming) scan, B>4 the LDS scan: same bits."""
+    docs, doclens, Q = make_case(123, 900, 20, 32)
+    ix = ColbertIndex(docs.to(dev), doclens.to(dev))
+    full = ix.score(Q.to(dev))
+    for lo, hi in [(0, 1), (3, 5), (7, 10), (10, 14), (5, 6)]:
+        part = ix.score(Q[lo:hi].to(dev))
+        assert torch.equal(part, full[lo:hi]), (lo, hi)
+    s1, i1 = ix.search(Q[:1].to(dev), k=30)
+    s, i = ix.search(Q.to(dev), k=30)
+    assert torch.equal(i1[0], i[0]) and torch.equal(s1[0], s[0])

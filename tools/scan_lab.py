@@ -46,7 +46,7 @@ def main():
                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     dev = torch.device("cuda:0")
     Qf = synth.make_queries(a.batch, 32, seed=1)
-    planted = synth.planted_ids(a.batch, a.docs, 10, seed=2)
+    planted = synth.planted_ids(max(a.batch, 8), a.docs, 10, seed=2)[: a.batch]
     tokens, doclens = synth.make_shard(0, a.docs, Qf, planted, dev, seed=0)
     # ragged tail so every variant's masking path runs
     doclens[-1000:] = torch.randint(0, 129, (1000,), device=dev, dtype=torch.int32)
@@ -74,17 +74,20 @@ def main():
             times[v].append(e0.elapsed_time(e1))
     # oracle on a slice (first 64 and last 200 docs, 8 queries)
     sl = torch.cat([torch.arange(64), torch.arange(a.docs - 200, a.docs)]).to(dev)
-    ref = orc.maxsim(Q[:8].float().cpu().numpy(), tokens[sl].float().cpu().numpy(), doclens[sl].cpu().numpy())
+    nq = min(8, a.batch)
+    ref = orc.maxsim(Q[:nq].float().cpu().numpy(), tokens[sl].float().cpu().numpy(), doclens[sl].cpu().numpy())
     flop = a.batch * a.docs * 2 * 32 * 128 * 128
     base = outs[variants[0]]
     for v in variants:
         med = statistics.median(times[v])
-        got = outs[v][:8, sl].cpu().numpy()
+        got = outs[v][:nq, sl].cpu().numpy()
         fin = np.isfinite(ref)
         err = float(np.abs(got[fin] - ref[fin]).max())
         inf_ok = bool((np.isneginf(got) == np.isneginf(ref)).all())
         dv = float((outs[v] - base).abs().nan_to_num(0).max())
-        print(f"variant {v}: median {med:.3f} ms  min {min(times[v]):.3f}  {flop / med / 1e9:.1f} TFLOP/s "
+        gbs = a.docs * 32768 / med / 1e6
+        print(f"B={a.batch} variant {v}: median {med:.3f} ms  min {min(times[v]):.3f}  {gbs:.0f} GB/s doc bytes  "
+              f"{flop / med / 1e9:.1f} TFLOP/s "
               f"({flop / med / 1e9 / 2500 * 100:.1f}% of bf16 peak)  oracle_err {err:.2e} inf_ok {inf_ok} "
               f"max|d vs v{variants[0]}| {dv:.2e}", flush=True)
 
