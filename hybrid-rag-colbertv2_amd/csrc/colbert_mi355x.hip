@@ -572,6 +572,91 @@ __device__ void bitonic_desc(uint64_t* keys, int P) {
   __syncthreads();
 }
 
+// Exact selection of the kk largest keys of row x into sel[0..kk) (unordered).
+// Radix select on the 32-bit score key (11/11/10-bit digits); if the kk-th
+// score is tied, a second radix select over ~index keeps the lowest indices.
+__device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, uint64_t* sel, uint32_t* hist,
+                               uint32_t* s_bin, uint32_t* s_above, uint32_t* s_bincount, uint32_t* s_cnt) {
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int wave = tid >> 6;
+  if (kk == n) {
+    for (int i = tid; i < kk; i += nth) sel[i] = rank_key(x[i], (uint32_t)i);
+    __syncthreads();
+    return;
+  }
+  const int shifts[3] = {21, 10, 0};
+  const int bits[3] = {11, 11, 10};
+  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)kk, last_count = 0;
+  for (int p = 0; p < 3; ++p) {
+    const int nb = 1 << bits[p];
+    for (int b = tid; b < nb; b += nth) hist[b] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += nth) {
+      const uint32_t u = f2u(x[i]);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shifts[p]) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    if (wave == 0) find_bin(hist, nb, kleft, s_bin, s_above, s_bincount);
+    __syncthreads();
+    kleft -= *s_above;
+    prefix |= *s_bin << shifts[p];
+    mask |= (uint32_t)(nb - 1) << shifts[p];
+    last_count = *s_bincount;
+    __syncthreads();
+  }
+  const uint32_t ustar = prefix;
+  uint32_t id_thr = 0xffffffffu;  // ties at ustar with index <= id_thr are taken
+  if (kleft < last_count) {
+    uint32_t iprefix = 0, imask = 0, kl2 = kleft;
+    for (int p = 0; p < 3; ++p) {
+      const int nb = 1 << bits[p];
+      for (int b = tid; b < nb; b += nth) hist[b] = 0;
+      __syncthreads();
+      for (int64_t i = tid; i < n; i += nth) {
+        const uint32_t key2 = ~(uint32_t)i;
+        if (f2u(x[i]) == ustar && (key2 & imask) == iprefix) atomicAdd(&hist[(key2 >> shifts[p]) & (nb - 1)], 1u);
+      }
+      __syncthreads();
+      if (wave == 0) find_bin(hist, nb, kl2, s_bin, s_above, s_bincount);
+      __syncthreads();
+      kl2 -= *s_above;
+      iprefix |= *s_bin << shifts[p];
+      imask |= (uint32_t)(nb - 1) << shifts[p];
+      __syncthreads();
+    }
+    id_thr = ~iprefix;
+  }
+  if (tid == 0) *s_cnt = 0;
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += nth) {
+    const uint32_t u = f2u(x[i]);
+    if (u > ustar || (u == ustar && (uint32_t)i <= id_thr)) {
+      const uint32_t pos = atomicAdd(s_cnt, 1u);
+      if (pos < (uint32_t)kk) sel[pos] = ((uint64_t)u << 32) | (uint32_t)(~(uint32_t)i);
+    }
+  }
+  __syncthreads();
+}
+
+// Sort sel[0..cnt) descending (padding to a power of two) and write the best k.
+__device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, float* out_s, int32_t* out_i) {
+  int P = 1;
+  while (P < cnt) P <<= 1;
+  for (int i = cnt + threadIdx.x; i < P; i += blockDim.x) sel[i] = 0;
+  bitonic_desc(sel, P);
+  for (int j = threadIdx.x; j < k; j += blockDim.x) {
+    float s = neg_inf();
+    int32_t id = -1;
+    if (j < cnt) {
+      const uint64_t key = sel[j];
+      s = u2f((uint32_t)(key >> 32));
+      id = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+    }
+    out_s[j] = s;
+    out_i[j] = id;
+  }
+}
+
 __global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __restrict__ scores, int64_t n,
                                                                int64_t ld, int k, int64_t id_base,
                                                                float* __restrict__ out_s,
@@ -579,83 +664,101 @@ __global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __re
   __shared__ uint32_t hist[2048];
   __shared__ uint64_t sel[kTopkMax];
   __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
   const float* x = scores + (size_t)blockIdx.x * ld;
   const int kk = (int)((int64_t)k < n ? k : n);
+  topk_exact_row(x, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
+  sort_and_write(sel, kk, k, id_base, out_s + (size_t)blockIdx.x * k, out_i + (size_t)blockIdx.x * k);
+}
 
-  if (kk == n) {
-    for (int i = tid; i < kk; i += kTkThreads) sel[i] = rank_key(x[i], (uint32_t)i);
-  } else {
-    const int shifts[3] = {21, 10, 0};
-    const int bits[3] = {11, 11, 10};
-    uint32_t prefix = 0, mask = 0, kleft = (uint32_t)kk, last_count = 0;
-    for (int p = 0; p < 3; ++p) {
-      const int nb = 1 << bits[p];
-      for (int b = tid; b < nb; b += kTkThreads) hist[b] = 0;
-      __syncthreads();
-      for (int64_t i = tid; i < n; i += kTkThreads) {
-        const uint32_t u = f2u(x[i]);
-        if ((u & mask) == prefix) atomicAdd(&hist[(u >> shifts[p]) & (nb - 1)], 1u);
-      }
-      __syncthreads();
-      if (wave == 0) find_bin(hist, nb, kleft, &s_bin, &s_above, &s_bincount);
-      __syncthreads();
-      kleft -= s_above;
-      prefix |= s_bin << shifts[p];
-      mask |= (uint32_t)(nb - 1) << shifts[p];
-      last_count = s_bincount;
-      __syncthreads();
-    }
-    const uint32_t ustar = prefix;
-    uint32_t id_thr = 0xffffffffu;  // ties at ustar with index <= id_thr are taken
-    if (kleft < last_count) {
-      uint32_t iprefix = 0, imask = 0, kl2 = kleft;
-      for (int p = 0; p < 3; ++p) {
-        const int nb = 1 << bits[p];
-        for (int b = tid; b < nb; b += kTkThreads) hist[b] = 0;
-        __syncthreads();
-        for (int64_t i = tid; i < n; i += kTkThreads) {
-          const uint32_t key2 = ~(uint32_t)i;
-          if (f2u(x[i]) == ustar && (key2 & imask) == iprefix)
-            atomicAdd(&hist[(key2 >> shifts[p]) & (nb - 1)], 1u);
-        }
-        __syncthreads();
-        if (wave == 0) find_bin(hist, nb, kl2, &s_bin, &s_above, &s_bincount);
-        __syncthreads();
-        kl2 -= s_above;
-        iprefix |= s_bin << shifts[p];
-        imask |= (uint32_t)(nb - 1) << shifts[p];
-        __syncthreads();
-      }
-      id_thr = ~iprefix;
-    }
-    if (tid == 0) s_cnt = 0;
+// ---------------------------------------------------------------------------
+// Sampled top-k for long rows (n >= kSampledMinN), two launches:
+//  1. topk_filter_kernel, grid (S splits, B rows): every workgroup of a row
+//     derives the SAME threshold t = the m-th largest key of a fixed strided
+//     sample (m sized for ~8k expected survivors), then streams its 1/S of the
+//     row once and appends every element with key >= t to the row's candidate
+//     list (one global atomic per survivor).
+//  2. topk_select_kernel, one workgroup per row: if count(key >= t) is in
+//     [k, capacity] the top-k are exactly the top-k of the candidates (every
+//     element >= the k-th largest is >= t), sorted in LDS; otherwise the row
+//     falls back to the exact full-row radix select.  Results are identical to
+//     topk_rows_kernel in every case.
+// ---------------------------------------------------------------------------
+constexpr int kSampleN = 8192;
+constexpr int kCandCap = 8192;
+constexpr int64_t kSampledMinN = 65536;
+
+__global__ __launch_bounds__(256) void topk_filter_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
+                                                          int k, uint32_t* __restrict__ cnt,
+                                                          uint64_t* __restrict__ cand) {
+  __shared__ uint32_t skeys[kSampleN];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_bin, s_above, s_bincount;
+  const int tid = threadIdx.x;
+  const int row = blockIdx.y;
+  const float* x = scores + (size_t)row * ld;
+  const int64_t stride = n / kSampleN;
+  for (int j = tid; j < kSampleN; j += 256) skeys[j] = f2u(x[(int64_t)j * stride]);
+  int64_t m64 = (8LL * k * kSampleN + n - 1) / n;
+  const uint32_t m = (uint32_t)(m64 < 1 ? 1 : (m64 > kSampleN ? kSampleN : m64));
+  uint32_t prefix = 0, mask = 0, kleft = m;
+  for (int p = 0; p < 4; ++p) {
+    const int shift = 24 - 8 * p;
+    hist[tid] = 0;
     __syncthreads();
-    for (int64_t i = tid; i < n; i += kTkThreads) {
-      const uint32_t u = f2u(x[i]);
-      if (u > ustar || (u == ustar && (uint32_t)i <= id_thr)) {
-        const uint32_t pos = atomicAdd(&s_cnt, 1u);
-        if (pos < (uint32_t)kTopkMax) sel[pos] = ((uint64_t)u << 32) | (uint32_t)(~(uint32_t)i);
+    for (int j = tid; j < kSampleN; j += 256) {
+      const uint32_t u = skeys[j];
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) find_bin(hist, 256, kleft, &s_bin, &s_above, &s_bincount);
+    __syncthreads();
+    kleft -= s_above;
+    prefix |= s_bin << shift;
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  const uint32_t t = prefix;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t a = (int64_t)blockIdx.x * per;
+  const int64_t b = (a + per < n) ? a + per : n;
+  uint64_t* crow = cand + (size_t)row * kCandCap;
+  for (int64_t i = a + tid; i < b; i += 4 * 256) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (i + u * 256 < b) ? x[i + u * 256] : neg_inf();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t key = f2u(v[u]);
+      if (i + u * 256 < b && key >= t) {
+        const uint32_t pos = atomicAdd(&cnt[row], 1u);
+        if (pos < (uint32_t)kCandCap) crow[pos] = ((uint64_t)key << 32) | (uint32_t)(~(uint32_t)(i + u * 256));
       }
     }
   }
-  __syncthreads();
-  int P = 1;
-  while (P < kk) P <<= 1;
-  for (int i = kk + tid; i < P; i += kTkThreads) sel[i] = 0;
-  bitonic_desc(sel, P);
-  for (int j = tid; j < k; j += kTkThreads) {
-    float s = neg_inf();
-    int32_t id = -1;
-    if (j < kk) {
-      const uint64_t key = sel[j];
-      s = u2f((uint32_t)(key >> 32));
-      id = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
-    }
-    out_s[(size_t)blockIdx.x * k + j] = s;
-    out_i[(size_t)blockIdx.x * k + j] = id;
+}
+
+__global__ __launch_bounds__(kTkThreads) void topk_select_kernel(const float* __restrict__ scores, int64_t n,
+                                                                 int64_t ld, int k, int64_t id_base,
+                                                                 const uint32_t* __restrict__ cnt,
+                                                                 const uint64_t* __restrict__ cand,
+                                                                 float* __restrict__ out_s,
+                                                                 int32_t* __restrict__ out_i) {
+  __shared__ uint64_t sel[kCandCap];
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+  const int row = blockIdx.x;
+  const int kk = (int)((int64_t)k < n ? k : n);
+  const uint32_t c = cnt[row];
+  int m = kk;
+  if (c >= (uint32_t)kk && c <= (uint32_t)kCandCap) {
+    const uint64_t* crow = cand + (size_t)row * kCandCap;
+    for (uint32_t i = threadIdx.x; i < c; i += kTkThreads) sel[i] = crow[i];
+    __syncthreads();
+    m = (int)c;
+  } else {
+    topk_exact_row(scores + (size_t)row * ld, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
   }
+  sort_and_write(sel, m, k, id_base, out_s + (size_t)row * k, out_i + (size_t)row * k);
 }
 
 // ---------------------------------------------------------------------------
@@ -946,6 +1049,9 @@ enum ScanVariant {
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
 // 1: 58.3 %, 2: 61.7 %, 3: 65.3 %, 4: 59.4 %, 5: 52.0 %, 6: 61.2 %, 8: 54.8 %
 // of the bf16 dense peak.  rerank_kernel uses the same 16x16 math as 2/3/5-8.
+// Tried and dropped: a 3-buffer variant that reads the next doc's first tile
+// under the current doc's last MFMAs (carried fragments push the loop past 256
+// VGPRs; hipcc spills the query fragments: 12 % of peak).
 constexpr int kDefaultScan = kScanAuto;
 // Auto dispatch (measured, 1M docs, tools/scan_lab.py): B<=8 direct scan
 // (B=1: 5.0 ms = 6.5 TB/s of doc bytes; B=8: 13.7 ms vs 18.4 ms for the LDS
@@ -1052,11 +1158,47 @@ int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t
   return scan_meanpool(ix, (const float*)Q, B, lq, out, ld_out, st);
 }
 
-int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, float* out_s,
-              int32_t* out_i, hipStream_t st) {
-  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
-                     out_s, out_i);
-  return launch_check("topk_rows_kernel");
+__global__ void fill_empty_kernel(float* out_s, int32_t* out_i, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < total) {
+    out_s[i] = neg_inf();
+    out_i[i] = -1;
+  }
+}
+
+int topk_impl_empty(int32_t B, int32_t k, float* out_s, int32_t* out_i, hipStream_t st) {
+  const int64_t total = (int64_t)B * k;
+  hipLaunchKernelGGL(fill_empty_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, out_s, out_i, total);
+  return launch_check("fill_empty_kernel");
+}
+
+size_t topk_ws_bytes(int32_t B, int64_t n) {
+  if (n < kSampledMinN) return 0;
+  return (size_t)B * kCandCap * sizeof(uint64_t) + (((size_t)B * sizeof(uint32_t) + 255) & ~(size_t)255);
+}
+
+int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, void* ws,
+              size_t ws_bytes, float* out_s, int32_t* out_i, hipStream_t st, int dev) {
+  const size_t need = topk_ws_bytes(B, n);
+  if (need == 0 || ws == nullptr || ws_bytes < need) {
+    hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
+                       out_s, out_i);
+    return launch_check("topk_rows_kernel");
+  }
+  uint64_t* cand = (uint64_t*)ws;
+  uint32_t* cnt = (uint32_t*)((uint8_t*)ws + (size_t)B * kCandCap * sizeof(uint64_t));
+  CBV2_HIP(hipMemsetAsync(cnt, 0, (size_t)B * sizeof(uint32_t), st));
+  int64_t splits = (2LL * cu_count(dev) + B - 1) / B;
+  const int64_t max_splits = n / 16384;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  hipLaunchKernelGGL(topk_filter_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, scores, n, ld, k, cnt,
+                     cand);
+  int rc = launch_check("topk_filter_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(topk_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base, cnt,
+                     cand, out_s, out_i);
+  return launch_check("topk_select_kernel");
 }
 }  // namespace
 
@@ -1122,7 +1264,7 @@ int cbv2_score(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, i
 
 size_t cbv2_search_workspace_bytes(const cbv2_index* ix, int32_t B) {
   if (!ix || B < 1) return 0;
-  return (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
+  return topk_ws_bytes(B, ix->n) + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
 }
 
 int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
@@ -1138,10 +1280,12 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
   hipStream_t st = (hipStream_t)stream;
-  float* ws = (float*)workspace;
-  rc = score_impl(ix, scorer, Q, B, lq, ws, ix->n, st);
+  if (ix->n == 0) return topk_impl_empty(B, k, out_scores, out_ids, st);
+  const size_t tk = topk_ws_bytes(B, ix->n);
+  float* sc = (float*)((uint8_t*)workspace + tk);
+  rc = score_impl(ix, scorer, Q, B, lq, sc, ix->n, st);
   if (rc) return rc;
-  return topk_impl(ws, B, ix->n, ix->n, k, ix->id_base, out_scores, out_ids, st);
+  return topk_impl(sc, B, ix->n, ix->n, k, ix->id_base, workspace, tk, out_scores, out_ids, st, ix->device);
 }
 
 int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
@@ -1172,15 +1316,20 @@ int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t
   return launch_check("select_small_kernel");
 }
 
+size_t cbv2_topk_workspace_bytes(int32_t B, int64_t n) { return B >= 1 && n >= 1 ? topk_ws_bytes(B, n) : 0; }
+
 int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base,
-                   float* out_scores, int32_t* out_ids, void* stream) {
+                   void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids, void* stream) {
   CBV2_REQUIRE(scores && out_scores && out_ids, "null pointer");
   CBV2_REQUIRE(B >= 1, "B must be >= 1");
   CBV2_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "n out of range");
   CBV2_REQUIRE(ld >= n, "ld < n");
   CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
   CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "ids must fit int32");
-  return topk_impl(scores, B, n, ld, k, id_base, out_scores, out_ids, (hipStream_t)stream);
+  int dev = 0;
+  CBV2_HIP(hipGetDevice(&dev));
+  return topk_impl(scores, B, n, ld, k, id_base, workspace, workspace_bytes, out_scores, out_ids,
+                   (hipStream_t)stream, dev);
 }
 
 int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,

@@ -231,8 +231,10 @@ def select_topk(scores: torch.Tensor, k: int, ids: Optional[torch.Tensor] = None
     return out_s, out_i, out_p
 
 
-def topk_rows(scores: torch.Tensor, k: int, id_base: int = 0):
-    """Top-k of each row of a [B, n] score matrix (exact; ties -> lower index)."""
+def topk_rows(scores: torch.Tensor, k: int, id_base: int = 0, sampled: bool = True):
+    """Top-k of each row of a [B, n] score matrix (exact; ties -> lower index).
+
+    ``sampled`` lets long rows use the threshold-filter path (same result)."""
     _require_cuda(scores, "scores")
     if scores.dim() == 1:
         scores = scores.unsqueeze(0)
@@ -243,8 +245,11 @@ def topk_rows(scores: torch.Tensor, k: int, id_base: int = 0):
     dev = scores.device
     out_s = torch.empty((B, k), dtype=torch.float32, device=dev)
     out_i = torch.empty((B, k), dtype=torch.int32, device=dev)
+    need = int(_lib.lib().cbv2_topk_workspace_bytes(B, n)) if sampled else 0
+    ws = torch.empty((max(need, 1),), dtype=torch.uint8, device=dev)
     _lib.check(_lib.lib().cbv2_topk_rows(scores.data_ptr(), B, n, scores.stride(0), int(k), int(id_base),
-                                         out_s.data_ptr(), out_i.data_ptr(), _stream_ptr(dev)))
+                                         ws.data_ptr() if need else None, need, out_s.data_ptr(),
+                                         out_i.data_ptr(), _stream_ptr(dev)))
     return out_s, out_i
 
 

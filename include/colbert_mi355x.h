@@ -120,9 +120,15 @@ int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t
                      float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
 
 /* cbv2_topk_rows — top-k of each row of a large score matrix scores[b*ld + i],
- * i < n (radix select, then bitonic sort).  ids written = id_base + i.      */
+ * i < n; ids written = id_base + i.  With a workspace of
+ * cbv2_topk_workspace_bytes(B, n) bytes (0 for short rows) long rows use the
+ * sampled-threshold filter + candidate sort; with workspace NULL, or on a
+ * candidate overflow, the exact single-pass-per-digit radix select.  The
+ * result is identical either way.                                          */
+size_t cbv2_topk_workspace_bytes(int32_t B, int64_t n);
 int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k,
-                   int64_t id_base, float* out_scores, int32_t* out_ids, void* stream);
+                   int64_t id_base, void* workspace, size_t workspace_bytes,
+                   float* out_scores, int32_t* out_ids, void* stream);
 
 /* cbv2_merge_topk — merge G per-shard sorted top-k lists ([G][B][k] scores and
  * global ids, e.g. after an RCCL all-gather) into the global top-k [B][k].

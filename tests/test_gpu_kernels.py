@@ -267,3 +267,28 @@ def test_small_batch_scan_bit_identical_to_batched(dev):
     s1, i1 = ix.search(Q[:1].to(dev), k=30)
     s, i = ix.search(Q.to(dev), k=30)
     assert torch.equal(i1[0], i[0]) and torch.equal(s1[0], s[0])
+
+
+@pytest.mark.parametrize("dist", ["normal", "ints", "const", "spike", "neg"])
+@pytest.mark.parametrize("n,k", [(65536, 100), (300000, 100), (1000000, 10), (200000, 1024)])
+def test_sampled_topk_equals_exact(dev, dist, n, k):
+    """The threshold-filter top-k path (long rows) == exact radix select == oracle."""
+    g = torch.Generator(device=dev).manual_seed(n + k)
+    B = 3
+    if dist == "normal":
+        x = torch.randn(B, n, device=dev, generator=g)
+    elif dist == "ints":       # massive ties -> candidate overflow -> exact fallback
+        x = torch.randint(-3, 4, (B, n), device=dev, generator=g).float()
+    elif dist == "const":
+        x = torch.zeros(B, n, device=dev)
+    elif dist == "spike":      # a few huge values: count(>= t) may be < k -> fallback
+        x = torch.randn(B, n, device=dev, generator=g) * 1e-3
+        x[:, ::50000] = 100.0
+    else:
+        x = -torch.rand(B, n, device=dev, generator=g) - 1.0
+    s1, i1 = topk_rows(x, k, sampled=True)
+    s0, i0 = topk_rows(x, k, sampled=False)
+    assert torch.equal(i1, i0) and torch.equal(s1, s0)
+    if n <= 300000:
+        rs, ri = orc.topk(x.cpu().numpy(), k)
+        assert np.array_equal(i1.cpu().numpy(), ri)

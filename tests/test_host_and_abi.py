@@ -36,7 +36,7 @@ def test_validation_errors_without_gpu(L):
     assert L.cbv2_index_create(0, None, 1, 10, 64, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
     assert L.cbv2_index_create(0, None, 1, -1, 128, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EINVAL
     assert L.cbv2_index_create(0, None, 1, 10, 128, 128, None, 0, None) == _lib.ERR_EINVAL
-    assert L.cbv2_topk_rows(None, 1, 10, 10, 5, 0, None, None, None) == _lib.ERR_EINVAL
+    assert L.cbv2_topk_rows(None, 1, 10, 10, 5, 0, None, 0, None, None, None) == _lib.ERR_EINVAL
     assert L.cbv2_select_topk(ctypes.c_void_p(16), None, 1, 10, 0, ctypes.c_void_p(16), None, None, None) \
         == _lib.ERR_EINVAL
     assert L.cbv2_merge_topk(ctypes.c_void_p(16), ctypes.c_void_p(16), 65, 1, 10, ctypes.c_void_p(16),
