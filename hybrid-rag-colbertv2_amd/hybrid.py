@@ -247,3 +247,70 @@ class HybridRetriever:
         cand_d = torch.from_numpy(cand).pin_memory().to(retr.device, non_blocking=True)
         s, i, _ = retr.rerank_ids(Q, cand_d, k_final)
         return s, i
+
+
+# ---------------------------------------------------------------------- pipelined batches
+class PipelinedRetriever:
+    """Software-pipelined three-stage retrieval over a stream of query batches.
+
+    The host step in the middle of the path (RRF fusion of the stage-2 ids,
+    LRC:960-978) would otherwise idle the GPU once per batch.  Here batch j+1's
+    stage-2 scan is enqueued BEFORE the host fuses batch j, so the GPU scans
+    while the host fuses:
+
+        GPU main stream:  scan(j) | scan(j+1) | rerank(j) | scan(j+2) | rerank(j+1) ...
+        GPU side stream:  D2H ids(j) (after scan(j) only)
+        host:                       fuse(j) -> H2D cand(j)
+
+    ``searcher`` is anything with ``search(Q, k)`` and ``rerank(Q, cand, k)``:
+    a ``ColbertIndex`` or a ``distributed.ShardedSearcher`` (the collectives
+    are issued in the same order on every rank).  Results per batch are exactly
+    those of the unpipelined path.
+    """
+
+    def __init__(self, searcher, device, colbert_k: int = 100, fused: int = 50, final_k: int = 10,
+                 rrf_k: int = 60):
+        self.searcher, self.device = searcher, torch.device(device)
+        self.k, self.fused, self.final_k, self.rrf_k = colbert_k, fused, final_k, rrf_k
+        self.side = torch.cuda.Stream(self.device)
+        self._ids_h = None
+        self._cand_h = [None, None]
+
+    def _host_buffers(self, B: int):
+        if self._ids_h is None or self._ids_h.shape[0] < B:
+            self._ids_h = torch.empty((B, self.k), dtype=torch.int32, pin_memory=True)
+            self._cand_h = [torch.empty((B, self.fused), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+
+    def run(self, batches):
+        """batches: sequence of (Q [B, lq, D] device, bm25_ids [B, kb] host).  Returns [(scores, ids)]."""
+        batches = list(batches)
+        if not batches:
+            return []
+        main = torch.cuda.current_stream(self.device)
+        self._host_buffers(max(q.shape[0] for q, _ in batches))
+        out = []
+        _, ids = self.searcher.search(batches[0][0], self.k)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for j, (Q, bm) in enumerate(batches):
+            B = Q.shape[0]
+            if j + 1 < len(batches):                       # keep the GPU busy during the host step
+                _, nxt_ids = self.searcher.search(batches[j + 1][0], self.k)
+                nxt_ev = torch.cuda.Event()
+                nxt_ev.record(main)
+            ids_h = self._ids_h[:B]
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(ev)
+                ids.record_stream(self.side)
+                ids_h.copy_(ids, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(self.side)
+            done.synchronize()
+            cand = self._cand_h[j & 1][:B]
+            cand.numpy()[:] = rrf_fuse(bm, ids_h.numpy(), rrf_k=self.rrf_k, C=self.fused)
+            cand_d = cand.to(self.device, non_blocking=True)
+            s, i, _ = self.searcher.rerank(Q, cand_d, self.final_k)
+            out.append((s, i))
+            if j + 1 < len(batches):
+                ids, ev = nxt_ids, nxt_ev
+        return out

@@ -166,3 +166,24 @@ def test_sharded_searcher_single_process(dev):
     r1 = ss.rerank(Q, cand, 3)
     r2 = ix.rerank(Q, cand, 3)
     assert all(torch.equal(x, y) for x, y in zip(r1, r2))
+
+
+def test_pipelined_batches_equal_unpipelined(dev):
+    """PipelinedRetriever overlaps batch j+1's scan with batch j's host fusion;
+    every batch's result must equal the plain sequential path."""
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.hybrid import PipelinedRetriever, rrf_fuse
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    N = 20000
+    Qall = synth.make_queries(48, seed=5)
+    planted = synth.planted_ids(48, N, 10)
+    tokens, doclens = synth.make_shard(0, N, Qall, planted, dev)
+    ix = ColbertIndex(tokens, doclens)
+    bm = synth.bm25_lists(48, N, planted)
+    batches = [(Qall[a:b].to(dev, torch.bfloat16), bm[a:b]) for a, b in [(0, 16), (16, 17), (17, 40), (40, 48)]]
+    got = PipelinedRetriever(ix, dev).run(batches)
+    for (Q, b), (s, i) in zip(batches, got):
+        _, ids = ix.search(Q, 100)
+        cand = torch.from_numpy(rrf_fuse(b, ids.cpu().numpy())).to(dev)
+        es, ei, _ = ix.rerank(Q, cand, 10)
+        assert torch.equal(i, ei) and torch.equal(s, es)
