@@ -40,9 +40,10 @@ sys.path.insert(0, ROOT)
 from hybrid_rag_colbertv2_amd import synth  # noqa: E402
 from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range  # noqa: E402
 from hybrid_rag_colbertv2_amd.hybrid import PipelinedRetriever, rrf_fuse  # noqa: E402
-from hybrid_rag_colbertv2_amd.index import ColbertIndex  # noqa: E402
+from hybrid_rag_colbertv2_amd.index import ColbertIndex, quantize_mxfp8  # noqa: E402
 
 LQ, LD, DIM = 32, 128, 128
+PEAK_FP8_TFLOPS = 5000.0                   # MI355X dense fp8 (block-scaled MFMA)
 FLOP_PER_PAIR = 2 * LQ * LD * DIM          # 1,048,576 algorithmic FLOP per (query, doc)
 PEAK_BF16_TFLOPS = 2500.0                  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
@@ -94,6 +95,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check-queries", type=int, default=4)
     ap.add_argument("--no-pipeline", action="store_true", help="time unpipelined steps")
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="index tokens: bf16 (config 3) or MXFP8 e4m3 + E8M0 (config 5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,7 +122,11 @@ def main():
     planted = synth.planted_ids(B, n_total, 10, seed=2)
     bm25 = synth.bm25_lists(B, n_total, planted, k=args.k, seed=3)
     tokens, doclens = synth.make_shard(begin, end, Qf, planted, dev, seed=0)
-    ix = ColbertIndex(tokens, doclens, id_base=begin)
+    if args.dtype == "fp8":
+        ix = ColbertIndex.mxfp8(tokens, doclens, id_base=begin)   # quantized on the GPU (HIP kernel)
+        tokens_ref = tokens                                          # kept only for the spot parity check
+    else:
+        ix = ColbertIndex(tokens, doclens, id_base=begin)
     searcher = ShardedSearcher(ix)
     Q = Qf.to(dev, torch.bfloat16)
     Q1 = Q[:1].contiguous()
@@ -195,7 +202,8 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             d = json.load(f)
-        if d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == SCAN_KERNEL:
+        if d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == (
+                "maxsim_scan_f8_kernel" if args.dtype == "fp8" else SCAN_KERNEL):
             traffic = d.get("hbm_bytes_per_launch")
 
     # ---- spot parity: oracle MaxSim of the final candidates for a few queries
@@ -205,30 +213,43 @@ def main():
         ids_b = [int(x) for x in fi_h[b] if begin <= x < end]
         if world > 1 or not ids_b:
             continue
-        d = tokens[torch.tensor(ids_b, device=dev) - begin].float().cpu().numpy()
-        ref = orc.maxsim(Q[b:b + 1].float().cpu().numpy(), d)[0]
+        sel = torch.tensor(ids_b, device=dev) - begin
+        if args.dtype == "fp8":          # the oracle scores the same dequantized fp8 values
+            d = orc.mxfp8_dequant(ix.tokens[sel].cpu().numpy(), ix.scales[sel].cpu().numpy())
+            qq, qs = quantize_mxfp8(Q[b:b + 1])
+            qd = orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy())
+            tol = 2e-3
+        else:
+            d = tokens[sel].float().cpu().numpy()
+            qd = Q[b:b + 1].float().cpu().numpy()
+            tol = 1e-3
+        ref = orc.maxsim(qd, d)[0]
         got = fs[b, : len(ids_b)].cpu().numpy()
-        bad += int(np.abs(got - ref).max() > 1e-3)
+        bad += int(np.abs(got - ref).max() > tol)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(Q, tokens, n_total, args.cpu_budget)
 
+    fp8 = args.dtype == "fp8"
+    peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
+    kern = "maxsim_scan_f8_kernel" if fp8 else SCAN_KERNEL
     if rank == 0:
         line = {
             "metric": "queries/sec + p50 retrieval latency, 1M-chunk corpus, top-10 rerank",
             "value": round(qps, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (unit-norm N(0,I) tokens, 10 planted positives/query, synthetic BM25 lists)",
-            "config": {"workload": "config 3: 1M chunks x 128 tokens x 128-d, BM25 top-100 (precomputed) + "
+            "config": {"workload": ("config 5 (MXFP8 e4m3 tokens, block-scaled fp8 MFMA)" if fp8 else "config 3") +
+                                   f": {n_total} chunks x 128 tokens x 128-d, BM25 top-100 (precomputed) + "
                                    "ColBERT MaxSim top-100 + RRF + rerank top-10",
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
                        "parallelism": f"corpus sharded x{world}" + (" (RCCL all-gather + all-reduce)" if world > 1 else "")},
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
-            "roofline": {"bound": "mfma", "kernel": SCAN_KERNEL, "achieved": round(achieved, 2),
-                         "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "kernel": kern, "achieved": round(achieved, 2),
+                         "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic, "avg_ms": round(scan_avg, 3)},
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad},

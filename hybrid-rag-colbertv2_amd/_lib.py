@@ -16,6 +16,7 @@ HEADER = os.path.join(os.path.dirname(PKG), "include", "colbert_mi355x.h")
 
 DTYPE_BF16 = 1
 DTYPE_F32 = 2
+DTYPE_MXFP8 = 3
 SCORER_MAXSIM = 0
 SCORER_REF_MEANPOOL_COSINE = 1
 SCORERS = {"maxsim": SCORER_MAXSIM, "ref_meanpool_cosine": SCORER_REF_MEANPOOL_COSINE}
@@ -28,6 +29,9 @@ _SIGS = {
     "cbv2_index_create": (ctypes.c_int, [ctypes.c_int, _p, _i32, _i64, _i32, _i32, _p, _i64,
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_index_destroy": (ctypes.c_int, [_p]),
+    "cbv2_index_create_mxfp8": (ctypes.c_int, [ctypes.c_int, _p, _p, _i64, _i32, _i32, _p, _i64,
+                                               ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_quantize_mxfp8": (ctypes.c_int, [_p, _i32, _i64, _p, _p, _p]),
     "cbv2_index_build_means": (ctypes.c_int, [_p, _p, _i32, _p, _p]),
     "cbv2_score": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _p, _i64, _p]),
     "cbv2_search_workspace_bytes": (_sz, [_p, _i32]),

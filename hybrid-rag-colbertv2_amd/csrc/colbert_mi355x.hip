@@ -515,6 +515,294 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_direct_kernel(
   }
 }
 
+// ===========================================================================
+// MXFP8 path (config 5): doc and query tokens as e4m3 bytes with one E8M0
+// power-of-two scale per token per 64 dims, scored on the block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate on gfx950).
+// Operand map (verified on MI355X by tools/probes/mx_probe{2,3,4}.hip):
+//   lane l (c = l&15, g = l>>4) holds 32 bytes = K range [32g, 32g+32) of
+//   row/column c; lane c + 16h (h = 0, 1) supplies byte 0 of its scale VGPR
+//   for K range [64h, 64h+64) of row/column c; lanes 32..63's scales are unused.
+// One MFMA covers the whole 128-dim contraction of a 16x16 token tile.
+// ===========================================================================
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+constexpr int kF8DocBytes = kLd * kDim;            // 16 KiB of e4m3 per doc
+constexpr int kF8ScaleBytes = kLd * 2;             // 256 B of E8M0 per doc
+constexpr int kF8Stage = kF8DocBytes + kF8ScaleBytes;
+
+// LDS image of a doc: 128 rows x 8 slots of 16 B, slot s of row t stored at
+// s ^ swz8(t) (conflict-free for the two ds_read_b128 of a fragment), then the
+// 256 scale bytes.
+__device__ __forceinline__ int swz8(int t) { return (((t >> 1) & 1) << 2) | ((t >> 2) & 1); }
+
+// E8M0 exponent for a half-row with max magnitude m: smallest e with m <= 448 * 2^e.
+__device__ __forceinline__ int mx_exp(float m) {
+  if (!(m > 0.0f)) return 0;
+  int p;
+  const float f = frexpf(m, &p);  // m = f * 2^p, f in [0.5, 1); 448 = 0.875 * 2^9
+  int e = (f <= 0.875f) ? p - 9 : p - 8;
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+template <typename T>
+__device__ __forceinline__ float to_f32(T v);
+template <>
+__device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ float to_f32<uint16_t>(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+template <typename T>
+__device__ __forceinline__ void quantize_row(const T* __restrict__ x, int64_t row, int lane, uint8_t* __restrict__ q,
+                                             uint8_t* __restrict__ sc);
+
+// One wave per 128-value row: bytes q[row][128] (e4m3, RNE) and scales[row][2].
+template <typename T>
+__global__ __launch_bounds__(256) void quantize_mxfp8_kernel(const T* __restrict__ x, int64_t rows,
+                                                             uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
+  const int lane = threadIdx.x & 63;
+  // grid-stride over rows: a dispatch's grid is a 32-bit work-item count
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4)
+    quantize_row<T>(x, row, lane, q, sc);
+}
+
+template <typename T>
+__device__ __forceinline__ void quantize_row(const T* __restrict__ x, int64_t row, int lane, uint8_t* __restrict__ q,
+                                             uint8_t* __restrict__ sc) {
+  const float a = to_f32<T>(x[row * kDim + 2 * lane]);
+  const float b = to_f32<T>(x[row * kDim + 2 * lane + 1]);
+  float m = fmaxf(fabsf(a), fabsf(b));
+  m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, true)));
+  m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, true)));
+  m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x141, 0xF, 0xF, true)));
+  m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x140, 0xF, 0xF, true)));
+  m = fold16_max(m);  // max over the 32 lanes of this half (dims 64h .. 64h+63)
+  const int e = mx_exp(m);
+  const int packed = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(a, -e), ldexpf(b, -e), 0, false);
+  *reinterpret_cast<uint16_t*>(q + row * kDim + 2 * lane) = (uint16_t)(packed & 0xffff);
+  if ((lane & 31) == 0) sc[row * 2 + (lane >> 5)] = (uint8_t)(127 + e);
+}
+
+// Query fragments for the f8 tiling: 32 bytes + the scale byte of half g&1.
+__device__ __forceinline__ void load_qfrag_f8(const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int qi,
+                                              int B, int lq, int lane, i32x8 (&qa)[2], int (&qs)[2]) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int tok = 16 * ct + c;
+    const bool ok = (qi < B) && (tok < lq);
+    const size_t row = ok ? (size_t)qi * lq + tok : 0;
+    const i32x8* src = reinterpret_cast<const i32x8*>(Qb + row * kDim + 32 * g);
+    qa[ct] = ok ? *src : i32x8{0, 0, 0, 0, 0, 0, 0, 0};
+    qs[ct] = ok ? (int)Qs[row * 2 + (g & 1)] : 127;
+  }
+}
+
+__device__ __forceinline__ void lds_afrag_f8(const uint8_t* buf, int rt, int lane, i32x8& a, int& as) {
+  const int c = lane & 15, g = lane >> 4;
+  const int t = 16 * rt + c;
+  const uint8_t* row = buf + t * kDim;
+  const int sw = swz8(t);
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g) ^ sw));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g + 1) ^ sw));
+  a = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  as = buf[kF8DocBytes + t * 2 + (g & 1)];
+}
+
+__device__ __forceinline__ void gbl_afrag_f8(const uint8_t* doc, const uint8_t* dsc, int rt, int lane, i32x8& a,
+                                             int& as) {
+  const int c = lane & 15, g = lane >> 4;
+  const int t = 16 * rt + c;
+  a = *reinterpret_cast<const i32x8*>(doc + t * kDim + 32 * g);
+  as = dsc[t * 2 + (g & 1)];
+}
+
+template <int QW>
+__device__ __forceinline__ void tile_f8(const i32x8& a, int as, const i32x8 (&qa)[QW][2], const int (&qs)[QW][2],
+                                        const f32x4& init, float (&m)[QW][2]) {
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const f32x4 acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, qa[q][ct], init, 0, 0, 0, as, 0, qs[q][ct]);
+      m[q][ct] = fmaxf(fmaxf(m[q][ct], fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
+    }
+  }
+}
+
+// Whole (query, doc) pass of the f8 tiling; FRAG(rt, a, as) loads row tile rt.
+template <int QW, typename Frag>
+__device__ __forceinline__ void doc_f8(Frag frag, const i32x8 (&qa)[QW][2], const int (&qs)[QW][2], int dl, int lane,
+                                       float (&m)[QW][2]) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+  if (dl >= kLd) {
+    i32x8 a0, a1;
+    int s0, s1;
+    frag(0, a0, s0);
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; rt += 2) {
+      frag(rt + 1, a1, s1);
+      tile_f8<QW>(a0, s0, qa, qs, f32x4{}, m);
+      if (rt + 2 < kLd / 16) frag(rt + 2, a0, s0);
+      tile_f8<QW>(a1, s1, qa, qs, f32x4{}, m);
+    }
+    return;
+  }
+  const int nrt = (dl + 15) >> 4;
+  for (int rt = 0; rt < nrt; ++rt) {
+    i32x8 a;
+    int as;
+    frag(rt, a, as);
+    const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+    tile_f8<QW>(a, as, qa, qs, init, m);
+  }
+}
+
+// LDS-staged f8 scan: 8 waves x 8 queries = 64 queries per workgroup.
+template <int WAVES, int QW>
+__global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8_kernel(
+    const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
+    int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
+    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs) {
+  constexpr int QPB = WAVES * QW;
+  constexpr int kPieces = kF8DocBytes / 1024;
+  constexpr int kPiecesPerWave = kPieces / WAVES;
+  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * kF8Stage + 256];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int g = lin % nq_groups;
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;
+  const int nd = (int)(d_end - d_begin);
+
+  i32x8 qa[QW][2];
+  int qs[QW][2];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, g * QPB + wave * QW + q, B, lq, lane, qa[q], qs[q]);
+
+  uint32_t src_off[kPiecesPerWave];
+#pragma unroll
+  for (int j = 0; j < kPiecesPerWave; ++j) {
+    const int piece = wave * kPiecesPerWave + j;
+    const int t = 8 * piece + (lane >> 3);
+    src_off[j] = t * kDim + 16 * ((lane & 7) ^ swz8(t));
+  }
+  auto issue = [&](int i, int buf) {
+    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kF8DocBytes;
+    uint8_t* sbuf = smem + buf * kF8Stage;
+#pragma unroll
+    for (int j = 0; j < kPiecesPerWave; ++j) {
+      const int piece = wave * kPiecesPerWave + j;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(dbase + src_off[j]), (lds_void_t*)(sbuf + piece * 1024), 16, 0,
+                                       0);
+    }
+    if (wave == 0)  // the doc's 256 scale bytes: one dword per lane
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(tscales + (size_t)(d_begin + i) * kF8ScaleBytes + 4 * lane),
+                                       (lds_void_t*)(sbuf + kF8DocBytes), 4, 0, 0);
+  };
+
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+
+  issue(0, 0);
+  for (int i = 0; i < nd; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i + 1 < nd) issue(i + 1, (i + 1) & 1);
+    const uint8_t* buf = smem + (i & 1) * kF8Stage;
+    int dl = doclens[d_begin + i];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    float m[QW][2];
+    doc_f8<QW>([&](int rt, i32x8& a, int& as) { lds_afrag_f8(buf, rt, lane, a, as); }, qa, qs, dl, lane, m);
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = g * QPB + wave * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
+// Small-batch f8 scan: one doc chunk per wave, docs streamed to VGPRs.
+template <int QW>
+__global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
+    const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
+    int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
+    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t lin = (int64_t)blockIdx.x * 4 + wave;
+  const int qg = (int)(lin % nq_groups);
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;
+  const int nd = (int)(d_end - d_begin);
+  i32x8 qa[QW][2];
+  int qs[QW][2];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, qg * QW + q, B, lq, lane, qa[q], qs[q]);
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+  for (int i = 0; i < nd; ++i) {
+    int dl = doclens[d_begin + i];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kF8DocBytes;
+    const uint8_t* dsc = tscales + (size_t)(d_begin + i) * kF8ScaleBytes;
+    i32x8 af[kLd / 16];
+    int as[kLd / 16];
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt)
+      if (16 * rt < dl) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+    float m[QW][2];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt) {
+      if (16 * rt < dl) {
+        const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+        tile_f8<QW>(af[rt], as[rt], qa, qs, init, m);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = qg * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Row top-k: exact radix select (11/11/10-bit digits of the order-preserving
 // score key; if the k-th score is tied, a second radix select over ~index picks
@@ -855,6 +1143,59 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
                   out_p ? out_p + (size_t)b * k : nullptr);
 }
 
+
+__global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
+    const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
+    int64_t n, int64_t id_base, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int lq,
+    const int32_t* __restrict__ cand, int C, int k, float* __restrict__ out_s, int32_t* __restrict__ out_i,
+    int32_t* __restrict__ out_p) {
+  __shared__ float sc[kSmallMax];
+  __shared__ uint64_t keys[kSmallMax];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x;
+  const int g = lane >> 4;
+  i32x8 qa[1][2];
+  int qs[1][2];
+  load_qfrag_f8(Qb, Qs, b, b + 1, lq, lane, qa[0], qs[0]);
+  const int32_t* crow = cand + (size_t)b * C;
+  for (int c = wave; c < C; c += kRrWaves) {
+    const int32_t id = crow[c];
+    const int64_t loc = (int64_t)id - id_base;
+    float v = neg_inf();
+    if (id >= 0 && loc >= 0 && loc < n) {
+      int dl = doclens[loc];
+      dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+      const uint8_t* dbase = tokens + (size_t)loc * kF8DocBytes;
+      const uint8_t* dsc = tscales + (size_t)loc * kF8ScaleBytes;
+      i32x8 af[kLd / 16];
+      int as[kLd / 16];
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; ++rt)
+        if (16 * rt < dl) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+      float m[1][2] = {{neg_inf(), neg_inf()}};
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; ++rt) {
+        if (16 * rt < dl) {
+          const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+          tile_f8<1>(af[rt], as[rt], qa, qs, init, m);
+        }
+      }
+      v = reduce16(m[0][0], m[0][1], lane, lq);
+    }
+    if (lane == 0) sc[c] = v;
+  }
+  __syncthreads();
+  if (k == 0) {
+    for (int t = threadIdx.x; t < C; t += blockDim.x) out_s[(size_t)b * C + t] = sc[t];
+    return;
+  }
+  for (int t = threadIdx.x; t < C; t += blockDim.x) keys[t] = rank_key(sc[t], (uint32_t)t);
+  __syncthreads();
+  select_from_lds(sc, keys, C, k, crow, out_s + (size_t)b * k, out_i + (size_t)b * k,
+                  out_p ? out_p + (size_t)b * k : nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Merge G sorted per-shard lists: rank = own position + #greater keys in every
 // other list (binary search); ids are unique across shards so ranks are too.
@@ -985,6 +1326,8 @@ struct cbv2_index {
   const int32_t* doclens;
   int64_t id_base;
   const float* doc_means;
+  int32_t dtype;           // CBV2_DTYPE_BF16 or CBV2_DTYPE_MXFP8
+  const uint8_t* scales;   // MXFP8: E8M0 [n][128][2]
 };
 
 namespace {
@@ -1127,6 +1470,41 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
   }
 }
 
+constexpr int kF8DirectMaxB = 8;
+constexpr int kF8Waves = 8, kF8QW = 8;
+
+int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+  if (ix->n == 0) return CBV2_OK;
+  const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+  if (B <= kF8DirectMaxB) {
+    constexpr int QW = 2;
+    const int nq_groups = (B + QW - 1) / QW;
+    const int64_t target_waves = 8LL * cu_count(ix->device);
+    int64_t n_chunks = (target_waves + nq_groups - 1) / nq_groups;
+    if (n_chunks > ix->n) n_chunks = ix->n;
+    if (n_chunks < 1) n_chunks = 1;
+    const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+    n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+    const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
+    hipLaunchKernelGGL(maxsim_scan_f8_direct_kernel<QW>, dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                       ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
+    return launch_check("maxsim_scan_f8_direct_kernel");
+  }
+  constexpr int QPB = kF8Waves * kF8QW;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int64_t target = cu_count(ix->device);
+  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  if (n_chunks < 1) n_chunks = 1;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t grid = (int64_t)nq_groups * n_chunks;
+  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  hipLaunchKernelGGL((maxsim_scan_f8_kernel<kF8Waves, kF8QW>), dim3((unsigned)grid), dim3(kF8Waves * 64), 0, st,
+                     ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
+  return launch_check("maxsim_scan_f8_kernel");
+}
+
 int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
   if (ix->n == 0) return CBV2_OK;
   dim3 grid((unsigned)((ix->n + kMpDocs - 1) / kMpDocs), (unsigned)((B + kMpQ - 1) / kMpQ));
@@ -1141,7 +1519,10 @@ int check_query(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   CBV2_REQUIRE(lq >= 1, "lq must be >= 1 (got %d)", lq);
   CBV2_REQUIRE(aligned16(Q), "query pointer must be 16-byte aligned");
   if (scorer == CBV2_SCORER_MAXSIM) {
-    CBV2_REQUIRE(q_dtype == CBV2_DTYPE_BF16, "maxsim scorer takes bf16 queries");
+    if (ix->dtype == CBV2_DTYPE_MXFP8)
+      CBV2_REQUIRE(q_dtype == CBV2_DTYPE_MXFP8, "an MXFP8 index takes MXFP8 queries (cbv2_quantize_mxfp8)");
+    else
+      CBV2_REQUIRE(q_dtype == CBV2_DTYPE_BF16, "maxsim scorer takes bf16 queries");
     CBV2_REQUIRE(lq <= kLqMax, "maxsim takes at most %d query tokens (got %d)", kLqMax, lq);
   } else if (scorer == CBV2_SCORER_REF_MEANPOOL_COSINE) {
     CBV2_REQUIRE(q_dtype == CBV2_DTYPE_F32, "ref_meanpool_cosine scorer takes f32 queries");
@@ -1154,6 +1535,8 @@ int check_query(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
 
 int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t lq, float* out,
                int64_t ld_out, hipStream_t st) {
+  if (scorer == CBV2_SCORER_MAXSIM && ix->dtype == CBV2_DTYPE_MXFP8)
+    return scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st);
   if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st);
   return scan_meanpool(ix, (const float*)Q, B, lq, out, ld_out, st);
 }
@@ -1180,7 +1563,7 @@ size_t topk_ws_bytes(int32_t B, int64_t n) {
 int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, void* ws,
               size_t ws_bytes, float* out_s, int32_t* out_i, hipStream_t st, int dev) {
   const size_t need = topk_ws_bytes(B, n);
-  if (need == 0 || ws == nullptr || ws_bytes < need) {
+  if (need == 0 || ws == nullptr || ws_bytes < need || B > 65535) {  // grid.y of the filter launch
     hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
                        out_s, out_i);
     return launch_check("topk_rows_kernel");
@@ -1224,9 +1607,49 @@ int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, 
   int ndev = 0;
   CBV2_HIP(hipGetDeviceCount(&ndev));
   CBV2_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
-  cbv2_index* ix = new cbv2_index{device, (const uint8_t*)tokens, n, ld, d, doclens, id_base, nullptr};
+  cbv2_index* ix = new cbv2_index{device, (const uint8_t*)tokens, n, ld, d, doclens, id_base, nullptr,
+                                  CBV2_DTYPE_BF16, nullptr};
   *out = ix;
   return CBV2_OK;
+}
+
+int cbv2_index_create_mxfp8(int device, const void* tokens, const void* scales, int64_t n, int32_t ld, int32_t d,
+                            const int32_t* doclens, int64_t id_base, cbv2_index** out) {
+  CBV2_REQUIRE(out != nullptr, "null output handle pointer");
+  *out = nullptr;
+  CBV2_REQUIRE(n >= 0 && n <= 0x7fffffffLL, "n out of range (%lld)", (long long)n);
+  CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "global ids must fit int32");
+  if (ld != kLd || d != kDim)
+    return fail(CBV2_EUNSUPPORTED, "index geometry ld=%d d=%d not built (ld=128, d=128)", ld, d);
+  if (n > 0) {
+    CBV2_REQUIRE(tokens != nullptr && scales != nullptr && doclens != nullptr, "null tokens/scales/doclens");
+    CBV2_REQUIRE(aligned16(tokens), "tokens must be 16-byte aligned");
+    CBV2_REQUIRE(((uintptr_t)scales & 3u) == 0, "scales must be 4-byte aligned");
+  }
+  int ndev = 0;
+  CBV2_HIP(hipGetDeviceCount(&ndev));
+  CBV2_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
+  *out = new cbv2_index{device, (const uint8_t*)tokens, n, ld, d, doclens, id_base, nullptr, CBV2_DTYPE_MXFP8,
+                        (const uint8_t*)scales};
+  return CBV2_OK;
+}
+
+int cbv2_quantize_mxfp8(const void* x, int32_t dtype, int64_t rows, void* q, void* scales, void* stream) {
+  CBV2_REQUIRE(rows >= 0, "rows must be >= 0");
+  if (rows == 0) return CBV2_OK;
+  CBV2_REQUIRE(x && q && scales, "null pointer");
+  const int64_t want = (rows + 3) / 4;
+  const unsigned grid = (unsigned)(want < 65536 ? want : 65536);  // grid-stride beyond 2^24 work-items
+  if (dtype == CBV2_DTYPE_F32) {
+    hipLaunchKernelGGL(quantize_mxfp8_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       rows, (uint8_t*)q, (uint8_t*)scales);
+  } else if (dtype == CBV2_DTYPE_BF16) {
+    hipLaunchKernelGGL(quantize_mxfp8_kernel<uint16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint16_t*)x, rows, (uint8_t*)q, (uint8_t*)scales);
+  } else {
+    return fail(CBV2_EINVAL, "quantize takes bf16 or f32 input (got dtype %d)", dtype);
+  }
+  return launch_check("quantize_mxfp8_kernel");
 }
 
 int cbv2_index_destroy(cbv2_index* index) {
@@ -1239,6 +1662,7 @@ int cbv2_index_build_means(cbv2_index* ix, const float* tokens_f32, int32_t ld_s
   CBV2_REQUIRE(ix != nullptr, "null index");
   CBV2_REQUIRE(ld_src >= 1, "ld_src must be >= 1");
   CBV2_REQUIRE(ix->n == 0 || (tokens_f32 && doc_means), "null tokens_f32/doc_means");
+  CBV2_REQUIRE(ix->n < (1LL << 25), "build_means: n too large for one dispatch");  // 128 work-items per doc
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
   if (ix->n > 0) {
@@ -1290,7 +1714,8 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
 
 int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
                 float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
-  int rc = check_query(ix, CBV2_SCORER_MAXSIM, Q, CBV2_DTYPE_BF16, B, lq);
+  const int32_t qdt = ix && ix->dtype == CBV2_DTYPE_MXFP8 ? CBV2_DTYPE_MXFP8 : CBV2_DTYPE_BF16;
+  int rc = check_query(ix, CBV2_SCORER_MAXSIM, Q, qdt, B, lq);
   if (rc) return rc;
   CBV2_REQUIRE(cand != nullptr, "null candidates");
   CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
@@ -1299,6 +1724,13 @@ int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int3
   CBV2_REQUIRE(k == 0 || out_ids != nullptr, "null out_ids");
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  if (ix->dtype == CBV2_DTYPE_MXFP8) {
+    const uint8_t* Qb = (const uint8_t*)Q;
+    hipLaunchKernelGGL(rerank_f8_kernel, dim3((unsigned)B), dim3(kRrWaves * 64), 0, (hipStream_t)stream, ix->tokens,
+                       ix->scales, ix->doclens, ix->n, ix->id_base, Qb, Qb + (size_t)B * lq * kDim, lq, cand, C, k,
+                       out_scores, out_ids, out_pos);
+    return launch_check("rerank_f8_kernel");
+  }
   hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)B), dim3(kRrWaves * 64), 0, (hipStream_t)stream, ix->tokens,
                      ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids,
                      out_pos);

@@ -70,17 +70,45 @@ def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
     return tokens, doclens
 
 
-class ColbertIndex:
-    """One shard of the corpus resident in HBM, with a C handle borrowing it."""
+def quantize_mxfp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """[..., 128] bf16/f32 device tensor -> (e4m3 bytes uint8 [..., 128], E8M0 scales uint8 [..., 2])."""
+    _require_cuda(x, "x")
+    if x.shape[-1] != DIM:
+        raise ValueError(f"last dim must be {DIM}")
+    dt = {torch.bfloat16: _lib.DTYPE_BF16, torch.float32: _lib.DTYPE_F32}.get(x.dtype)
+    if dt is None:
+        x, dt = x.float(), _lib.DTYPE_F32
+    x = x.contiguous()
+    rows = x.numel() // DIM
+    buf = torch.empty(rows * (DIM + 2), dtype=torch.uint8, device=x.device)
+    q, sc = buf[: rows * DIM], buf[rows * DIM:]
+    _lib.check(_lib.lib().cbv2_quantize_mxfp8(x.data_ptr(), dt, rows, q.data_ptr(), sc.data_ptr(),
+                                              _stream_ptr(x.device)))
+    return q.view(*x.shape[:-1], DIM), sc.view(*x.shape[:-1], 2)
 
-    def __init__(self, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0):
+
+class ColbertIndex:
+    """One shard of the corpus resident in HBM, with a C handle borrowing it.
+
+    bf16 tokens (default), or MXFP8 (``tokens`` uint8 e4m3 [n, 128, 128] plus
+    ``scales`` uint8 E8M0 [n, 128, 2]; see ``ColbertIndex.mxfp8``)."""
+
+    def __init__(self, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0,
+                 scales: Optional[torch.Tensor] = None):
         _require_cuda(tokens, "tokens")
         _require_cuda(doclens, "doclens")
-        if tokens.dtype != torch.bfloat16 or tokens.dim() != 3 or tuple(tokens.shape[1:]) != (LD, DIM):
-            raise ValueError(f"tokens must be bf16 [n, {LD}, {DIM}] (got {tokens.dtype} {tuple(tokens.shape)})")
+        self.fp8 = tokens.dtype == torch.uint8
+        want = torch.uint8 if self.fp8 else torch.bfloat16
+        if tokens.dtype != want or tokens.dim() != 3 or tuple(tokens.shape[1:]) != (LD, DIM):
+            raise ValueError(f"tokens must be bf16 or MXFP8 uint8 [n, {LD}, {DIM}] "
+                             f"(got {tokens.dtype} {tuple(tokens.shape)})")
         if doclens.dtype != torch.int32 or doclens.shape != (tokens.shape[0],):
             raise ValueError("doclens must be int32 [n]")
+        if self.fp8 and (scales is None or scales.dtype != torch.uint8
+                         or tuple(scales.shape) != (tokens.shape[0], LD, 2)):
+            raise ValueError("an MXFP8 index needs uint8 scales [n, 128, 2]")
         self.tokens = tokens.contiguous()
+        self.scales = scales.contiguous() if self.fp8 else None
         self.doclens = doclens.contiguous()
         self.device = tokens.device
         self.n = int(tokens.shape[0])
@@ -88,11 +116,22 @@ class ColbertIndex:
         self.means: Optional[torch.Tensor] = None
         self._ws: Optional[torch.Tensor] = None
         h = ctypes.c_void_p()
-        _lib.check(_lib.lib().cbv2_index_create(
-            self.device.index if self.device.index is not None else torch.cuda.current_device(),
-            self.tokens.data_ptr(), _lib.DTYPE_BF16, self.n, LD, DIM, self.doclens.data_ptr(),
-            self.id_base, ctypes.byref(h)))
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        if self.fp8:
+            _lib.check(_lib.lib().cbv2_index_create_mxfp8(
+                dev, self.tokens.data_ptr(), self.scales.data_ptr(), self.n, LD, DIM, self.doclens.data_ptr(),
+                self.id_base, ctypes.byref(h)))
+        else:
+            _lib.check(_lib.lib().cbv2_index_create(
+                dev, self.tokens.data_ptr(), _lib.DTYPE_BF16, self.n, LD, DIM, self.doclens.data_ptr(),
+                self.id_base, ctypes.byref(h)))
         self._h = h
+
+    @classmethod
+    def mxfp8(cls, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0) -> "ColbertIndex":
+        """Quantize bf16/f32 [n, 128, 128] device tokens to MXFP8 (HIP kernel) and index them."""
+        q, sc = quantize_mxfp8(tokens)
+        return cls(q, doclens, id_base=id_base, scales=sc)
 
     @classmethod
     def from_embeddings(cls, embs, device="cuda", id_base: int = 0, build_means: bool = False):
@@ -142,15 +181,24 @@ class ColbertIndex:
         self._means_src = None
 
     # ----------------------------------------------------------------- query prep
-    def _prep_query(self, Q: torch.Tensor, scorer: str) -> Tuple[torch.Tensor, int]:
+    def _prep_query(self, Q: torch.Tensor, scorer: str):
+        """-> (buffer kept alive, pointer, ABI dtype, B, lq) in the layout the scorer takes."""
         if Q.dim() == 2:
             Q = Q.unsqueeze(0)
         if Q.dim() != 3 or Q.shape[2] != DIM:
             raise ValueError(f"queries must be [B, lq, {DIM}] (got {tuple(Q.shape)})")
+        B, lq = int(Q.shape[0]), int(Q.shape[1])
         Q = Q.to(self.device)
+        if scorer == "maxsim" and self.fp8:
+            if lq > LQ_MAX:
+                raise ValueError(f"maxsim takes at most {LQ_MAX} query tokens (got {lq})")
+            q, _ = quantize_mxfp8(Q)                   # one buffer: B*lq*128 bytes, then B*lq*2 scales
+            return q, q.data_ptr(), _lib.DTYPE_MXFP8, B, lq
         if scorer == "maxsim":
-            return Q.to(torch.bfloat16).contiguous(), _lib.DTYPE_BF16
-        return Q.to(torch.float32).contiguous(), _lib.DTYPE_F32
+            Qd = Q.to(torch.bfloat16).contiguous()
+            return Qd, Qd.data_ptr(), _lib.DTYPE_BF16, B, lq
+        Qd = Q.to(torch.float32).contiguous()
+        return Qd, Qd.data_ptr(), _lib.DTYPE_F32, B, lq
 
     def _scorer(self, scorer: str) -> int:
         try:
@@ -162,25 +210,23 @@ class ColbertIndex:
     def score(self, Q: torch.Tensor, scorer: str = "maxsim") -> torch.Tensor:
         """f32 [B, n] scores of every doc of the shard (the reference's _maxsim_score)."""
         sid = self._scorer(scorer)
-        Qd, qdt = self._prep_query(Q, scorer)
-        B, lq = int(Qd.shape[0]), int(Qd.shape[1])
+        _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
         out = torch.empty((B, max(self.n, 1)), dtype=torch.float32, device=self.device)
-        _lib.check(_lib.lib().cbv2_score(self._h, sid, Qd.data_ptr(), qdt, B, lq, out.data_ptr(),
+        _lib.check(_lib.lib().cbv2_score(self._h, sid, qptr, qdt, B, lq, out.data_ptr(),
                                          out.shape[1], _stream_ptr(self.device)))
         return out[:, : self.n]
 
     def search(self, Q: torch.Tensor, k: int, scorer: str = "maxsim") -> Tuple[torch.Tensor, torch.Tensor]:
         """Top-k over the shard: (f32 [B, k] scores, int32 [B, k] global ids), -inf/-1 padded."""
         sid = self._scorer(scorer)
-        Qd, qdt = self._prep_query(Q, scorer)
-        B, lq = int(Qd.shape[0]), int(Qd.shape[1])
+        _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
         L = _lib.lib()
         need = int(L.cbv2_search_workspace_bytes(self._h, B))
         if self._ws is None or self._ws.numel() * 4 < need:
             self._ws = torch.empty(((need + 3) // 4,), dtype=torch.float32, device=self.device)
         out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
         out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
-        _lib.check(L.cbv2_search(self._h, sid, Qd.data_ptr(), qdt, B, lq, int(k), self._ws.data_ptr(),
+        _lib.check(L.cbv2_search(self._h, sid, qptr, qdt, B, lq, int(k), self._ws.data_ptr(),
                                  self._ws.numel() * 4, out_s.data_ptr(), out_i.data_ptr(),
                                  _stream_ptr(self.device)))
         return out_s, out_i
@@ -190,22 +236,22 @@ class ColbertIndex:
 
         k > 0: (scores [B, k], ids [B, k], positions [B, k]); k == 0: raw scores [B, C].
         """
-        Qd, _ = self._prep_query(Q, "maxsim")
+        _keep, qptr, _, Bq, lq = self._prep_query(Q, "maxsim")
         cand = cand.to(device=self.device, dtype=torch.int32).contiguous()
         if cand.dim() == 1:
             cand = cand.unsqueeze(0)
         B, C = int(cand.shape[0]), int(cand.shape[1])
-        if Qd.shape[0] != B:
-            raise ValueError(f"{Qd.shape[0]} queries but {B} candidate rows")
+        if Bq != B:
+            raise ValueError(f"{Bq} queries but {B} candidate rows")
         if k == 0:
             out_s = torch.empty((B, C), dtype=torch.float32, device=self.device)
-            _lib.check(_lib.lib().cbv2_rerank(self._h, Qd.data_ptr(), B, int(Qd.shape[1]), cand.data_ptr(), C, 0,
+            _lib.check(_lib.lib().cbv2_rerank(self._h, qptr, B, lq, cand.data_ptr(), C, 0,
                                               out_s.data_ptr(), None, None, _stream_ptr(self.device)))
             return out_s
         out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
         out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
         out_p = torch.empty((B, k), dtype=torch.int32, device=self.device)
-        _lib.check(_lib.lib().cbv2_rerank(self._h, Qd.data_ptr(), B, int(Qd.shape[1]), cand.data_ptr(), C, int(k),
+        _lib.check(_lib.lib().cbv2_rerank(self._h, qptr, B, lq, cand.data_ptr(), C, int(k),
                                           out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(),
                                           _stream_ptr(self.device)))
         return out_s, out_i, out_p

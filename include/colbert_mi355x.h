@@ -45,6 +45,7 @@ extern "C" {
 /* dtypes */
 #define CBV2_DTYPE_BF16 1
 #define CBV2_DTYPE_F32 2
+#define CBV2_DTYPE_MXFP8 3 /* e4m3 bytes + one E8M0 scale per token per 64 dims */
 
 /* scorers */
 #define CBV2_SCORER_MAXSIM 0              /* sum_i max_j <q_i, d_j>            */
@@ -71,6 +72,20 @@ const char* cbv2_last_error(void);
 int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, int32_t ld,
                       int32_t d, const int32_t* doclens, int64_t id_base, cbv2_index** out);
 int cbv2_index_destroy(cbv2_index* index);
+
+/* MXFP8 index (config 5: half the HBM bytes of bf16, scored on the
+ * block-scaled fp8 MFMA): tokens e4m3 [n][128][128] (16-B aligned), scales
+ * E8M0 [n][128][2] (byte h scales dims 64h .. 64h+63 by 2^(byte-127)).
+ * Queries for such an index are MXFP8 too (q_dtype CBV2_DTYPE_MXFP8): one
+ * buffer holding B*lq*128 e4m3 bytes followed by B*lq*2 scale bytes, as
+ * written by cbv2_quantize_mxfp8 (rows = B*lq, scales = q + rows*128).     */
+int cbv2_index_create_mxfp8(int device, const void* tokens, const void* scales, int64_t n, int32_t ld,
+                            int32_t d, const int32_t* doclens, int64_t id_base, cbv2_index** out);
+
+/* cbv2_quantize_mxfp8 — rows of 128 values (dtype BF16 or F32) -> e4m3 bytes
+ * q [rows][128] (round-to-nearest-even) and E8M0 scales [rows][2], with
+ * scale = the smallest power of two that keeps each 64-value half <= 448.   */
+int cbv2_quantize_mxfp8(const void* x, int32_t dtype, int64_t rows, void* q, void* scales, void* stream);
 
 /* Literal-reference scorer support: build the L2-normalised per-doc token means
  * the reference recomputes on every call (local_rag_complete.py:822,825-829)

@@ -52,6 +52,49 @@ def bf16_round(x: np.ndarray) -> np.ndarray:
     return from_bf16_bits(to_bf16_bits(x))
 
 
+# ------------------------------------------------------------------ MXFP8 helpers
+def _e4m3_table() -> np.ndarray:
+    """OCP e4m3fn decode of all 256 byte values (0x7F / 0xFF are NaN)."""
+    t = np.empty(256, np.float64)
+    for v in range(256):
+        s, e, m = v >> 7, (v >> 3) & 15, v & 7
+        x = (m / 8.0) * 2.0 ** -6 if e == 0 else (1 + m / 8.0) * 2.0 ** (e - 7)
+        t[v] = -x if s else x
+    t[0x7F] = t[0xFF] = np.nan
+    return t
+
+
+E4M3 = _e4m3_table()
+
+
+def mxfp8_dequant(q: np.ndarray, scales: np.ndarray) -> np.ndarray:
+    """e4m3 bytes [..., 128] + E8M0 scales [..., 2] (one per 64 dims) -> float64 values."""
+    vals = E4M3[np.asarray(q, np.uint8)]
+    mult = np.exp2(np.asarray(scales, np.float64) - 127.0)
+    return vals * np.repeat(mult, 64, axis=-1)
+
+
+def mxfp8_quantize(x: np.ndarray):
+    """Restatement of cbv2_quantize_mxfp8: per 64-value half, e = the smallest integer
+    with max|x| <= 448 * 2^e (0 for an all-zero half), bytes = RNE(x / 2^e) in e4m3."""
+    x = np.asarray(x, np.float32).astype(np.float64)
+    h = x.reshape(*x.shape[:-1], 2, 64)
+    m = np.abs(h).max(axis=-1)
+    f, p = np.frexp(m)                                   # m = f * 2^p, f in [0.5, 1)
+    e = np.where(f <= 0.875, p - 9, p - 8)
+    e = np.where(m > 0, np.clip(e, -127, 127), 0)
+    y = h / np.exp2(e)[..., None]
+    a = np.abs(y)
+    E = np.floor(np.log2(np.where(a > 0, a, 1.0)))
+    E = np.maximum(E, -6.0)                              # subnormals share the 2^-6 binade's quantum
+    quantum = np.exp2(E - 3)
+    r = np.round(a / quantum) * quantum                  # numpy rounds half to even
+    pos = {float(E4M3[v]): v for v in range(0x7F)}
+    code = np.vectorize(lambda z: pos[float(z)])(r).astype(np.uint8)
+    code = np.where(y < 0, code | 0x80, code).astype(np.uint8)   # sign kept, also for -0 (as the hardware)
+    return code.reshape(x.shape), (e + 127).astype(np.uint8)
+
+
 # ------------------------------------------------------------------ scorers
 def maxsim(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray | None = None,
            dtype=np.float64) -> np.ndarray:
