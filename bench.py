@@ -3,16 +3,17 @@
 1M-chunk x 128-token synthetic corpus, top-10 rerank (BASELINE.json metric,
 config 3).
 
-One STEP = one batch of B=256 query embeddings through the hot path:
+One STEP = one batch of B=256 queries (embeddings + BM25 term ids) through
+the whole path:
+  stage 1  host BM25 top-100 (native C++, csrc/host_bm25.cpp) over the
+           synthetic 1M-doc term corpus -- run while the GPU scans,
   stage 2  HIP MaxSim scan + radix top-100 over the corpus (sharded over ranks:
-           per-rank top-100 -> RCCL all-gather -> HIP merge),
-  fusion   host RRF (native C++, reference semantics) of a stage-1 BM25 list
-           with the ColBERT top-100 -> top-50 candidates,
+           per-rank top-100 -> RCCL all-gather -> HIP merge; the ranks' BM25
+           lists over their doc shards ride the same all-gather),
+  fusion   host RRF (native C++, reference semantics) -> top-50 candidates,
   stage 3  HIP gather-by-id MaxSim rerank -> top-10 (sharded: RCCL all-reduce MAX).
-Inputs (the query batch, the BM25 lists, the index) are resident before the
-timed region.  The stage-1 BM25 lists are precomputed synthetic lists (host
-BM25 at this scale is SURVEY §8 f3, not yet built); everything else is done in
-full inside every timed step.
+Inputs (the query batch and term ids, both indexes) are resident before the
+timed region; every stage runs in full inside every timed step.
 
 N>1: the SAME 1M-doc corpus is split into N contiguous shards, one per rank
 (strong scaling); value = B*K / max-over-ranks wall time.
@@ -37,6 +38,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from hybrid_rag_colbertv2_amd import bm25 as bm25_mod  # noqa: E402
 from hybrid_rag_colbertv2_amd import synth  # noqa: E402
 from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range  # noqa: E402
 from hybrid_rag_colbertv2_amd.hybrid import PipelinedRetriever, rrf_fuse  # noqa: E402
@@ -120,7 +122,14 @@ def main():
     t_setup = time.time()
     Qf = synth.make_queries(B, LQ, seed=1)
     planted = synth.planted_ids(B, n_total, 10, seed=2)
-    bm25 = synth.bm25_lists(B, n_total, planted, k=args.k, seed=3)
+    t_bm = time.time()
+    bm_terms, bm_off, vocab = synth.bm25_shard(begin, end, planted)
+    lex = bm25_mod.sharded(bm_terms, bm_off, vocab, id_base=begin, device=dev)   # global stats: 1 all-reduce
+    del bm_terms, bm_off
+    qt, qo = synth.bm25_queries(B)
+    log(f"host BM25 shard built in {time.time() - t_bm:.1f}s ({lex.n_docs} docs, {len(lex.doc_terms)} terms)")
+    bm_all = lambda: lex.search(qt, qo, args.k)                 # noqa: E731  stage 1, whole batch
+    bm_one = lambda: lex.search(qt[:qo[1]], qo[:2], args.k)     # noqa: E731  stage 1, query 0
     tokens, doclens = synth.make_shard(begin, end, Qf, planted, dev, seed=0)
     if args.dtype == "fp8":
         ix = ColbertIndex.mxfp8(tokens, doclens, id_base=begin)   # quantized on the GPU (HIP kernel)
@@ -133,20 +142,22 @@ def main():
     torch.cuda.synchronize()
     log(f"setup {time.time() - t_setup:.1f}s: rank {rank}/{world} docs [{begin},{end}) B={B}")
 
-    def step(Qb, bm):
+    def step(Qb, lexical):
         """One batch, unpipelined (used for the B=1 latency)."""
-        _, ids = searcher.search(Qb, args.k)
+        _, ids, bm = searcher.search_hybrid(Qb, args.k, lexical)
+        bm = bm.cpu().numpy() if isinstance(bm, torch.Tensor) else bm
         cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=args.fused)
         cand_d = torch.from_numpy(cand).to(dev, non_blocking=False)
         return searcher.rerank(Qb, cand_d, args.final_k)
 
     # Throughput: K batches through the software-pipelined path (batch j+1's
-    # scan runs on the GPU while the host fuses batch j; see PipelinedRetriever).
+    # scan runs on the GPU while the host runs its BM25 and fuses batch j; see
+    # PipelinedRetriever).
     pipe = PipelinedRetriever(searcher, dev, colbert_k=args.k, fused=args.fused, final_k=args.final_k)
     if args.no_pipeline:
-        run_steps = lambda K: [step(Q, bm25)[:2] for _ in range(K)]  # noqa: E731
+        run_steps = lambda K: [step(Q, bm_all)[:2] for _ in range(K)]  # noqa: E731
     else:
-        run_steps = lambda K: pipe.run([(Q, bm25)] * K)  # noqa: E731
+        run_steps = lambda K: pipe.run([(Q, bm_all)] * K)  # noqa: E731
     if args.warmup:
         run_steps(args.warmup)
     torch.cuda.synchronize()
@@ -178,11 +189,16 @@ def main():
         if world > 1:
             dist.barrier()
         t = time.perf_counter()
-        step(Q1, bm25[:1])
+        step(Q1, bm_one)
         torch.cuda.synchronize()
         if it >= 3:
             lat.append((time.perf_counter() - t) * 1e3)
     p50 = statistics.median(lat) if lat else None
+    bm_ms = []
+    for _ in range(3):                                  # stage 1 alone (host), for the record
+        t = time.perf_counter()
+        bm_all()
+        bm_ms.append((time.perf_counter() - t) * 1e3)
 
     # ---- dominant kernel: MaxSim scan, timed with HIP events on its stream
     scan_ms = []
@@ -240,14 +256,15 @@ def main():
             "value": round(qps, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic (unit-norm N(0,I) tokens, 10 planted positives/query, synthetic BM25 lists)",
+            "data": "synthetic (unit-norm N(0,I) tokens, Zipf term-id corpus for BM25, 10 planted positives/query)",
             "config": {"workload": ("config 5 (MXFP8 e4m3 tokens, block-scaled fp8 MFMA)" if fp8 else "config 3") +
-                                   f": {n_total} chunks x 128 tokens x 128-d, BM25 top-100 (precomputed) + "
+                                   f": {n_total} chunks x 128 tokens x 128-d, host BM25 top-100 + "
                                    "ColBERT MaxSim top-100 + RRF + rerank top-10",
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
                        "parallelism": f"corpus sharded x{world}" + (" (RCCL all-gather + all-reduce)" if world > 1 else "")},
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
+            "host_bm25_ms_per_batch": round(min(bm_ms), 3),
             "roofline": {"bound": "mfma", "kernel": kern, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic, "avg_ms": round(scan_avg, 3)},

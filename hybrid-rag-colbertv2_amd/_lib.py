@@ -42,6 +42,14 @@ _SIGS = {
     "cbv2_topk_rows": (ctypes.c_int, [_p, _i32, _i64, _i64, _i32, _i64, _p, _sz, _p, _p, _p]),
     "cbv2_merge_topk": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p]),
     "cbv2_rrf_fuse": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _p]),
+    "cbv2_bm25_build": (ctypes.c_int, [_p, _p, _i64, _i32, ctypes.c_float, ctypes.c_float,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_bm25_search": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _p, _p]),
+    "cbv2_bm25_doc_freq": (ctypes.c_int, [_p, _p, _i64, _i32, _p]),
+    "cbv2_bm25_build_shard": (ctypes.c_int, [_p, _p, _i64, _i32, ctypes.c_float, ctypes.c_float, _i64, _i64,
+                                             _i64, _p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_bm25_num_docs": (_i64, [_p]),
+    "cbv2_bm25_destroy": (ctypes.c_int, [_p]),
 }
 
 _lib = None

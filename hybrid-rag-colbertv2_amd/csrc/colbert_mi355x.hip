@@ -1587,6 +1587,9 @@ int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
 
 extern "C" {
 
+// Internal: lets host_bm25.cpp report errors through cbv2_last_error().
+int cbv2_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
 int cbv2_abi_version(void) { return CBV2_ABI_VERSION; }
 
 const char* cbv2_last_error(void) { return g_err; }

@@ -11,6 +11,11 @@ is the §8(e) design:
            all-reduce(MAX) over [B, C] -> HIP top-k select.  Each id is owned by
            exactly one shard, so MAX picks the owner's score.
 
+Stage 1 (host BM25) is doc-sharded the same way (bm25.sharded: global
+statistics from one build-time all-reduce), and its per-rank top-kb lists
+ride the stage-2 all-gather (search_hybrid), so a query costs each rank only
+its shard's postings and the whole exchange stays ONE collective per stage.
+
 Messages are tiny (B=256, k=100: 200 KiB per rank), so the exchange is
 latency-bound; it is one collective per stage.  torch.distributed's "nccl"
 backend IS RCCL on ROCm.  The same code runs on "gloo" for CPU tests, where
@@ -20,6 +25,7 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -52,11 +58,13 @@ class ShardedSearcher:
     ``rerank(Q, cand, 0)``); ``ops`` provides ``merge`` and ``select``.
     """
 
-    def __init__(self, local, group: Optional[dist.ProcessGroup] = None, ops=None):
+    def __init__(self, local, group: Optional[dist.ProcessGroup] = None, ops=None, world: Optional[int] = None):
         self.local = local
         self.group = group
         self.ops = ops if ops is not None else _DeviceOps()
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if world is None:
+            world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = world
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
@@ -70,6 +78,38 @@ class ShardedSearcher:
         s, i = self.local.search(Q, k)
         if self.world == 1:
             return s, i
+        return self.search_exchange(s, i, k)
+
+    def search_hybrid(self, Q: torch.Tensor, k: int, lexical=None):
+        """Stage 2 plus this rank's stage-1 lists in the SAME collective.
+
+        ``lexical()`` runs on the host AFTER the scan is enqueued (so it
+        overlaps the GPU) and returns this rank's BM25 top-kb (global ids int32
+        [B, kb], scores float32 [B, kb]) over its doc shard (``bm25.sharded``).
+        Returns (scores, ids, bm25_ids): with one rank bm25_ids is that host
+        array; otherwise both lists ride one all-gather and are merged with the
+        same (score desc, id asc) rule, which reproduces the unsharded stage 1
+        exactly because the shards were built with global statistics.
+        """
+        s, i = self.local.search(Q, k)
+        if lexical is None:
+            if self.world == 1:
+                return s, i, None
+            S, I = self.search_exchange(s, i, k)
+            return S, I, None
+        lex_i, lex_s = lexical()
+        if self.world == 1:
+            return s, i, np.ascontiguousarray(lex_i, np.int32)
+        kb = lex_i.shape[1]
+        lex = torch.stack([torch.from_numpy(np.ascontiguousarray(lex_s, np.float32)).view(torch.int32),
+                           torch.from_numpy(np.ascontiguousarray(lex_i, np.int32))], dim=-1).to(i.device)
+        packed = torch.cat([torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1), lex], dim=1)
+        allp = self._all_gather(packed)                                                    # [G, B, k+kb, 2]
+        S, I = self.ops.merge(allp[:, :, :k, 0].contiguous().view(torch.float32), allp[:, :, :k, 1].contiguous(), k)
+        _, LI = self.ops.merge(allp[:, :, k:, 0].contiguous().view(torch.float32), allp[:, :, k:, 1].contiguous(), kb)
+        return S, I, LI
+
+    def search_exchange(self, s: torch.Tensor, i: torch.Tensor, k: int):
         packed = torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1)  # [B, k, 2]
         allp = self._all_gather(packed)                                                    # [G, B, k, 2]
         S = allp[..., 0].contiguous().view(torch.float32)
@@ -77,7 +117,8 @@ class ShardedSearcher:
         return self.ops.merge(S, I, k)
 
     def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+        if self.world == 1:
+            return self.local.rerank(Q, cand, k)                                           # fused select
         raw = self.local.rerank(Q, cand, 0)                                                # [B, C]
-        if self.world > 1:
-            dist.all_reduce(raw, op=dist.ReduceOp.MAX, group=self.group)
+        dist.all_reduce(raw, op=dist.ReduceOp.MAX, group=self.group)
         return self.ops.select(raw, k, ids=cand)

@@ -253,64 +253,82 @@ class HybridRetriever:
 class PipelinedRetriever:
     """Software-pipelined three-stage retrieval over a stream of query batches.
 
-    The host step in the middle of the path (RRF fusion of the stage-2 ids,
-    LRC:960-978) would otherwise idle the GPU once per batch.  Here batch j+1's
-    stage-2 scan is enqueued BEFORE the host fuses batch j, so the GPU scans
-    while the host fuses:
+    The host steps of the path -- stage-1 BM25 (LRC:937-950) and RRF fusion
+    (LRC:960-978) -- would otherwise idle the GPU once per batch.  Here batch
+    j+1's stage-2 scan is enqueued, and its BM25 runs on the host while the
+    GPU scans, BEFORE the host fuses batch j:
 
-        GPU main stream:  scan(j) | scan(j+1) | rerank(j) | scan(j+2) | rerank(j+1) ...
-        GPU side stream:  D2H ids(j) (after scan(j) only)
-        host:                       fuse(j) -> H2D cand(j)
+        GPU main stream:  scan(j) | scan(j+1)          | rerank(j) | scan(j+2) ...
+        GPU side stream:  D2H ids(j)
+        host:             bm25(j) | bm25(j+1), fuse(j) -> H2D cand(j) | ...
 
-    ``searcher`` is anything with ``search(Q, k)`` and ``rerank(Q, cand, k)``:
-    a ``ColbertIndex`` or a ``distributed.ShardedSearcher`` (the collectives
-    are issued in the same order on every rank).  Results per batch are exactly
-    those of the unpipelined path.
+    ``searcher`` is a ``ColbertIndex`` (one shard) or a
+    ``distributed.ShardedSearcher``; with several ranks each one runs BM25
+    over its own doc shard and the lists ride the stage-2 all-gather (the
+    collectives are issued in the same order on every rank).  Results per
+    batch are exactly those of the unpipelined path.
     """
 
     def __init__(self, searcher, device, colbert_k: int = 100, fused: int = 50, final_k: int = 10,
                  rrf_k: int = 60):
+        from .distributed import ShardedSearcher
+        if not hasattr(searcher, "search_hybrid"):
+            searcher = ShardedSearcher(searcher, world=1)     # a bare index: one shard
         self.searcher, self.device = searcher, torch.device(device)
         self.k, self.fused, self.final_k, self.rrf_k = colbert_k, fused, final_k, rrf_k
         self.side = torch.cuda.Stream(self.device)
-        self._ids_h = None
+        self._ids_h = self._lex_h = None
         self._cand_h = [None, None]
 
-    def _host_buffers(self, B: int):
-        if self._ids_h is None or self._ids_h.shape[0] < B:
+    def _host_buffers(self, B: int, kb: int):
+        if self._ids_h is None or self._ids_h.shape[0] < B or self._lex_h.shape[1] != kb:
+            B = max(B, self._ids_h.shape[0] if self._ids_h is not None else 0)
             self._ids_h = torch.empty((B, self.k), dtype=torch.int32, pin_memory=True)
+            self._lex_h = torch.empty((B, kb), dtype=torch.int32, pin_memory=True)
             self._cand_h = [torch.empty((B, self.fused), dtype=torch.int32, pin_memory=True) for _ in range(2)]
 
+    def _stage12(self, Q, lex):
+        """Enqueue stage 2; run (or take) stage 1 on the host meanwhile."""
+        if callable(lex):
+            _, ids, bm = self.searcher.search_hybrid(Q, self.k, lex)
+        else:
+            _, ids = self.searcher.search(Q, self.k)
+            bm = np.ascontiguousarray(lex, np.int32)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ids, bm, ev
+
     def run(self, batches):
-        """batches: sequence of (Q [B, lq, D] device, bm25_ids [B, kb] host).  Returns [(scores, ids)]."""
+        """batches: sequence of (Q [B, lq, D] device, lexical), where lexical is
+        either the stage-1 ids [B, kb] (host) or a callable returning this
+        rank's BM25 top-kb (ids, scores) -- called on the host while the GPU
+        scans (see ShardedSearcher.search_hybrid).  Returns [(scores, ids)]."""
         batches = list(batches)
         if not batches:
             return []
-        main = torch.cuda.current_stream(self.device)
-        self._host_buffers(max(q.shape[0] for q, _ in batches))
         out = []
-        _, ids = self.searcher.search(batches[0][0], self.k)
-        ev = torch.cuda.Event()
-        ev.record(main)
-        for j, (Q, bm) in enumerate(batches):
+        cur = self._stage12(*batches[0])
+        for j, (Q, _) in enumerate(batches):
             B = Q.shape[0]
-            if j + 1 < len(batches):                       # keep the GPU busy during the host step
-                _, nxt_ids = self.searcher.search(batches[j + 1][0], self.k)
-                nxt_ev = torch.cuda.Event()
-                nxt_ev.record(main)
+            nxt = self._stage12(*batches[j + 1]) if j + 1 < len(batches) else None   # GPU busy during host work
+            ids, bm, ev = cur
+            self._host_buffers(B, bm.shape[1])
             ids_h = self._ids_h[:B]
             with torch.cuda.stream(self.side):
                 self.side.wait_event(ev)
                 ids.record_stream(self.side)
                 ids_h.copy_(ids, non_blocking=True)
+                if isinstance(bm, torch.Tensor):                   # merged across ranks on the device
+                    bm.record_stream(self.side)
+                    self._lex_h[:B].copy_(bm, non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(self.side)
             done.synchronize()
+            bm_h = self._lex_h[:B].numpy() if isinstance(bm, torch.Tensor) else bm
             cand = self._cand_h[j & 1][:B]
-            cand.numpy()[:] = rrf_fuse(bm, ids_h.numpy(), rrf_k=self.rrf_k, C=self.fused)
+            cand.numpy()[:] = rrf_fuse(bm_h, ids_h.numpy(), rrf_k=self.rrf_k, C=self.fused)
             cand_d = cand.to(self.device, non_blocking=True)
             s, i, _ = self.searcher.rerank(Q, cand_d, self.final_k)
             out.append((s, i))
-            if j + 1 < len(batches):
-                ids, ev = nxt_ids, nxt_ev
+            cur = nxt
         return out

@@ -75,3 +75,57 @@ def make_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, devic
         docs = _unit(Q[torch.from_numpy(qb)] + sigma * _unit(noise))
         tokens[torch.from_numpy(ids - begin).to(device), :lq] = docs.to(device=device, dtype=torch.bfloat16)
     return tokens, doclens
+
+
+BM25_VOCAB = 30000
+
+
+def bm25_queries(B: int, q_len: int = 6, seed: int = 4):
+    """Stage-1 queries as term-id CSR: ``q_len`` mid-frequency terms each."""
+    rng = np.random.default_rng([seed, 1 << 20])
+    q = rng.integers(100, 5000, size=(B, q_len)).astype(np.int32)
+    return q.reshape(-1), np.arange(B + 1, dtype=np.int64) * q_len
+
+
+def bm25_shard(begin: int, end: int, planted: np.ndarray, q_len: int = 6, vocab: int = BM25_VOCAB, seed: int = 4):
+    """Docs [begin, end) of the synthetic stage-1 corpus as term ids (CSR with
+    offsets from 0): lengths U[40, 120], Zipf-like term frequencies
+    (p ~ 1/(rank + 10)), one RNG per CHUNK of global ids so any rank can build
+    its own range.  Planted docs get their query's terms appended, so the
+    lexical and late-interaction stages agree on the positives as they would
+    on a relevant chunk.  Returns (doc_terms int32, doc_offsets int64, vocab)."""
+    q_terms, _ = bm25_queries(planted.shape[0], q_len, seed)
+    q_terms = q_terms.reshape(-1, q_len)
+    flat = planted.reshape(-1)
+    owner = dict(zip(flat.tolist(), np.repeat(np.arange(planted.shape[0]), planted.shape[1]).tolist()))
+    p = 1.0 / (np.arange(vocab, dtype=np.float64) + 10.0)
+    cdf = np.cumsum(p / p.sum())
+    rows_t, rows_l = [], []
+    for c in range(begin // CHUNK, (end + CHUNK - 1) // CHUNK):
+        rng = np.random.default_rng([seed, c])
+        lens = rng.integers(40, 121, size=CHUNK)
+        terms = np.minimum(np.searchsorted(cdf, rng.random(int(lens.sum()))), vocab - 1).astype(np.int32)
+        off = np.zeros(CHUNK + 1, np.int64)
+        off[1:] = np.cumsum(lens)
+        lo, hi = max(begin, c * CHUNK) - c * CHUNK, min(end, (c + 1) * CHUNK) - c * CHUNK
+        mine = [d for d in owner if c * CHUNK + lo <= d < c * CHUNK + hi]
+        if not mine:
+            rows_t.append(terms[off[lo]:off[hi]])
+            rows_l.append(lens[lo:hi])
+            continue
+        prev = lo
+        for d in sorted(mine):
+            dl = d - c * CHUNK
+            rows_t.append(terms[off[prev]:off[dl + 1]])
+            rows_t.append(q_terms[owner[d]])
+            ln = lens[prev:dl + 1].copy()
+            ln[-1] += q_len
+            rows_l.append(ln)
+            prev = dl + 1
+        rows_t.append(terms[off[prev]:off[hi]])
+        rows_l.append(lens[prev:hi])
+    lens = np.concatenate(rows_l) if rows_l else np.zeros(0, np.int64)
+    offsets = np.zeros(len(lens) + 1, np.int64)
+    offsets[1:] = np.cumsum(lens)
+    terms = np.concatenate(rows_t).astype(np.int32) if rows_t else np.zeros(0, np.int32)
+    return terms, offsets, vocab

@@ -162,6 +162,36 @@ int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, in
 int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_ids, int32_t kc, int32_t B,
                   int32_t rrf_k, int32_t C, int32_t* out_ids, double* out_scores, int32_t* out_count);
 
+/* Host BM25 (HOST pointers, no GPU) ---------------------------------------
+ * Stage 1 of HybridRetriever.retrieve (local_rag_complete.py:937-950; the
+ * reference uses bm25s: LRC:851-858, 939-945) over term ids (tokenisation
+ * and stopwords stay in the caller).  Lucene BM25:
+ *   idf = ln(1 + (N - df + 0.5) / (df + 0.5)),
+ *   w   = idf * tf * (k1 + 1) / (tf + k1 * (1 - b + b * |d| / avgdl)),
+ * summed over the distinct query terms.  Corpus as CSR: doc i's term ids are
+ * doc_terms[doc_offsets[i] .. doc_offsets[i+1]).  Search: queries as CSR,
+ * out_ids [B][k] (score desc, then doc id asc; padded with the lowest-id
+ * zero-score docs, then -1), out_scores [B][k] (nullable).  n_threads <= 0:
+ * min(16, hardware threads).  Parity with bm25s itself: unpinned.          */
+typedef struct cbv2_bm25 cbv2_bm25;
+int cbv2_bm25_build(const int32_t* doc_terms, const int64_t* doc_offsets, int64_t n_docs, int32_t vocab,
+                    float k1, float b, cbv2_bm25** out);
+int cbv2_bm25_search(const cbv2_bm25* index, const int32_t* q_terms, const int64_t* q_offsets, int32_t B,
+                     int32_t k, int32_t n_threads, int32_t* out_ids, float* out_scores);
+/* Sharded BM25 (no reference counterpart): a rank indexes
+ * only its doc range [id_base, id_base + n_docs) but with the GLOBAL
+ * statistics (n_global docs, total_global tokens, df_global [vocab] from an
+ * all-reduce of cbv2_bm25_doc_freq), so every weight equals the unsharded
+ * index's; search then returns global ids (local + id_base), and merging the
+ * ranks' lists by (score desc, id asc) reproduces the unsharded top-k.      */
+int cbv2_bm25_doc_freq(const int32_t* doc_terms, const int64_t* doc_offsets, int64_t n_docs, int32_t vocab,
+                       int64_t* df_out);
+int cbv2_bm25_build_shard(const int32_t* doc_terms, const int64_t* doc_offsets, int64_t n_docs, int32_t vocab,
+                          float k1, float b, int64_t id_base, int64_t n_global, int64_t total_global,
+                          const int64_t* df_global, cbv2_bm25** out);
+int64_t cbv2_bm25_num_docs(const cbv2_bm25* index);
+int cbv2_bm25_destroy(cbv2_bm25* index);
+
 #ifdef __cplusplus
 }
 #endif

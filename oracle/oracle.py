@@ -210,6 +210,45 @@ def merge_topk(scores: np.ndarray, ids: np.ndarray, k: int):
     return out_s, out_i
 
 
+# ------------------------------------------------------------------ BM25 (stage 1)
+def bm25_topk(doc_terms, doc_offsets, q_terms, q_offsets, vocab: int, k: int, k1: float = 1.5, b: float = 0.75):
+    """Lucene BM25 as bm25s scores it (LRC:851-858, 939-945; bm25s absent here, so
+    its published formula), restated with the C++ index's exact operation order
+    so every float matches: weights in float64 -> float32, query terms distinct and
+    ascending, float32 accumulation in doc order, ties -> lower doc id, all docs ranked."""
+    import math
+    k1, b = float(np.float32(k1)), float(np.float32(b))      # the C ABI takes them as float
+    doc_terms = np.asarray(doc_terms, np.int64)
+    doc_offsets = np.asarray(doc_offsets, np.int64)
+    N = len(doc_offsets) - 1
+    avgdl = float(int(doc_offsets[-1])) / N if N else 1.0
+    per_doc = []
+    df = np.zeros(vocab, np.int64)
+    for d in range(N):
+        t, tf = np.unique(doc_terms[doc_offsets[d]:doc_offsets[d + 1]], return_counts=True)
+        per_doc.append((t, tf, int(doc_offsets[d + 1] - doc_offsets[d])))
+        df[t] += 1
+    idf = [math.log(1.0 + (N - int(df[t]) + 0.5) / (int(df[t]) + 0.5)) for t in range(vocab)]
+    post = [[] for _ in range(vocab)]
+    for d, (ts, tfs, dl) in enumerate(per_doc):
+        for t, tf in zip(ts.tolist(), tfs.tolist()):
+            norm = tf + k1 * (1.0 - b + b * dl / avgdl)
+            post[t].append((d, np.float32(idf[t] * tf * (k1 + 1.0) / norm)))
+    B = len(q_offsets) - 1
+    out_i = np.full((B, k), -1, np.int64)
+    out_s = np.zeros((B, k), np.float32)
+    for qb in range(B):
+        acc = np.zeros(N, np.float32)
+        for t in sorted(set(int(x) for x in q_terms[q_offsets[qb]:q_offsets[qb + 1]])):
+            if 0 <= t < vocab:
+                for d, w in post[t]:
+                    acc[d] = np.float32(acc[d] + w)
+        order = np.lexsort((np.arange(N), -acc))[:k]
+        out_i[qb, :len(order)] = order
+        out_s[qb, :len(order)] = acc[order]
+    return out_i, out_s
+
+
 # ------------------------------------------------------------------ fusion
 def rrf(bm25_ids: Sequence[int], colbert_ids: Sequence[int], k: int = 60) -> List[Tuple[int, float]]:
     """LRC:960-978: score[id] += 1/(k + rank) over the BM25 list, then the ColBERT

@@ -1,0 +1,130 @@
+"""CPU: the native host BM25 (csrc/host_bm25.cpp, stage 1 of
+HybridRetriever.retrieve, local_rag_complete.py:937-950) against the oracle's
+restatement (oracle/oracle.py:bm25_topk), bit-for-bit: ids and float32 score
+bits.  Parity with bm25s itself is unpinned (bm25s is not installed; see
+DESIGN.md); the formula is bm25s' published Lucene variant.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+
+def _corpus(rng, N, V, maxlen=30, dup=0.0):
+    lens = rng.integers(0, maxlen, size=N)
+    rows = [rng.integers(0, V, size=int(n)).astype(np.int32) for n in lens]
+    for d in range(1, N):                 # duplicated docs -> exactly tied scores
+        if rng.random() < dup:
+            rows[d] = rows[int(rng.integers(0, d))].copy()
+    off = np.zeros(N + 1, np.int64)
+    off[1:] = np.cumsum([len(r) for r in rows])
+    terms = np.concatenate(rows) if N else np.zeros(0, np.int32)
+    return terms.astype(np.int32), off
+
+
+def _queries(rng, B, V, maxq=6):
+    ql = rng.integers(0, maxq, size=B)
+    qo = np.zeros(B + 1, np.int64)
+    qo[1:] = np.cumsum(ql)
+    return rng.integers(-1, V + 2, size=int(qo[-1])).astype(np.int32), qo
+
+
+def _same(a_ids, a_sc, b_ids, b_sc):
+    assert np.array_equal(a_ids.astype(np.int64), b_ids.astype(np.int64))
+    assert np.array_equal(np.asarray(a_sc, np.float32).view(np.uint32), np.asarray(b_sc, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_native_bm25_matches_oracle(seed):
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    rng = np.random.default_rng(seed)
+    N = int(rng.integers(1, 400))
+    V = int(rng.integers(1, 60))
+    terms, off = _corpus(rng, N, V, dup=0.2)
+    qt, qo = _queries(rng, 9, V)
+    for k in (1, 10, N, N + 7):              # k > N: -1 padding after every doc
+        ids, sc = NativeBM25(terms, off, V).search(qt, qo, k, n_threads=3)
+        oi, os_ = orc.bm25_topk(terms, off, qt, qo, V, k)
+        _same(ids, sc, oi, os_)
+
+
+def test_native_bm25_k1_b_and_threads():
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    rng = np.random.default_rng(11)
+    terms, off = _corpus(rng, 500, 40, maxlen=60)
+    qt, qo = _queries(rng, 33, 40)
+    ix = NativeBM25(terms, off, 40, k1=0.9, b=0.4)
+    ref = orc.bm25_topk(terms, off, qt, qo, 40, 20, k1=0.9, b=0.4)
+    for th in (1, 2, 8, 64):
+        _same(*ix.search(qt, qo, 20, n_threads=th), *ref)
+
+
+@pytest.mark.parametrize("G", [2, 3, 5])
+def test_sharded_bm25_merge_equals_unsharded(G):
+    """Doc-sharded index with global statistics: the (score desc, id asc)
+    merge of the shards' top-k lists is the unsharded top-k, ties included."""
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    from hybrid_rag_colbertv2_amd.distributed import shard_range
+    rng = np.random.default_rng(G)
+    N, V, k = 257, 25, 30
+    terms, off = _corpus(rng, N, V, dup=0.3)
+    qt, qo = _queries(rng, 12, V)
+    parts = []
+    for r in range(G):
+        a, b = shard_range(N, r, G)
+        parts.append((a, terms[off[a]:off[b]], off[a:b + 1] - off[a]))
+    df = sum(NativeBM25.doc_freq(t, o, V) for _, t, o in parts)
+    stats = (N, int(off[-1]), df)
+    res = [NativeBM25(t, o, V, id_base=a, stats=stats).search(qt, qo, k) for a, t, o in parts]
+    S = np.stack([r[1] for r in res])
+    I = np.stack([r[0] for r in res])
+    ms, mi = orc.merge_topk(S, I, k)
+    oi, os_ = orc.bm25_topk(terms, off, qt, qo, V, k)
+    _same(mi, ms, oi, os_)
+
+
+def test_bm25_validation():
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    with pytest.raises(ValueError):
+        NativeBM25(np.array([0, 5], np.int32), np.array([0, 2], np.int64), 3)        # term >= vocab
+    with pytest.raises(ValueError):
+        NativeBM25(np.array([0, 1], np.int32), np.array([2, 0], np.int64), 3)        # offsets descending
+    with pytest.raises(ValueError):
+        NativeBM25(np.array([0], np.int32), np.array([0, 1], np.int64), 3, id_base=5,
+                   stats=(2, 1, np.ones(3, np.int64)))                               # shard beyond n_global
+    ix = NativeBM25(np.array([0, 1], np.int32), np.array([0, 1, 2], np.int64), 2)
+    with pytest.raises(ValueError):
+        ix.search(np.zeros(0, np.int32), np.zeros(2, np.int64), 0)                   # k < 1
+    ids, sc = ix.search(np.zeros(0, np.int32), np.zeros(2, np.int64), 3)           # empty query
+    assert ids.tolist() == [[0, 1, -1]] and sc.tolist() == [[0, 0, 0]]
+
+
+def test_synth_bm25_shards_compose_and_plant():
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    n, B = 40000, 8
+    pl = synth.planted_ids(B, n, 10)
+    terms, off, V = synth.bm25_shard(0, n, pl)
+    assert len(off) == n + 1 and terms.min() >= 0 and terms.max() < V
+    a, b = 12345, 30001
+    t2, o2, _ = synth.bm25_shard(a, b, pl)
+    assert np.array_equal(t2, terms[off[a]:off[b]]) and np.array_equal(o2, off[a:b + 1] - off[a])
+    qt, qo = synth.bm25_queries(B)
+    ids, _ = NativeBM25(terms, off, V).search(qt, qo, 100)
+    assert all(set(pl[q]) <= set(ids[q].tolist()) for q in range(B))
+
+
+def test_hostbm25_text_roundtrip(tmp_path):
+    from hybrid_rag_colbertv2_amd.bm25 import HostBM25
+    corpus = ["The quick brown fox", "jumps over the lazy dog", "quick quick dog", "", "fox and dog"]
+    bm = HostBM25()
+    bm.index(bm.tokenize(corpus))
+    ids, sc = bm.retrieve(bm.tokenize("quick dog"), k=5)
+    # oracle over the same term ids
+    rows = [bm._ids(t, grow=False) for t in bm.tokenize(corpus)]
+    from hybrid_rag_colbertv2_amd.bm25 import to_csr
+    terms, off = to_csr(rows)
+    q, qo = to_csr([bm._ids(bm.tokenize("quick dog"), grow=False)])
+    oi, os_ = orc.bm25_topk(terms, off, q, qo, len(bm.vocab), 5)
+    _same(ids, sc, oi, os_)
+    assert ids[0][0] == 2

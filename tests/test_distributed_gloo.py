@@ -108,3 +108,55 @@ def test_sharded_protocol_world2_equals_unsharded():
         np.testing.assert_allclose(s, es, atol=1e-5)
         assert np.array_equal(gp, rp) and np.array_equal(gi, ri)
         np.testing.assert_allclose(gs, rs, atol=1e-5)
+
+
+def _bm25_data():
+    rng = np.random.default_rng(9)
+    N, V = 301, 30
+    lens = rng.integers(0, 25, size=N)
+    off = np.zeros(N + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    terms = rng.integers(0, V, size=int(off[-1])).astype(np.int32)
+    qo = np.arange(4, dtype=np.int64) * 3
+    qt = rng.integers(0, V, size=9).astype(np.int32)
+    return terms, off, qt, qo, V
+
+
+def _hybrid_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hybrid_rag_colbertv2_amd import bm25
+        from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range
+        Q, docs, doclens, _ = _data()
+        terms, off, qt, qo, V = _bm25_data()
+        a, b = shard_range(len(docs), rank, world)
+        lex = bm25.sharded(terms[off[a]:off[b]], off[a:b + 1] - off[a], V, id_base=a)   # all-reduced stats
+        ss = ShardedSearcher(OracleShard(Q, docs[a:b], doclens[a:b], a), ops=OracleOps())
+        s, i, li = ss.search_hybrid(Q, 40, lambda: lex.search(qt, qo, 50))
+        q.put((rank, s.numpy(), i.numpy(), li.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_hybrid_exchange_world2_equals_unsharded():
+    """Doc-sharded BM25 (global stats by all-reduce) + stage 2 in one all-gather."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Q, docs, doclens, _ = _data()
+    es, ei = orc.topk(orc.maxsim(Q.numpy(), docs, doclens), 40)
+    terms, off, qt, qo, V = _bm25_data()
+    bi, _ = orc.bm25_topk(terms, off, qt, qo, V, 50)
+    for _, s, i, li in res:
+        assert np.array_equal(i, ei) and np.array_equal(li, bi)
+        np.testing.assert_allclose(s, es, atol=1e-5)

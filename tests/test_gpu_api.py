@@ -187,3 +187,38 @@ def test_pipelined_batches_equal_unpipelined(dev):
         cand = torch.from_numpy(rrf_fuse(b, ids.cpu().numpy())).to(dev)
         es, ei, _ = ix.rerank(Q, cand, 10)
         assert torch.equal(i, ei) and torch.equal(s, es)
+
+
+def test_pipelined_with_host_bm25_equals_sequential(dev):
+    """Stage 1 as a host callable (native BM25 run while the GPU scans): every
+    batch equals BM25 (oracle-checked lists) -> search -> RRF -> rerank done
+    one step at a time, and the planted docs are the final top-10."""
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    from hybrid_rag_colbertv2_amd.hybrid import PipelinedRetriever, rrf_fuse
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    N, B = 20000, 40
+    Qall = synth.make_queries(B, seed=6)
+    planted = synth.planted_ids(B, N, 10)
+    tokens, doclens = synth.make_shard(0, N, Qall, planted, dev)
+    ix = ColbertIndex(tokens, doclens)
+    terms, off, V = synth.bm25_shard(0, N, planted)
+    lex = NativeBM25(terms, off, V)
+    qt, qo = synth.bm25_queries(B)
+    spans = [(0, 16), (16, 17), (17, 40)]
+
+    def fn(a, b):
+        return lambda: lex.search(qt[qo[a]:qo[b]], qo[a:b + 1] - qo[a], 100)
+    batches = [(Qall[a:b].to(dev, torch.bfloat16), fn(a, b)) for a, b in spans]
+    got = PipelinedRetriever(ix, dev).run(batches)
+    oi, _ = orc.bm25_topk(terms[:off[2000]], off[:2001], qt, qo, V, 5)   # oracle spot check on a prefix
+    pi, _ = NativeBM25(terms[:off[2000]], off[:2001], V).search(qt, qo, 5)
+    assert np.array_equal(pi, oi)
+    for (a, b), (Q, f), (s, i) in zip(spans, batches, got):
+        bm, _ = f()
+        _, ids = ix.search(Q, 100)
+        cand = torch.from_numpy(rrf_fuse(bm, ids.cpu().numpy())).to(dev)
+        es, ei, _ = ix.rerank(Q, cand, 10)
+        assert torch.equal(i, ei) and torch.equal(s, es)
+        for r in range(b - a):
+            assert set(i[r].tolist()) == set(planted[a + r].tolist())
