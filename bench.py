@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check-queries", type=int, default=4)
     ap.add_argument("--no-pipeline", action="store_true", help="time unpipelined steps")
+    ap.add_argument("--native-exchange", action="store_true",
+                    help="N>1: run the all-gather / all-reduce inside the C ABI (cbv2_*_sharded) on torch's RCCL comm")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="index tokens: bf16 (config 3) or MXFP8 e4m3 + E8M0 (config 5)")
     args = ap.parse_args()
@@ -136,7 +138,8 @@ def main():
         tokens_ref = tokens                                          # kept only for the spot parity check
     else:
         ix = ColbertIndex(tokens, doclens, id_base=begin)
-    searcher = ShardedSearcher(ix)
+    searcher = ShardedSearcher(ix, native=args.native_exchange and world > 1 and backend == "nccl",
+                               lexical_k=args.k)
     Q = Qf.to(dev, torch.bfloat16)
     Q1 = Q[:1].contiguous()
     torch.cuda.synchronize()

@@ -7,7 +7,7 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "colbert_mi355x.hip")
-SRC_HOST = os.path.join(PKG, "csrc", "host_bm25.cpp")
+SRC_HOST = [os.path.join(PKG, "csrc", f) for f in ("host_bm25.cpp", "sharded.cpp")]
 HDR = os.path.join(ROOT, "include", "colbert_mi355x.h")
 LIB = os.path.join(PKG, "libcolbert_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -25,8 +25,8 @@ def stale(out: str, deps) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
-    if force or stale(LIB, [SRC, SRC_HOST, HDR, __file__]):
-        cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), SRC, SRC_HOST, "-o", LIB + ".tmp"]
+    if force or stale(LIB, [SRC, *SRC_HOST, HDR, __file__]):
+        cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), SRC, *SRC_HOST, "-ldl", "-o", LIB + ".tmp"]
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

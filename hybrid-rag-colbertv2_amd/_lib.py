@@ -49,6 +49,16 @@ _SIGS = {
     "cbv2_bm25_build_shard": (ctypes.c_int, [_p, _p, _i64, _i32, ctypes.c_float, ctypes.c_float, _i64, _i64,
                                              _i64, _p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_bm25_num_docs": (_i64, [_p]),
+    "cbv2_comm_init": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_comm_size": (ctypes.c_int, [_p]),
+    "cbv2_comm_rank": (ctypes.c_int, [_p]),
+    "cbv2_comm_destroy": (ctypes.c_int, [_p]),
+    "cbv2_sharded_workspace_bytes": (_sz, [_p, _p, _i32, _i32, _i32, _i32]),
+    "cbv2_search_sharded": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _sz, _p, _p,
+                                           _p, _p]),
+    "cbv2_search_sharded_local": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _sz, _p]),
+    "cbv2_search_sharded_exchange": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _p, _i32, _p, _sz, _p, _p, _p, _p]),
+    "cbv2_rerank_sharded": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
     "cbv2_bm25_destroy": (ctypes.c_int, [_p]),
 }
 

@@ -1202,20 +1202,20 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void merge_topk_kernel(const float* __restrict__ in_s,
                                                          const int32_t* __restrict__ in_i, int G, int B,
-                                                         int k, float* __restrict__ out_s,
+                                                         int k, size_t g_stride, float* __restrict__ out_s,
                                                          int32_t* __restrict__ out_i) {
   __shared__ uint64_t keys[kMergeMax];
   __shared__ int nvalid[64];
   const int b = blockIdx.x;
   for (int t = threadIdx.x; t < G * k; t += blockDim.x) {
     const int g = t / k, j = t % k;
-    const size_t src = ((size_t)g * B + b) * k + j;
+    const size_t src = (size_t)g * g_stride + (size_t)b * k + j;
     const int32_t id = in_i[src];
     keys[t] = id >= 0 ? rank_key(in_s[src], (uint32_t)id) : 0ull;
   }
   if (threadIdx.x < G) {
     int cnt = 0;
-    const size_t base = ((size_t)threadIdx.x * B + b) * k;
+    const size_t base = (size_t)threadIdx.x * g_stride + (size_t)b * k;
     while (cnt < k && in_i[base + cnt] >= 0) ++cnt;
     nvalid[threadIdx.x] = cnt;
   }
@@ -1775,7 +1775,17 @@ int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, in
   CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d]", kTopkMax);
   CBV2_REQUIRE((int64_t)G * k <= kMergeMax, "G*k must be <= %d", kMergeMax);
   hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores, in_ids, G,
-                     B, k, out_scores, out_ids);
+                     B, k, (size_t)B * k, out_scores, out_ids);
+  return launch_check("merge_topk_kernel");
+}
+
+// Internal (sharded.cpp): the same merge with shard g's lists at g * g_stride.
+int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
+                            size_t g_stride, float* out_scores, int32_t* out_ids, void* stream) {
+  CBV2_REQUIRE(G >= 1 && G <= 64 && B >= 1 && k >= 1 && k <= kTopkMax && (int64_t)G * k <= kMergeMax,
+               "bad merge sizes");
+  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores, in_ids, G,
+                     B, k, g_stride, out_scores, out_ids);
   return launch_check("merge_topk_kernel");
 }
 

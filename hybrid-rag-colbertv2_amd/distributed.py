@@ -51,6 +51,91 @@ class _DeviceOps:
         return select_topk(scores, k, ids=ids)
 
 
+class NativeExchange:
+    """The exchange inside libcolbert_mi355x.so (include/colbert_mi355x.h:
+    cbv2_search_sharded_local/_exchange, cbv2_rerank_sharded) over the RCCL
+    communicator torch.distributed's "nccl" backend already holds: scan,
+    all-gather and merges are all enqueued by C++ on the current stream, with
+    no Python between them."""
+
+    def __init__(self, index, group: Optional[dist.ProcessGroup] = None, lexical_k: int = 100):
+        import ctypes
+        import os
+
+        from . import _lib
+        self.index, self.dev, self.lexical_k = index, index.device, int(lexical_k)
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        if dist.get_backend(pg) != "nccl":
+            raise RuntimeError("the native exchange needs the RCCL ('nccl') backend")
+        warm = torch.zeros(1, device=self.dev)
+        dist.all_reduce(warm, group=group)                 # the communicator exists after one collective
+        torch.cuda.synchronize(self.dev)
+        comm_ptr = pg._get_backend(self.dev)._comm_ptr()
+        rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().cbv2_comm_init(comm_ptr, rccl.encode() if os.path.exists(rccl) else None,
+                                             ctypes.byref(h)))
+        self._h, self._lib = h, _lib
+        self.world = int(_lib.lib().cbv2_comm_size(h))
+        self.rank = int(_lib.lib().cbv2_comm_rank(h))
+        self._ws = None
+
+    def __del__(self):
+        try:
+            self._lib.lib().cbv2_comm_destroy(self._h)
+        except Exception:
+            pass
+
+    def _workspace(self, B: int, k: int, kb: int, C: int) -> torch.Tensor:
+        need = int(self._lib.lib().cbv2_sharded_workspace_bytes(self.index._h, self._h, B, k, kb, C))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty((need,), dtype=torch.uint8, device=self.dev)
+        return self._ws
+
+    def search(self, Q: torch.Tensor, k: int, lexical=None):
+        from .index import _stream_ptr
+        L = self._lib.lib()
+        _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
+        st = _stream_ptr(self.dev)
+        # the local scan is enqueued BEFORE stage 1 runs on the host, so the
+        # workspace is sized for up to ``lexical_k`` stage-1 ids per query
+        kb_cap = self.lexical_k if lexical is not None else 0
+        ws = self._workspace(B, k, kb_cap, 0)
+        self._lib.check(L.cbv2_search_sharded_local(self.index._h, self._h, self._lib.SCORERS["maxsim"], qptr, qdt,
+                                                    B, lq, int(k), kb_cap, ws.data_ptr(), ws.numel(), st))
+        kb = 0
+        out_s = torch.empty((B, k), dtype=torch.float32, device=self.dev)
+        out_i = torch.empty((B, k), dtype=torch.int32, device=self.dev)
+        li = ls = out_li = None
+        if lexical is not None:
+            lex_i, lex_s = lexical()
+            kb = int(lex_i.shape[1])
+            if lex_i.shape[0] != B or not 1 <= kb <= kb_cap:
+                raise ValueError(f"stage-1 lists must be [B, <= {kb_cap}] (got {lex_i.shape})")
+            li = torch.from_numpy(np.ascontiguousarray(lex_i, np.int32)).to(self.dev)
+            ls = torch.from_numpy(np.ascontiguousarray(lex_s, np.float32)).to(self.dev)
+            out_li = torch.empty((B, kb), dtype=torch.int32, device=self.dev)
+        self._lib.check(L.cbv2_search_sharded_exchange(
+            self.index._h, self._h, B, int(k), li.data_ptr() if li is not None else None,
+            ls.data_ptr() if ls is not None else None, kb, ws.data_ptr(), ws.numel(), out_s.data_ptr(),
+            out_i.data_ptr(), out_li.data_ptr() if out_li is not None else None, st))
+        return out_s, out_i, out_li
+
+    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+        from .index import _stream_ptr
+        _keep, qptr, _, B, lq = self.index._prep_query(Q, "maxsim")
+        cand = cand.to(device=self.dev, dtype=torch.int32).contiguous()
+        C = int(cand.shape[1])
+        ws = self._workspace(B, 1, 0, C)
+        out_s = torch.empty((B, k), dtype=torch.float32, device=self.dev)
+        out_i = torch.empty((B, k), dtype=torch.int32, device=self.dev)
+        out_p = torch.empty((B, k), dtype=torch.int32, device=self.dev)
+        self._lib.check(self._lib.lib().cbv2_rerank_sharded(
+            self.index._h, self._h, qptr, B, lq, cand.data_ptr(), C, int(k), ws.data_ptr(), ws.numel(),
+            out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), _stream_ptr(self.dev)))
+        return out_s, out_i, out_p
+
+
 class ShardedSearcher:
     """Global search / rerank over a corpus whose shards live on the ranks of ``group``.
 
@@ -58,13 +143,16 @@ class ShardedSearcher:
     ``rerank(Q, cand, 0)``); ``ops`` provides ``merge`` and ``select``.
     """
 
-    def __init__(self, local, group: Optional[dist.ProcessGroup] = None, ops=None, world: Optional[int] = None):
+    def __init__(self, local, group: Optional[dist.ProcessGroup] = None, ops=None, world: Optional[int] = None,
+                 native: bool = False, lexical_k: int = 100):
         self.local = local
         self.group = group
         self.ops = ops if ops is not None else _DeviceOps()
         if world is None:
             world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.world = world
+        # native=True: the whole exchange runs inside the C ABI (NativeExchange)
+        self._nx = NativeExchange(local, group, lexical_k) if native else None
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
@@ -75,6 +163,8 @@ class ShardedSearcher:
         return out
 
     def search(self, Q: torch.Tensor, k: int):
+        if self._nx is not None:
+            return self._nx.search(Q, k)[:2]
         s, i = self.local.search(Q, k)
         if self.world == 1:
             return s, i
@@ -91,6 +181,8 @@ class ShardedSearcher:
         same (score desc, id asc) rule, which reproduces the unsharded stage 1
         exactly because the shards were built with global statistics.
         """
+        if self._nx is not None:
+            return self._nx.search(Q, k, lexical)
         s, i = self.local.search(Q, k)
         if lexical is None:
             if self.world == 1:
@@ -117,6 +209,8 @@ class ShardedSearcher:
         return self.ops.merge(S, I, k)
 
     def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+        if self._nx is not None:
+            return self._nx.rerank(Q, cand, k)
         if self.world == 1:
             return self.local.rerank(Q, cand, k)                                           # fused select
         raw = self.local.rerank(Q, cand, 0)                                                # [B, C]

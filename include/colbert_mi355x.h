@@ -192,6 +192,51 @@ int cbv2_bm25_build_shard(const int32_t* doc_terms, const int64_t* doc_offsets, 
 int64_t cbv2_bm25_num_docs(const cbv2_bm25* index);
 int cbv2_bm25_destroy(cbv2_bm25* index);
 
+/* Multi-GPU exchange (SURVEY.md §8(b) "cbv2_comm_init(ncclComm_t) +
+ * cbv2_search_sharded", §8(e)).  No reference counterpart: the reference is
+ * single-process.  One process per GPU, each holding the shard
+ * [id_base, id_base + n) of the corpus as a cbv2_index.
+ *
+ * cbv2_comm_init — borrow an initialised RCCL communicator (ncclComm_t; e.g.
+ *   torch's ProcessGroupNCCL._comm_ptr()).  rccl_library: path of the RCCL
+ *   library that created it (NULL: "librccl.so"); the collectives are
+ *   resolved from that library.  cbv2_comm_destroy does not free the comm.
+ * cbv2_search_sharded — every rank: local scan + top-k, plus (kb > 0) this
+ *   rank's stage-1 BM25 top-kb over its doc shard (global ids; host or device
+ *   pointers), -> ONE ncclAllGather -> merged global top-k [B][k] and merged
+ *   BM25 ids [B][kb] (out_lex_ids, device), identical on every rank.
+ *   Workspace: cbv2_sharded_workspace_bytes(ix, comm, B, k, kb, 0).
+ *   The same in two calls, so a host stage-1 can run while the GPU scans:
+ *   cbv2_search_sharded_local (enqueue the local scan) then
+ *   cbv2_search_sharded_exchange (lists in, all-gather, merges) with the SAME
+ *   workspace, sized for the exchange's kb (the local call writes only the
+ *   head of the send block; its kb just sizes its workspace check).
+ * cbv2_rerank_sharded — every rank scores the candidates it owns (-inf
+ *   otherwise) -> ncclAllReduce(MAX) -> top-k select; cand [B][C] global ids
+ *   (device).  Workspace >= B*C*4 bytes (or the size above with C).
+ * Collectives are enqueued on `stream`; every rank must call in the same
+ * order (as with any RCCL program).                                        */
+typedef struct cbv2_comm cbv2_comm;
+int cbv2_comm_init(void* nccl_comm, const char* rccl_library, cbv2_comm** out);
+int cbv2_comm_size(const cbv2_comm* comm);
+int cbv2_comm_rank(const cbv2_comm* comm);
+int cbv2_comm_destroy(cbv2_comm* comm);
+size_t cbv2_sharded_workspace_bytes(const cbv2_index* index, const cbv2_comm* comm, int32_t B, int32_t k,
+                                    int32_t kb, int32_t C);
+int cbv2_search_sharded(cbv2_index* index, cbv2_comm* comm, int32_t scorer, const void* Q, int32_t q_dtype,
+                        int32_t B, int32_t lq, int32_t k, const int32_t* lex_ids, const float* lex_scores,
+                        int32_t kb, void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids,
+                        int32_t* out_lex_ids, void* stream);
+int cbv2_search_sharded_local(cbv2_index* index, cbv2_comm* comm, int32_t scorer, const void* Q, int32_t q_dtype,
+                              int32_t B, int32_t lq, int32_t k, int32_t kb, void* workspace, size_t workspace_bytes,
+                              void* stream);
+int cbv2_search_sharded_exchange(cbv2_index* index, cbv2_comm* comm, int32_t B, int32_t k, const int32_t* lex_ids,
+                                 const float* lex_scores, int32_t kb, void* workspace, size_t workspace_bytes,
+                                 float* out_scores, int32_t* out_ids, int32_t* out_lex_ids, void* stream);
+int cbv2_rerank_sharded(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t B, int32_t lq,
+                        const int32_t* cand, int32_t C, int32_t k, void* workspace, size_t workspace_bytes,
+                        float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

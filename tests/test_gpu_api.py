@@ -222,3 +222,51 @@ def test_pipelined_with_host_bm25_equals_sequential(dev):
         assert torch.equal(i, ei) and torch.equal(s, es)
         for r in range(b - a):
             assert set(i[r].tolist()) == set(planted[a + r].tolist())
+
+
+def test_native_exchange_rccl_world1(dev, tmp_path):
+    """cbv2_search_sharded_local/_exchange and cbv2_rerank_sharded over torch's
+    RCCL communicator (one rank on this box: the all-gather/all-reduce run for
+    real with G=1; G>1 is the same code path with a longer receive buffer, and
+    the protocol itself is covered at world 2 over gloo)."""
+    import torch.distributed as dist
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher
+    from hybrid_rag_colbertv2_amd.hybrid import PipelinedRetriever
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        N, B = 5000, 12
+        Qf = synth.make_queries(B, seed=8)
+        planted = synth.planted_ids(B, N, 10)
+        tokens, doclens = synth.make_shard(0, N, Qf, planted, dev)
+        ix = ColbertIndex(tokens, doclens)
+        terms, off, V = synth.bm25_shard(0, N, planted)
+        lex = NativeBM25(terms, off, V)
+        qt, qo = synth.bm25_queries(B)
+        Q = Qf.to(dev, torch.bfloat16)
+        ss = ShardedSearcher(ix, native=True)
+        assert ss._nx.world == 1 and ss._nx.rank == 0
+        s, i, li = ss.search_hybrid(Q, 100, lambda: lex.search(qt, qo, 100))
+        es, ei = ix.search(Q, 100)
+        bi, _ = lex.search(qt, qo, 100)
+        assert torch.equal(s, es) and torch.equal(i, ei)
+        assert np.array_equal(li.cpu().numpy(), bi)
+        s2, i2 = ss.search(Q, 37)
+        assert torch.equal(i2, ix.search(Q, 37)[1])
+        cand = i[:, :50].contiguous()
+        r = ss.rerank(Q, cand, 10)
+        er = ix.rerank(Q, cand, 10)
+        assert all(torch.equal(a, b) for a, b in zip(r, er))
+        # the pipelined path over the native exchange equals the plain one
+        batches = [(Q[a:b], (lambda a=a, b=b: lex.search(qt[qo[a]:qo[b]], qo[a:b + 1] - qo[a], 100)))
+                   for a, b in [(0, 5), (5, 12)]]
+        got = PipelinedRetriever(ss, dev).run(batches)
+        ref = PipelinedRetriever(ix, dev).run(batches)
+        for (gs, gi), (rs, ri) in zip(got, ref):
+            assert torch.equal(gi, ri) and torch.equal(gs, rs)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
