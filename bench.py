@@ -49,7 +49,7 @@ PEAK_FP8_TFLOPS = 5000.0                   # MI355X dense fp8 (block-scaled MFMA
 FLOP_PER_PAIR = 2 * LQ * LD * DIM          # 1,048,576 algorithmic FLOP per (query, doc)
 PEAK_BF16_TFLOPS = 2500.0                  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
-SCAN_KERNEL = "maxsim_scan16_kernel"      # the B=256 scan (auto dispatch, 32 queries / workgroup)
+SCAN_KERNEL = "maxsim_scan16x4_kernel"    # the B=256 scan (auto dispatch: doc-interleaved tiles, 32 queries / workgroup)
 
 
 def log(*a):
@@ -216,14 +216,17 @@ def main():
     scan_avg = sum(scan_ms) / len(scan_ms)
     n_local = end - begin
     achieved = B * n_local * FLOP_PER_PAIR / (scan_avg * 1e-3) / 1e12
-    traffic = None
+    # HBM bytes per launch from the committed PMC passes of the same kernel and
+    # shape (tools/profile_round.sh -> tools/pmc_summary.py); null otherwise
+    traffic = clock = None
     pmc = os.path.join(ROOT, "profiles", "pmc_scan.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            d = json.load(f)
-        if d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == (
-                "maxsim_scan_f8_kernel" if args.dtype == "fp8" else SCAN_KERNEL):
-            traffic = d.get("hbm_bytes_per_launch")
+            entries = json.load(f).get("entries", [])
+        want = "maxsim_scan_f8_kernel" if args.dtype == "fp8" else SCAN_KERNEL
+        for d in entries:
+            if d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == want:
+                traffic, clock = d.get("hbm_bytes_per_launch"), d.get("clock_ghz")
 
     # ---- spot parity: oracle MaxSim of the final candidates for a few queries
     from oracle import oracle as orc
@@ -270,7 +273,8 @@ def main():
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
             "roofline": {"bound": "mfma", "kernel": kern, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "traffic": traffic, "avg_ms": round(scan_avg, 3)},
+                         "traffic": traffic, "avg_ms": round(scan_avg, 3),
+                         "clock_ghz_under_load": round(clock, 3) if clock else None},
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad},
         }

@@ -450,6 +450,200 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// The production B > 8 scan: doc-interleaved row tiles.  A 16-row A tile
+// holds 4 consecutive tokens of each of 4 docs (rows 4g..4g+3 = doc g), so
+// the lanes of MFMA output group g accumulate exactly doc g's row maxima:
+// the per-doc epilogue needs no cross-group fold (no permlane swaps), just one
+// 16-lane DPP sum per query per 4 docs — ~8x less epilogue VALU than
+// maxsim_scan16_kernel, whose epilogue ran with no MFMA work to hide under.
+// Each iteration streams 32 tokens of 4 docs (32 KiB) HBM -> LDS by LDS-DMA
+// into a 3-deep ring (the next iteration's pieces stay in flight across the
+// barrier); 4 iterations per doc group.  Within an iteration the 8 tiles x
+// 2*QW MFMA chains run as one software pipeline: chain k's row max is taken
+// after chains k+1..k+D have issued, so the MFMA->VALU read hazard is covered
+// by MFMAs instead of s_nop.  LDS image [4 docs][32 tokens][16 slots of 16 B]
+// with slot p of row R at p ^ swz4(R): the 16 rows a ds_read_b128 lane group
+// touches get 16 distinct slots (conflict-free).  Per (query, doc) the dot
+// products, the max and the column-sum order are those of doc16 + reduce16,
+// so scores are bit-identical to every other scan and to the rerank kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int swz4(int R) { return (((R >> 5) & 3) << 2) | (R & 3); }
+
+// Full iteration (all 4 docs valid for its 32 tokens): 8 tiles, pipelined.
+template <int QW, int D>
+__device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
+                                           float (&m)[QW][2]) {
+  constexpr int NC = 2 * QW;
+  constexpr int NK = 8 * NC;
+  const int c = lane & 15, g = lane >> 4;
+  const uint8_t* rowp = buf + (32 * (c >> 2) + (c & 3)) * kRowBytes;  // row of tile t: + 4t rows
+  auto frag = [&](int t, bf16x8 (&a)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      a[s] = *reinterpret_cast<const bf16x8*>(rowp + 4 * t * kRowBytes + 16 * ((4 * g + s) ^ c));
+  };
+  bf16x8 a[2][4];
+  f32x4 acc[D + 1];
+  frag(0, a[0]);
+#pragma unroll
+  for (int k = 0; k < NK + D; ++k) {
+    if (k < NK) {
+      const int t = k / NC, cc = k % NC;
+      if (cc == 0 && t + 1 < 8) frag(t + 1, a[(t + 1) & 1]);
+      f32x4 x = f32x4{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t & 1][s], qf[cc >> 1][cc & 1][s], x, 0, 0, 0);
+      acc[k % (D + 1)] = x;
+    }
+    if (k >= D) {
+      const int kk = k - D, pc = kk % NC;
+      const f32x4& y = acc[kk % (D + 1)];
+      float& mm = m[pc >> 1][pc & 1];
+      mm = fmaxf(fmaxf(fmaxf(fmaxf(mm, y[0]), y[1]), y[2]), y[3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Iteration j with ragged docs: per-lane-group -inf C-init masks padding rows.
+template <int QW>
+__device__ __forceinline__ void iter4_ragged(const uint8_t* buf, int lane, int j, int dl_g, int dl_max,
+                                             const bf16x8 (&qf)[QW][2][4], float (&m)[QW][2]) {
+  const int c = lane & 15, g = lane >> 4;
+  const uint8_t* rowp = buf + (32 * (c >> 2) + (c & 3)) * kRowBytes;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int tok0 = 32 * j + 4 * t;
+    if (tok0 >= dl_max) break;
+    bf16x8 a[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      a[s] = *reinterpret_cast<const bf16x8*>(rowp + 4 * t * kRowBytes + 16 * ((4 * g + s) ^ c));
+    f32x4 init;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) init[r] = (tok0 + r < dl_g) ? 0.0f : neg_inf();
+    tile16<QW>(a, qf, init, m);
+  }
+}
+
+template <int WAVES, int QW, int D = 2, int NBUF = 3>
+__global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
+    int64_t chunk_docs) {
+  constexpr int QPB = WAVES * QW;
+  constexpr int kPieces = kDocBytes / 1024;  // 32 x 1 KiB per iteration
+  constexpr int kPiecesPerWave = kPieces / WAVES;
+  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
+  static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kDocBytes];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int qg = lin % nq_groups;
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;
+  const int nd = (int)(d_end - d_begin);
+  const int ngr = (nd + 3) >> 2;
+
+  bf16x8 qf[QW][2][4];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QPB + wave * QW + q, B, lq, lane, qf[q]);
+
+  // LDS-DMA piece p = rows 4p..4p+3 of the image = doc p>>3, tokens 32j + 4(p&7) + 0..3
+  uint32_t src_off[kPiecesPerWave];
+  int src_doc[kPiecesPerWave];
+#pragma unroll
+  for (int jj = 0; jj < kPiecesPerWave; ++jj) {
+    const int R = 4 * (wave * kPiecesPerWave + jj) + (lane >> 4);
+    src_off[jj] = (R & 31) * kRowBytes + 16 * ((lane & 15) ^ swz4(R));
+    src_doc[jj] = R >> 5;
+  }
+  auto issue = [&](int it, int buf) {
+    const int G = it >> 2, j = it & 3;
+#pragma unroll
+    for (int jj = 0; jj < kPiecesPerWave; ++jj) {
+      const int piece = wave * kPiecesPerWave + jj;
+      int d = 4 * G + src_doc[jj];
+      d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
+      const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * 32 * kRowBytes + src_off[jj];
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16, 0,
+                                       0);
+    }
+  };
+
+  float sc[QW];
+  float m[QW][2];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
+  int dl_g = 0, dl_min = 0, dl_max = 0;
+
+  const int nit = 4 * ngr;
+  issue(0, 0);
+  if (NBUF == 3 && nit > 1) issue(1, 1);
+  int cur = 0;           // ring slot of iteration it
+  bool stored = false;   // global stores issued last iteration (they count in vmcnt)
+  for (int it = 0; it < nit; ++it) {
+    if (NBUF == 3 && it + 1 < nit && !stored)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    stored = false;
+    if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
+    if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+    const uint8_t* buf = smem + cur * kDocBytes;
+    cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+
+    const int G = it >> 2, j = it & 3;
+    if (j == 0) {
+      int dl4[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int v = (4 * G + x < nd) ? doclens[d_begin + 4 * G + x] : 0;
+        dl4[x] = v < 0 ? 0 : (v > kLd ? kLd : v);
+      }
+      dl_min = min(min(dl4[0], dl4[1]), min(dl4[2], dl4[3]));
+      dl_max = max(max(dl4[0], dl4[1]), max(dl4[2], dl4[3]));
+      dl_g = g == 0 ? dl4[0] : (g == 1 ? dl4[1] : (g == 2 ? dl4[2] : dl4[3]));
+#pragma unroll
+      for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    }
+    if (32 * j + 32 <= dl_min)
+      iter4_full<QW, D>(buf, lane, qf, m);
+    else if (32 * j < dl_max)
+      iter4_ragged<QW>(buf, lane, j, dl_g, dl_max, qf, m);
+    if (j == 3) {
+      // doc 4G+g's score in every lane of group g; lane c of the 64-doc block
+      // register keeps doc group c, so lane (c, g) holds doc 4c+g of the block
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const float v = dpp_row_sum16((c < lq ? m[q][0] : 0.0f) + (16 + c < lq ? m[q][1] : 0.0f));
+        sc[q] = (c == (G & 15)) ? v : sc[q];
+      }
+      if ((G & 15) == 15 || G == ngr - 1) {
+        const int dd = 64 * (G >> 4) + 4 * c + g;
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const int qi = qg * QPB + wave * QW + q;
+          if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+        }
+        stored = true;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Small-batch scan (B <= 2 per query group): HBM-bound, so no LDS staging —
 // every wave owns a contiguous doc range and streams each doc (32 KiB, 128 B
 // per lane per row tile) straight into VGPRs; 8 waves per CU keep ~256 KiB in
@@ -1387,7 +1581,7 @@ int launch_check(const char* what) {
 enum ScanVariant {
   kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
-  kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScanAuto = -1
+  kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
 // 1: 58.3 %, 2: 61.7 %, 3: 65.3 %, 4: 59.4 %, 5: 52.0 %, 6: 61.2 %, 8: 54.8 %
@@ -1441,7 +1635,8 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
                 int variant = kDefaultScan) {
   if (ix->n == 0) return CBV2_OK;
   if (variant == kScanAuto)
-    variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2) : (B <= kSmallLdsMaxB ? kScan16W4 : kScan16W8);
+    variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2)
+                               : (B <= kSmallLdsMaxB ? kScan16x4W4 : kScan16x4W8);
   switch (variant) {
     case kScanDirectQ1:
       return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
@@ -1465,6 +1660,12 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan<8, 3, 1>(maxsim_scan16_kernel<8, 3>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
     case kScan16W4Q2:
       return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
+    case kScan16x4W8:
+      return launch_scan<8, 4, 1>(maxsim_scan16x4_kernel<8, 4>, ix, Q, B, lq, out, ld_out, st,
+                                  "maxsim_scan16x4_kernel");
+    case kScan16x4W4:
+      return launch_scan<4, 4, 2>(maxsim_scan16x4_kernel<4, 4, 2, 2>, ix, Q, B, lq, out, ld_out, st,
+                                  "maxsim_scan16x4_kernel");
     default:
       return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
   }

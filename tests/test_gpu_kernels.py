@@ -257,11 +257,12 @@ def test_errors_raise_without_launch(dev):
 
 
 def test_small_batch_scan_bit_identical_to_batched(dev):
-    """B<=4 runs the direct (HBM-streaming) scan, B>4 the LDS scan: same bits."""
+    """B<=8 runs the direct (HBM-streaming) scan, 9..16 the 4-wave and larger B the
+    8-wave doc-interleaved LDS scan: same bits."""
     docs, doclens, Q = make_case(123, 900, 20, 32)
     ix = ColbertIndex(docs.to(dev), doclens.to(dev))
     full = ix.score(Q.to(dev))
-    for lo, hi in [(0, 1), (3, 5), (7, 10), (10, 14), (5, 6)]:
+    for lo, hi in [(0, 1), (3, 5), (7, 10), (10, 14), (5, 6), (2, 14), (0, 16), (1, 18)]:
         part = ix.score(Q[lo:hi].to(dev))
         assert torch.equal(part, full[lo:hi]), (lo, hi)
     s1, i1 = ix.search(Q[:1].to(dev), k=30)

@@ -1,35 +1,50 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs for one kernel: per-launch HBM bytes.
+"""Summarise rocprofv3 --pmc CSVs (one counter per pass) for one kernel.
 
-gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half of the
-bytes of a wide coalesced read -> x2; WRITE_SIZE is exact for 16-B stores.
-Both counters are in KB (x1024).
-usage: pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel-substr> <out.json> [batch docs]
+usage: pmc_summary.py <out.json> <kernel-substr> <batch> <docs> <dtype> <csv>...
+Each CSV is a counter_collection.csv of one pass.  Per-launch values are
+averaged over the kernel's dispatches.  Derived (MI355X_MICROARCH.md):
+  hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+      (gfx950: FETCH_SIZE reports half of a wide coalesced read; both in KB)
+  clock_ghz = GRBM_GUI_ACTIVE / 8 / launch duration (summed over 8 XCDs)
+The output file holds one entry per (kernel, dtype); an existing entry for
+the same pair is replaced.
 """
 import csv
 import json
+import os
 import sys
 
-
-def per_dispatch(path, kernel, counter):
-    vals = {}
+out_path, kernel, batch, docs, dtype = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+vals, durs = {}, []
+for path in sys.argv[6:]:
+    per = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                d = row.get("Dispatch_Id") or row.get("Correlation_Id")
-                vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
-
-
-fetch = per_dispatch(sys.argv[1], sys.argv[3], "FETCH_SIZE")
-write = per_dispatch(sys.argv[2], sys.argv[3], "WRITE_SIZE")
-f_avg = sum(fetch) / len(fetch)
-w_avg = sum(write) / len(write)
-out = {"kernel": sys.argv[3], "dispatches": [len(fetch), len(write)],
-       "fetch_size_kb_raw": f_avg, "write_size_kb": w_avg,
-       "hbm_bytes_per_launch": (2.0 * f_avg + w_avg) * 1024.0,
-       "correction": "FETCH_SIZE x2 (gfx950 wide-read under-count), both KB x1024"}
-if len(sys.argv) > 6:
-    out["batch"], out["docs_per_gpu"] = int(sys.argv[5]), int(sys.argv[6])
-json.dump(out, open(sys.argv[4], "w"), indent=1)
-print(json.dumps(out))
+            if kernel not in row.get("Kernel_Name", ""):
+                continue
+            d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            c = row["Counter_Name"]
+            per.setdefault(c, {}).setdefault(d, 0.0)
+            per[c][d] += float(row["Counter_Value"])
+            if c.startswith("GRBM_GUI_ACTIVE"):
+                durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    for c, byd in per.items():
+        vals[c] = {"per_launch": sum(byd.values()) / len(byd), "dispatches": len(byd)}
+e = {"kernel": kernel, "dtype": dtype, "batch": batch, "docs_per_gpu": docs, "counters": vals}
+if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+    e["hbm_bytes_per_launch"] = (2.0 * vals["FETCH_SIZE"]["per_launch"] + vals["WRITE_SIZE"]["per_launch"]) * 1024.0
+    e["correction"] = "FETCH_SIZE x2 (gfx950 wide-read under-count), both KB x1024"
+if "GRBM_GUI_ACTIVE" in vals and durs:
+    d = sorted(durs)[len(durs) // 2]
+    e["profiled_launch_s"] = d
+    e["clock_ghz"] = vals["GRBM_GUI_ACTIVE"]["per_launch"] / 8.0 / d / 1e9
+doc = {"entries": []}
+if os.path.exists(out_path):
+    with open(out_path) as f:
+        old = json.load(f)
+    doc["entries"] = [x for x in old.get("entries", []) if (x["kernel"], x.get("dtype")) != (kernel, dtype)]
+doc["entries"].append(e)
+with open(out_path, "w") as f:
+    json.dump(doc, f, indent=1)
+print(json.dumps(e))

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Scan-only workload for rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE).
+"""Scan-only workload for rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE,
+GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES: one counter per pass).
 
-Builds the bench's synthetic 1M-doc index and runs the MaxSim scan kernel
-(B=256) a few times; tools/pmc_summary.py turns the counter CSVs into
-profiles/pmc_scan.json, which bench.py reports as roofline.traffic.
+Builds the bench's synthetic 1M-doc index (bf16, or MXFP8 via the HIP
+quantizer) and runs the MaxSim scan kernel (B=256) a few times;
+tools/pmc_summary.py turns the counter CSVs into profiles/pmc_scan.json, which
+bench.py reports as roofline.traffic.
 """
 import argparse
 import os
@@ -20,14 +22,19 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--docs", type=int, default=1_000_000)
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 Qf = synth.make_queries(a.batch, 32, seed=1)
 planted = synth.planted_ids(a.batch, a.docs, 10, seed=2)
 tokens, doclens = synth.make_shard(0, a.docs, Qf, planted, dev, seed=0)
-ix = ColbertIndex(tokens, doclens)
+if a.dtype == "fp8":
+    ix = ColbertIndex.mxfp8(tokens, doclens)
+    del tokens
+else:
+    ix = ColbertIndex(tokens, doclens)
 Q = Qf.to(dev, torch.bfloat16)
 for _ in range(a.reps):
     ix.score(Q)
 torch.cuda.synchronize()
-print("done", a.docs, a.batch, a.reps)
+print("done", a.dtype, a.docs, a.batch, a.reps)

@@ -1,9 +1,324 @@
 // Scan-kernel A/B lab (development tool, not part of the product ABI).
 // Includes the product source so every variant is the exact production code,
 // and exports one entry point that launches a chosen scan variant.
+// Variants >= 100 are experimental copies of maxsim_scan16_kernel<8,4>:
+//   100: same code path (sanity)        101: epilogue reduced to one add (INVALID scores: timing only)
+//   102: one max per MFMA chain (INVALID) 103: waves 4-7 defer each doc's epilogue to mid-next-doc
+//   104: full docs as a software-pipelined chain stream (doc16_pipe) with sched_barriers;  105: same, no barriers
+//   106: doc16_pipe with sched_group_barrier (MFMA x2, VALU x3, MFMA x2) per chain
+//   107 / 108: 2 / 4 independent chains interleaved by k-step (tile16_il)
+//   111 / 112 / 113: doc16_deep, chain k's max after chains k+1..k+D (D = 1 / 2 / 3)
+// The doc-interleaved kernel these experiments led to is in the product
+// (maxsim_scan16x4_kernel, variants 11/12); its lab history: pipeline depth
+// D=1/2/3 70.8/74.2/74.1 %, 3-deep LDS ring +0.4 %, without doc streaming 76.0 %.
+//   109: no doc streaming and no barrier (doc 0's LDS image reused; INVALID)  110: same with the per-doc barrier
 #include "../hybrid-rag-colbertv2_amd/csrc/colbert_mi355x.hip"
+
+namespace {
+
+template <int QW>
+__device__ __forceinline__ void tile16_cheap(const bf16x8 (&a)[4], const bf16x8 (&qf)[QW][2][4], float (&m)[QW][2]) {
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      f32x4 acc = f32x4{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], qf[q][ct][s], acc, 0, 0, 0);
+      m[q][ct] = fmaxf(m[q][ct], acc[0] + acc[3]);
+    }
+  }
+}
+
+// Row tile with NI independent MFMA chains interleaved by k-step (chains of
+// the same tile share the A fragment), so one wave keeps several MFMAs in
+// flight instead of waiting on each chain's dependent accumulation.
+template <int QW, int NI>
+__device__ __forceinline__ void tile16_il(const bf16x8 (&a)[4], const bf16x8 (&qf)[QW][2][4], float (&m)[QW][2]) {
+  constexpr int NC = 2 * QW;
+#pragma unroll
+  for (int c0 = 0; c0 < NC; c0 += NI) {
+    f32x4 acc[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[j] = f32x4{};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int c = c0 + j;
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], qf[c >> 1][c & 1][s], acc[j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int c = c0 + j;
+      float& mm = m[c >> 1][c & 1];
+      mm = __builtin_fmaxf(__builtin_fmaxf(mm, __builtin_fmaxf(acc[j][0], acc[j][1])),
+                           __builtin_fmaxf(acc[j][2], acc[j][3]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Deeper pipeline: chain k's max runs after chains k+1 .. k+D have issued
+// (D+1 accumulators), so the MFMA->VALU read hazard is covered by MFMAs
+// instead of s_nop; the max is two v_max3 (exact, any association).
+template <int QW, int D, typename Frag>
+__device__ __forceinline__ void doc16_deep(Frag frag, const bf16x8 (&qf)[QW][2][4], float (&m)[QW][2]) {
+  constexpr int NC = 2 * QW;
+  constexpr int NK = kLd / 16 * NC;
+#pragma unroll
+  for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+  bf16x8 a[2][4];
+  f32x4 acc[D + 1];
+  frag(0, a[0]);
+#pragma unroll
+  for (int k = 0; k < NK + D; ++k) {
+    if (k < NK) {
+      const int rt = k / NC, c = k % NC;
+      if (c == 0 && rt + 1 < kLd / 16) frag(rt + 1, a[(rt + 1) & 1]);
+      const int q = c >> 1, ct = c & 1;
+      f32x4 x = f32x4{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt & 1][s], qf[q][ct][s], x, 0, 0, 0);
+      acc[k % (D + 1)] = x;
+    }
+    if (k >= D) {
+      const int kk = k - D;
+      const int pc = kk % NC;
+      const f32x4& y = acc[kk % (D + 1)];
+      float& mm = m[pc >> 1][pc & 1];
+      mm = __builtin_fmaxf(__builtin_fmaxf(mm, __builtin_fmaxf(y[0], y[1])), __builtin_fmaxf(y[2], y[3]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Full doc as one software-pipelined stream of 8 tiles x 2*QW MFMA chains:
+// chain k's 4 MFMAs are issued while chain k-1's max runs (2 accumulators);
+// sched_barrier keeps hipcc from re-serialising the chains.
+template <int QW, int SB, typename Frag>
+__device__ __forceinline__ void doc16_pipe(Frag frag, const bf16x8 (&qf)[QW][2][4], float (&m)[QW][2]) {
+  constexpr int NC = 2 * QW;
+#pragma unroll
+  for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+  bf16x8 a[2][4];
+  f32x4 acc[2];
+  frag(0, a[0]);
+#pragma unroll
+  for (int rt = 0; rt < kLd / 16; ++rt) {
+    if (rt + 1 < kLd / 16) frag(rt + 1, a[(rt + 1) & 1]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int k = rt * NC + c;
+      const int q = c >> 1, ct = c & 1;
+      f32x4 x = f32x4{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt & 1][s], qf[q][ct][s], x, 0, 0, 0);
+      acc[k & 1] = x;
+      if (k > 0) {
+        const int pc = (k - 1) % NC;
+        const f32x4& y = acc[(k - 1) & 1];
+        float& mm = m[pc >> 1][pc & 1];
+        mm = __builtin_fmaxf(__builtin_fmaxf(mm, __builtin_fmaxf(y[0], y[1])), __builtin_fmaxf(y[2], y[3]));
+      }
+      if (SB == 1) __builtin_amdgcn_sched_barrier(0);
+      if (SB == 2) {   // 2 MFMA, the previous chain's max (<= 3 VALU), 2 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  {
+    const int pc = NC - 1;
+    const f32x4& y = acc[(kLd / 16 * NC - 1) & 1];
+    float& mm = m[pc >> 1][pc & 1];
+    mm = __builtin_fmaxf(__builtin_fmaxf(mm, __builtin_fmaxf(y[0], y[1])), __builtin_fmaxf(y[2], y[3]));
+  }
+}
+
+template <int WAVES, int QW, int MODE>
+__global__ __launch_bounds__(WAVES * 64, 2) void scan16x_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
+    int64_t chunk_docs) {
+  constexpr int QPB = WAVES * QW;
+  constexpr int kPieces = kDocBytes / 1024;
+  constexpr int kPiecesPerWave = kPieces / WAVES;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * kDocBytes];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int g = lin % nq_groups;
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;
+  const int nd = (int)(d_end - d_begin);
+
+  bf16x8 qf[QW][2][4];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag16(Q, g * QPB + wave * QW + q, B, lq, lane, qf[q]);
+  uint32_t src_off[kPiecesPerWave];
+#pragma unroll
+  for (int j = 0; j < kPiecesPerWave; ++j) {
+    const int piece = wave * kPiecesPerWave + j;
+    const int t = 4 * piece + (lane >> 4);
+    src_off[j] = t * kRowBytes + 16 * ((lane & 15) ^ swz16(t));
+  }
+  auto issue = [&](int i, int buf) {
+    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kDocBytes;
+#pragma unroll
+    for (int j = 0; j < kPiecesPerWave; ++j) {
+      const int piece = wave * kPiecesPerWave + j;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(dbase + src_off[j]),
+                                       (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16, 0, 0);
+    }
+  };
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+
+  auto epilogue = [&](int j, float (&m)[QW][2]) {
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = MODE == 101 ? m[q][0] + m[q][1] : reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (j & 63)) ? v : sc[q];
+    }
+    if ((j & 63) == 63 || j == nd - 1) {
+      const int i0 = j & ~63;
+      const int cnt = j - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = g * QPB + wave * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  };
+
+  const bool defer = MODE == 103 && wave >= 4;
+  float mp[QW][2];
+  int jp = -1;
+
+  issue(0, 0);
+  if (MODE == 109 || MODE == 110) {      // timing probes: doc 0's image only (INVALID scores)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  for (int i = 0; i < nd; ++i) {
+    if (MODE != 109 && MODE != 110) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (i + 1 < nd) issue(i + 1, (i + 1) & 1);
+    } else if (MODE == 110) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    const uint8_t* buf = smem + ((MODE == 109 || MODE == 110) ? 0 : (i & 1) * kDocBytes);
+    int dl = doclens[d_begin + i];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    float m[QW][2];
+    auto frag = [&](int rt, bf16x8 (&a)[4]) { lds_afrag16(buf, rt, lane, a); };
+    if ((MODE == 104 || MODE == 105 || MODE == 106) && dl >= kLd) {
+      doc16_pipe<QW, MODE == 104 ? 1 : (MODE == 106 ? 2 : 0)>(frag, qf, m);
+      epilogue(i, m);
+    } else if ((MODE == 111 || MODE == 112 || MODE == 113) && dl >= kLd) {
+      doc16_deep<QW, (MODE >= 111 && MODE <= 113) ? MODE - 110 : 1>(frag, qf, m);
+      epilogue(i, m);
+    } else if ((MODE == 107 || MODE == 108) && dl >= kLd) {
+      constexpr int NI = MODE == 107 ? 2 : 4;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+      bf16x8 a0[4], a1[4];
+      frag(0, a0);
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; rt += 2) {
+        frag(rt + 1, a1);
+        tile16_il<QW, NI>(a0, qf, m);
+        if (rt + 2 < kLd / 16) frag(rt + 2, a0);
+        tile16_il<QW, NI>(a1, qf, m);
+      }
+      epilogue(i, m);
+    } else if (MODE == 102 && dl >= kLd) {
+#pragma unroll
+      for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+      bf16x8 a0[4], a1[4];
+      frag(0, a0);
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; rt += 2) {
+        frag(rt + 1, a1);
+        tile16_cheap<QW>(a0, qf, m);
+        if (rt + 2 < kLd / 16) frag(rt + 2, a0);
+        tile16_cheap<QW>(a1, qf, m);
+      }
+      epilogue(i, m);
+    } else if (MODE == 103 && dl >= kLd) {
+#pragma unroll
+      for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+      bf16x8 a0[4], a1[4];
+      frag(0, a0);
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; rt += 2) {
+        frag(rt + 1, a1);
+        tile16<QW>(a0, qf, f32x4{}, m);
+        if (rt + 2 < kLd / 16) frag(rt + 2, a0);
+        tile16<QW>(a1, qf, f32x4{}, m);
+        if (rt == 2 && defer && jp >= 0) {       // mid-doc: the previous doc's epilogue
+          epilogue(jp, mp);
+          jp = -1;
+        }
+      }
+      if (defer) {
+#pragma unroll
+        for (int q = 0; q < QW; ++q) mp[q][0] = m[q][0], mp[q][1] = m[q][1];
+        jp = i;
+      } else {
+        epilogue(i, m);
+      }
+    } else {
+      if (defer && jp >= 0) {
+        epilogue(jp, mp);
+        jp = -1;
+      }
+      doc16<QW>(frag, qf, dl, lane, m);
+      epilogue(i, m);
+    }
+  }
+  if (defer && jp >= 0) epilogue(jp, mp);
+}
+
+template <int MODE>
+int launch_x(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld, hipStream_t st) {
+  return launch_scan<8, 4, 1>(scan16x_kernel<8, 4, MODE>, ix, Q, B, lq, out, ld, st, "scan16x_kernel");
+}
+}  // namespace
 
 extern "C" int lab_scan(cbv2_index* ix, int variant, const void* Q, int B, int lq, float* out, int64_t ld,
                         void* stream) {
-  return scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld, (hipStream_t)stream, variant);
+  const uint16_t* q = (const uint16_t*)Q;
+  hipStream_t st = (hipStream_t)stream;
+  switch (variant) {
+    case 100: return launch_x<100>(ix, q, B, lq, out, ld, st);
+    case 101: return launch_x<101>(ix, q, B, lq, out, ld, st);
+    case 102: return launch_x<102>(ix, q, B, lq, out, ld, st);
+    case 103: return launch_x<103>(ix, q, B, lq, out, ld, st);
+    case 104: return launch_x<104>(ix, q, B, lq, out, ld, st);
+    case 105: return launch_x<105>(ix, q, B, lq, out, ld, st);
+    case 106: return launch_x<106>(ix, q, B, lq, out, ld, st);
+    case 107: return launch_x<107>(ix, q, B, lq, out, ld, st);
+    case 108: return launch_x<108>(ix, q, B, lq, out, ld, st);
+    case 109: return launch_x<109>(ix, q, B, lq, out, ld, st);
+    case 110: return launch_x<110>(ix, q, B, lq, out, ld, st);
+    case 111: return launch_x<111>(ix, q, B, lq, out, ld, st);
+    case 112: return launch_x<112>(ix, q, B, lq, out, ld, st);
+    case 113: return launch_x<113>(ix, q, B, lq, out, ld, st);
+    default: return scan_maxsim(ix, q, B, lq, out, ld, st, variant);
+  }
 }
