@@ -936,6 +936,202 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8_kernel(
   }
 }
 
+// Doc-interleaved f8 scan (the production B > 8 MXFP8 path; same design as
+// maxsim_scan16x4_kernel): each iteration stages 32 tokens of 4 docs (16 KiB
+// of e4m3 + 256 B of scales) into a 3-deep LDS ring; row tile t holds tokens
+// 4t..4t+3 of docs 0..3 in rows 4g..4g+3, so output lane group g is doc g and
+// the epilogue is one 16-lane DPP sum per query per 4 docs.  Image: row R =
+// 32*doc + token, 8 slots of 16 B with slot s at s ^ swz8x4(R) (the 8 rows of
+// one parity a lane group reads get 8 distinct slots); scales [128 rows][2].
+__device__ __forceinline__ int swz8x4(int R) { return (((R >> 5) & 3) << 1) | ((R >> 1) & 1); }
+constexpr int kF8IterBytes = 32 * 4 * kDim;        // 16 KiB of e4m3 per iteration
+constexpr int kF8IterStage = kF8IterBytes + 256;   // + 4 docs x 32 tokens x 2 scale bytes
+
+__device__ __forceinline__ void lds_afrag_f8x4(const uint8_t* buf, int t, int lane, i32x8& a, int& as) {
+  const int c = lane & 15, g = lane >> 4;
+  const int R = 32 * (c >> 2) + 4 * t + (c & 3);
+  const uint8_t* row = buf + R * kDim;
+  const int sw = swz8x4(R);
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g) ^ sw));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g + 1) ^ sw));
+  a = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  as = buf[kF8IterBytes + R * 2 + (g & 1)];
+}
+
+template <int QW, int D>
+__device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, const i32x8 (&qa)[QW][2],
+                                               const int (&qs)[QW][2], float (&m)[QW][2]) {
+  constexpr int NC = 2 * QW;
+  static_assert(D >= 1 && NC % (D + 1) == 0, "ring slot of chain k must be k % (D+1) across tiles");
+  i32x8 a[2];
+  int as[2];
+  f32x4 acc[D + 1];
+  lds_afrag_f8x4(buf, 0, lane, a[0], as[0]);
+  auto fold = [&](int k) {  // row max of chain k (k = t * NC + cc), issued D chains later
+    const int pc = k % NC;
+    const f32x4& y = acc[k % (D + 1)];
+    float& mm = m[pc >> 1][pc & 1];
+    mm = fmaxf(fmaxf(fmaxf(fmaxf(mm, y[0]), y[1]), y[2]), y[3]);
+  };
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) {
+      const int k = t * NC + cc;
+      if (cc == 0 && t + 1 < 8) lds_afrag_f8x4(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
+      acc[k % (D + 1)] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+          a[t & 1], qa[cc >> 1][cc & 1], f32x4{}, 0, 0, 0, as[t & 1], 0, qs[cc >> 1][cc & 1]);
+      if (k >= D) fold(k - D);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int k = 8 * NC - D; k < 8 * NC; ++k) fold(k);
+}
+
+template <int QW>
+__device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, int j, int dl_g, int dl_max,
+                                                 const i32x8 (&qa)[QW][2], const int (&qs)[QW][2],
+                                                 float (&m)[QW][2]) {
+  const int nt = min(8, (dl_max - 32 * j + 3) >> 2);
+#pragma unroll 1
+  for (int t = 0; t < nt; ++t) {
+    const int tok0 = 32 * j + 4 * t;
+    i32x8 a;
+    int as;
+    lds_afrag_f8x4(buf, t, lane, a, as);
+    f32x4 init;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) init[r] = (tok0 + r < dl_g) ? 0.0f : neg_inf();
+    tile_f8<QW>(a, as, qa, qs, init, m);
+  }
+}
+
+template <int WAVES, int QW, int D = 1, int NBUF = 3>   // D = 2 spills at QW = 8 (hipcc 7.2)
+__global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
+    const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
+    int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
+    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs) {
+  constexpr int QPB = WAVES * QW;
+  constexpr int kPieces = kF8IterBytes / 1024;  // 16 x 1 KiB per iteration
+  constexpr int kPiecesPerWave = kPieces / WAVES;
+  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kF8IterStage + 256];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int qg = lin % nq_groups;
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;
+  const int nd = (int)(d_end - d_begin);
+  const int ngr = (nd + 3) >> 2;
+
+  i32x8 qa[QW][2];
+  int qs[QW][2];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, qg * QPB + wave * QW + q, B, lq, lane, qa[q], qs[q]);
+
+  // piece p = image rows 8p..8p+7 (128 B each) = doc p>>2, tokens 32j + 8(p&3) + 0..7
+  uint32_t src_off[kPiecesPerWave];
+  int src_doc[kPiecesPerWave];
+#pragma unroll
+  for (int jj = 0; jj < kPiecesPerWave; ++jj) {
+    const int R = 8 * (wave * kPiecesPerWave + jj) + (lane >> 3);
+    src_off[jj] = (R & 31) * kDim + 16 * ((lane & 7) ^ swz8x4(R));
+    src_doc[jj] = R >> 5;
+  }
+  auto clamp_doc = [&](int d) { return d < nd ? d : nd - 1; };  // the last group's missing docs: rows masked
+  auto issue = [&](int it, int buf) {
+    const int G = it >> 2, j = it & 3;
+    uint8_t* sbuf = smem + buf * kF8IterStage;
+#pragma unroll
+    for (int jj = 0; jj < kPiecesPerWave; ++jj) {
+      const int piece = wave * kPiecesPerWave + jj;
+      const int d = clamp_doc(4 * G + src_doc[jj]);
+      const uint8_t* src = tokens + (size_t)(d_begin + d) * kF8DocBytes + (size_t)j * 32 * kDim + src_off[jj];
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + piece * 1024), 16, 0, 0);
+    }
+    if (wave == 0) {  // 4 docs x 64 scale bytes: lane L -> doc L>>4, bytes 4(L&15)
+      const int d = clamp_doc(4 * G + (lane >> 4));
+      const uint8_t* src = tscales + (size_t)(d_begin + d) * kF8ScaleBytes + (size_t)j * 64 + 4 * (lane & 15);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + kF8IterBytes), 4, 0, 0);
+    }
+  };
+  // vector-memory ops per wave per iteration (the vmcnt that leaves one iteration in flight)
+  const bool loader = wave == 0;
+
+  float sc[QW];
+  float m[QW][2];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
+  int dl_g = 0, dl_min = 0, dl_max = 0;
+
+  const int nit = 4 * ngr;
+  issue(0, 0);
+  if (NBUF == 3 && nit > 1) issue(1, 1);
+  int cur = 0;
+  bool stored = false;
+  for (int it = 0; it < nit; ++it) {
+    if (NBUF == 3 && it + 1 < nit && !stored) {
+      if (loader)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave + 1) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    stored = false;
+    if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
+    if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+    const uint8_t* buf = smem + cur * kF8IterStage;
+    cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+
+    const int G = it >> 2, j = it & 3;
+    if (j == 0) {
+      int dl4[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int v = (4 * G + x < nd) ? doclens[d_begin + 4 * G + x] : 0;
+        dl4[x] = v < 0 ? 0 : (v > kLd ? kLd : v);
+      }
+      dl_min = min(min(dl4[0], dl4[1]), min(dl4[2], dl4[3]));
+      dl_max = max(max(dl4[0], dl4[1]), max(dl4[2], dl4[3]));
+      dl_g = g == 0 ? dl4[0] : (g == 1 ? dl4[1] : (g == 2 ? dl4[2] : dl4[3]));
+#pragma unroll
+      for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    }
+    if (32 * j + 32 <= dl_min)
+      iter_f8x4_full<QW, D>(buf, lane, qa, qs, m);
+    else if (32 * j < dl_max)
+      iter_f8x4_ragged<QW>(buf, lane, j, dl_g, dl_max, qa, qs, m);
+    if (j == 3) {
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const float v = dpp_row_sum16((c < lq ? m[q][0] : 0.0f) + (16 + c < lq ? m[q][1] : 0.0f));
+        sc[q] = (c == (G & 15)) ? v : sc[q];
+      }
+      if ((G & 15) == 15 || G == ngr - 1) {
+        const int dd = 64 * (G >> 4) + 4 * c + g;
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const int qi = qg * QPB + wave * QW + q;
+          if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+        }
+        stored = true;
+      }
+    }
+  }
+}
+
 // Small-batch f8 scan: one doc chunk per wave, docs streamed to VGPRs.
 template <int QW>
 __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
@@ -1701,9 +1897,9 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = (int64_t)nq_groups * n_chunks;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_f8_kernel<kF8Waves, kF8QW>), dim3((unsigned)grid), dim3(kF8Waves * 64), 0, st,
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW>), dim3((unsigned)grid), dim3(kF8Waves * 64), 0, st,
                      ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
-  return launch_check("maxsim_scan_f8_kernel");
+  return launch_check("maxsim_scan_f8x4_kernel");
 }
 
 int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {

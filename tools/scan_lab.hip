@@ -322,3 +322,23 @@ extern "C" int lab_scan(cbv2_index* ix, int variant, const void* Q, int B, int l
     default: return scan_maxsim(ix, q, B, lq, out, ld, st, variant);
   }
 }
+
+// MXFP8 scans: variant 0 = the per-doc maxsim_scan_f8_kernel (round-1
+// production), 1 = the doc-interleaved maxsim_scan_f8x4_kernel.
+extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B, int lq, float* out, int64_t ld,
+                           void* stream) {
+  const uint8_t* Qb = (const uint8_t*)Qbuf;
+  const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+  hipStream_t st = (hipStream_t)stream;
+  if (variant == 1 || B <= kF8DirectMaxB) return scan_f8(ix, Qb, B, lq, out, ld, st);
+  constexpr int QPB = kF8Waves * kF8QW;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  int64_t n_chunks = (cu_count(ix->device) + nq_groups - 1) / nq_groups;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  hipLaunchKernelGGL((maxsim_scan_f8_kernel<kF8Waves, kF8QW>), dim3((unsigned)(nq_groups * n_chunks)),
+                     dim3(kF8Waves * 64), 0, st, ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld,
+                     chunk_docs);
+  return launch_check("maxsim_scan_f8_kernel");
+}

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16", help="fp8: lab_scan_f8 variants 0/1")
     a = ap.parse_args()
     build()
     if a.build_only:
@@ -44,20 +45,33 @@ def main():
     L = ctypes.CDLL(LAB)
     L.lab_scan.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    L.lab_scan_f8.argtypes = L.lab_scan.argtypes
     dev = torch.device("cuda:0")
     Qf = synth.make_queries(a.batch, 32, seed=1)
     planted = synth.planted_ids(max(a.batch, 8), a.docs, 10, seed=2)[: a.batch]
     tokens, doclens = synth.make_shard(0, a.docs, Qf, planted, dev, seed=0)
     # ragged tail so every variant's masking path runs
     doclens[-1000:] = torch.randint(0, 129, (1000,), device=dev, dtype=torch.int32)
-    ix = ColbertIndex(tokens, doclens)
-    Q = Qf.to(dev, torch.bfloat16)
+    fp8 = a.dtype == "fp8"
+    if fp8:
+        from hybrid_rag_colbertv2_amd.index import quantize_mxfp8
+        ix = ColbertIndex.mxfp8(tokens, doclens)
+        Q = Qf.to(dev, torch.bfloat16)
+        qq, qs = quantize_mxfp8(Q)
+        qbuf = torch.cat([qq.reshape(-1), qs.reshape(-1)])
+        qptr = qbuf.data_ptr()
+        Qd = torch.from_numpy(orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy()))
+    else:
+        ix = ColbertIndex(tokens, doclens)
+        Q = Qf.to(dev, torch.bfloat16)
+        qptr = Q.data_ptr()
     st = torch.cuda.current_stream()
     variants = [int(v) for v in a.variants.split(",")]
     outs = {v: torch.empty((a.batch, a.docs), device=dev) for v in variants}
 
     def run(v):
-        rc = L.lab_scan(ix._h, v, Q.data_ptr(), a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
+        fn = L.lab_scan_f8 if fp8 else L.lab_scan
+        rc = fn(ix._h, v, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
         assert rc == 0, rc
 
     for v in variants:
@@ -75,7 +89,12 @@ def main():
     # oracle on a slice (first 64 and last 200 docs, 8 queries)
     sl = torch.cat([torch.arange(64), torch.arange(a.docs - 200, a.docs)]).to(dev)
     nq = min(8, a.batch)
-    ref = orc.maxsim(Q[:nq].float().cpu().numpy(), tokens[sl].float().cpu().numpy(), doclens[sl].cpu().numpy())
+    qref = Qd[:nq].numpy() if fp8 else Q[:nq].float().cpu().numpy()
+    if fp8:   # the oracle scores the dequantized values of the slice
+        dsl = orc.mxfp8_dequant(ix.tokens[sl].cpu().numpy(), ix.scales[sl].cpu().numpy())
+    else:
+        dsl = tokens[sl].float().cpu().numpy()
+    ref = orc.maxsim(qref, dsl, doclens[sl].cpu().numpy())
     flop = a.batch * a.docs * 2 * 32 * 128 * 128
     base = outs[variants[0]]
     for v in variants:
@@ -88,7 +107,7 @@ def main():
         gbs = a.docs * 32768 / med / 1e6
         print(f"B={a.batch} variant {v}: median {med:.3f} ms  min {min(times[v]):.3f}  {gbs:.0f} GB/s doc bytes  "
               f"{flop / med / 1e9:.1f} TFLOP/s "
-              f"({flop / med / 1e9 / 2500 * 100:.1f}% of bf16 peak)  oracle_err {err:.2e} inf_ok {inf_ok} "
+              f"({flop / med / 1e9 / (5000 if fp8 else 2500) * 100:.1f}% of {a.dtype} peak)  oracle_err {err:.2e} inf_ok {inf_ok} "
               f"max|d vs v{variants[0]}| {dv:.2e}", flush=True)
 
 
