@@ -223,7 +223,7 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             entries = json.load(f).get("entries", [])
-        want = "maxsim_scan_f8_kernel" if args.dtype == "fp8" else SCAN_KERNEL
+        want = "maxsim_scan_f8x4_kernel" if args.dtype == "fp8" else SCAN_KERNEL
         for d in entries:
             if d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == want:
                 traffic, clock = d.get("hbm_bytes_per_launch"), d.get("clock_ghz")
@@ -255,7 +255,7 @@ def main():
 
     fp8 = args.dtype == "fp8"
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
-    kern = "maxsim_scan_f8_kernel" if fp8 else SCAN_KERNEL
+    kern = "maxsim_scan_f8x4_kernel" if fp8 else SCAN_KERNEL
     if rank == 0:
         line = {
             "metric": "queries/sec + p50 retrieval latency, 1M-chunk corpus, top-10 rerank",

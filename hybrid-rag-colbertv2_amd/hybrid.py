@@ -258,9 +258,8 @@ class PipelinedRetriever:
     j+1's stage-2 scan is enqueued, and its BM25 runs on the host while the
     GPU scans, BEFORE the host fuses batch j:
 
-        GPU main stream:  scan(j) | scan(j+1)          | rerank(j) | scan(j+2) ...
-        GPU side stream:  D2H ids(j)
-        host:             bm25(j) | bm25(j+1), fuse(j) -> H2D cand(j) | ...
+        GPU stream:  scan(j) D2H(j) | scan(j+1) D2H(j+1) | rerank(j) | scan(j+2) ...
+        host:        bm25(j)        | bm25(j+1), fuse(j) -> H2D cand(j) | ...
 
     ``searcher`` is a ``ColbertIndex`` (one shard) or a
     ``distributed.ShardedSearcher``; with several ranks each one runs BM25
@@ -276,27 +275,37 @@ class PipelinedRetriever:
             searcher = ShardedSearcher(searcher, world=1)     # a bare index: one shard
         self.searcher, self.device = searcher, torch.device(device)
         self.k, self.fused, self.final_k, self.rrf_k = colbert_k, fused, final_k, rrf_k
-        self.side = torch.cuda.Stream(self.device)
-        self._ids_h = self._lex_h = None
+        self._ids_h = [None, None]   # pinned, one per in-flight batch
+        self._lex_h = [None, None]
         self._cand_h = [None, None]
 
-    def _host_buffers(self, B: int, kb: int):
-        if self._ids_h is None or self._ids_h.shape[0] < B or self._lex_h.shape[1] != kb:
-            B = max(B, self._ids_h.shape[0] if self._ids_h is not None else 0)
-            self._ids_h = torch.empty((B, self.k), dtype=torch.int32, pin_memory=True)
-            self._lex_h = torch.empty((B, kb), dtype=torch.int32, pin_memory=True)
-            self._cand_h = [torch.empty((B, self.fused), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    @staticmethod
+    def _pinned(buf, rows: int, cols: int):
+        if buf is None or buf.shape[0] < rows or buf.shape[1] != cols:
+            buf = torch.empty((rows, cols), dtype=torch.int32, pin_memory=True)
+        return buf
 
-    def _stage12(self, Q, lex):
-        """Enqueue stage 2; run (or take) stage 1 on the host meanwhile."""
+    def _stage12(self, Q, lex, slot: int):
+        """Enqueue stage 2 (+ the D2H of its ids, on the same stream, so the
+        copy runs right after the scan and not starved behind the next one);
+        run (or take) stage 1 on the host meanwhile."""
         if callable(lex):
             _, ids, bm = self.searcher.search_hybrid(Q, self.k, lex)
         else:
             _, ids = self.searcher.search(Q, self.k)
             bm = np.ascontiguousarray(lex, np.int32)
+        B = ids.shape[0]
+        self._ids_h[slot] = self._pinned(self._ids_h[slot], B, self.k)
+        ids_h = self._ids_h[slot][:B]
+        ids_h.copy_(ids, non_blocking=True)
+        if isinstance(bm, torch.Tensor):                           # merged across ranks on the device
+            self._lex_h[slot] = self._pinned(self._lex_h[slot], B, bm.shape[1])
+            lex_h = self._lex_h[slot][:B]
+            lex_h.copy_(bm, non_blocking=True)
+            bm = lex_h
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        return ids, bm, ev
+        return ids_h, bm, ev
 
     def run(self, batches):
         """batches: sequence of (Q [B, lq, D] device, lexical), where lexical is
@@ -307,24 +316,15 @@ class PipelinedRetriever:
         if not batches:
             return []
         out = []
-        cur = self._stage12(*batches[0])
+        cur = self._stage12(*batches[0], slot=0)
         for j, (Q, _) in enumerate(batches):
             B = Q.shape[0]
-            nxt = self._stage12(*batches[j + 1]) if j + 1 < len(batches) else None   # GPU busy during host work
-            ids, bm, ev = cur
-            self._host_buffers(B, bm.shape[1])
-            ids_h = self._ids_h[:B]
-            with torch.cuda.stream(self.side):
-                self.side.wait_event(ev)
-                ids.record_stream(self.side)
-                ids_h.copy_(ids, non_blocking=True)
-                if isinstance(bm, torch.Tensor):                   # merged across ranks on the device
-                    bm.record_stream(self.side)
-                    self._lex_h[:B].copy_(bm, non_blocking=True)
-                done = torch.cuda.Event()
-                done.record(self.side)
-            done.synchronize()
-            bm_h = self._lex_h[:B].numpy() if isinstance(bm, torch.Tensor) else bm
+            # the GPU scans batch j+1 while the host runs its BM25 and fuses batch j
+            nxt = self._stage12(*batches[j + 1], slot=(j + 1) & 1) if j + 1 < len(batches) else None
+            ids_h, bm, ev = cur
+            ev.synchronize()
+            bm_h = bm.numpy() if isinstance(bm, torch.Tensor) else bm
+            self._cand_h[j & 1] = self._pinned(self._cand_h[j & 1], B, self.fused)
             cand = self._cand_h[j & 1][:B]
             cand.numpy()[:] = rrf_fuse(bm_h, ids_h.numpy(), rrf_k=self.rrf_k, C=self.fused)
             cand_d = cand.to(self.device, non_blocking=True)

@@ -18,4 +18,6 @@ for dt in bf16 fp8; do
       python3 "$ROOT/tools/profile_scan.py" --dtype $dt > "$OUT/pmc_${dt}_$c.log" 2>&1
   done
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/bench_fp8" -o bench -- \
+  python3 "$ROOT/bench.py" --dtype fp8 --steps 5 --warmup 2 --p50-iters 10 --no-cpu-baseline > "$OUT/bench_fp8.json" 2> "$OUT/bench_fp8.err"
 echo profile-done
