@@ -49,6 +49,11 @@ _SIGS = {
     "cbv2_bm25_build_shard": (ctypes.c_int, [_p, _p, _i64, _i32, ctypes.c_float, ctypes.c_float, _i64, _i64,
                                              _i64, _p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_bm25_num_docs": (_i64, [_p]),
+    "cbv2_index_file_info": (ctypes.c_int, [ctypes.c_char_p, _p, _p, _p]),
+    "cbv2_index_file_write": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _p, _p, _p, _i64, _p]),
+    "cbv2_index_file_read": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _p, _p, _p, _p]),
+    "cbv2_index_file_write_host": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _p, _p, _p, _i64]),
+    "cbv2_index_file_read_host": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _p, _p, _p]),
     "cbv2_comm_init": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_comm_size": (ctypes.c_int, [_p]),
     "cbv2_comm_rank": (ctypes.c_int, [_p]),

@@ -16,6 +16,7 @@ owned here and borrowed by the C handle.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
 import torch
@@ -150,6 +151,37 @@ class ColbertIndex:
             ix.build_means(f32)
         return ix
 
+    # ----------------------------------------------------------------- native file
+    def save(self, path: str) -> None:
+        """Write this shard to the native index file (include/colbert_mi355x.h)."""
+        dt = _lib.DTYPE_MXFP8 if self.fp8 else _lib.DTYPE_BF16
+        torch.cuda.current_stream(self.device).synchronize()
+        _lib.check(_lib.lib().cbv2_index_file_write(
+            os.fsencode(path), dt, self.n, self.tokens.data_ptr(), self.scales.data_ptr() if self.fp8 else None,
+            self.doclens.data_ptr(), self.id_base, _stream_ptr(self.device)))
+
+    @classmethod
+    def load(cls, path: str, device="cuda", begin: int = 0, end: Optional[int] = None) -> "ColbertIndex":
+        """Load docs [begin, end) of a native index file straight into HBM
+        (a rank's shard); global ids start at the file's id_base + begin."""
+        device = torch.device(device)
+        dt, n, id_base = index_file_info(path)
+        end = n if end is None else int(end)
+        begin = int(begin)
+        m = end - begin
+        if begin < 0 or m < 0 or end > n:
+            raise ValueError(f"doc range [{begin}, {end}) outside [0, {n})")
+        fp8 = dt == _lib.DTYPE_MXFP8
+        tokens = torch.empty((m, LD, DIM), dtype=torch.uint8 if fp8 else torch.bfloat16, device=device)
+        scales = torch.empty((m, LD, 2), dtype=torch.uint8, device=device) if fp8 else None
+        doclens = torch.empty((m,), dtype=torch.int32, device=device)
+        with torch.cuda.device(device):
+            _lib.check(_lib.lib().cbv2_index_file_read(
+                os.fsencode(path), begin, end, tokens.data_ptr() if m else None,
+                scales.data_ptr() if (fp8 and m) else None, doclens.data_ptr() if m else None,
+                _stream_ptr(device)))
+        return cls(tokens, doclens, id_base=id_base + begin, scales=scales)
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.lib().cbv2_index_destroy(self._h)
@@ -258,6 +290,14 @@ class ColbertIndex:
 
 
 # --------------------------------------------------------------------- free functions
+def index_file_info(path: str):
+    """(ABI dtype, doc count, id_base) of a native index file."""
+    dt, n, base = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib().cbv2_index_file_info(os.fsencode(path), ctypes.byref(dt), ctypes.byref(n),
+                                               ctypes.byref(base)))
+    return int(dt.value), int(n.value), int(base.value)
+
+
 def select_topk(scores: torch.Tensor, k: int, ids: Optional[torch.Tensor] = None):
     """Top-k of each row of a short [B, C] matrix (C <= 1024); ties -> lower position."""
     _require_cuda(scores, "scores")

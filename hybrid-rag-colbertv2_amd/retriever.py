@@ -19,6 +19,7 @@ LRC = local_rag_complete.py
 """
 from __future__ import annotations
 
+import json
 import os
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -62,11 +63,40 @@ class JinaColBERTRetriever:
                    os.path.join(self.config.colbert_index_path, "index.pt"))
 
     def load(self) -> None:
-        """LRC:748-753 (reads the reference's own index.pt format; never unpickles code)."""
+        """LRC:748-753 (reads the reference's own index.pt format; never unpickles code).
+        Without an index.pt, the native file written by ``save_native`` is loaded."""
         index_file = os.path.join(self.config.colbert_index_path, "index.pt")
+        if not os.path.exists(index_file) and os.path.exists(self._native_path()):
+            return self.load_native()
         data = torch.load(index_file, map_location="cpu", weights_only=True)
         self.corpus_embeddings = self._build(data["embeddings"])
         self.corpus = data["corpus"]
+
+    # ------------------------------------------------------------ native index file (SURVEY §8 f2)
+    def _native_path(self, path: Optional[str] = None) -> str:
+        return path or os.path.join(self.config.colbert_index_path, "index.cbv2")
+
+    def save_native(self, path: Optional[str] = None) -> None:
+        """Write the HBM index to the native flat file (+ corpus.json beside it)."""
+        path = self._native_path(path)
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        self.corpus_embeddings.save(path)
+        if self.corpus is not None:
+            with open(os.path.splitext(path)[0] + ".corpus.json", "w") as f:
+                json.dump(self.corpus, f)
+
+    def load_native(self, path: Optional[str] = None, begin: int = 0, end: Optional[int] = None) -> None:
+        """Load docs [begin, end) of a native index file straight into HBM (a
+        rank's shard: pass shard_range(n, rank, world)); maxsim scorer only."""
+        if self.scorer != "maxsim":
+            raise ValueError("the native index stores tokens, not the fp32 means the literal scorer needs")
+        path = self._native_path(path)
+        self.corpus_embeddings = ColbertIndex.load(path, device=self.device, begin=begin, end=end)
+        cpath = os.path.splitext(path)[0] + ".corpus.json"
+        self.corpus = None
+        if os.path.exists(cpath):
+            with open(cpath) as f:
+                self.corpus = json.load(f)
 
     def index_embeddings(self, embeddings, corpus: Optional[List[str]] = None) -> None:
         """Install precomputed token embeddings (dense [N, L, D], pooled [N, D] or a list)."""

@@ -192,6 +192,30 @@ int cbv2_bm25_build_shard(const int32_t* doc_terms, const int64_t* doc_offsets, 
 int64_t cbv2_bm25_num_docs(const cbv2_bm25* index);
 int cbv2_bm25_destroy(cbv2_bm25* index);
 
+/* Native index file (replaces the torch.save/torch.load of
+ * indexes/colbert/index.pt at local_rag_complete.py:743-746, 751 for large
+ * corpora — the index.pt reader stays in Python).  One flat file: a 4 KiB
+ * header, int32 doclens [n], tokens [n][128][128] (bf16, or e4m3 bytes) and,
+ * for MXFP8, E8M0 scales [n][128][2]; each section 4 KiB-aligned.
+ * cbv2_index_file_write  — DEVICE pointers (an HBM-resident index), D2H in
+ *                          64 MiB pinned chunks overlapped with pwrite.
+ * cbv2_index_file_read   — docs [begin, end) into DEVICE buffers (tokens
+ *                          (end-begin)*128*128*elem bytes, scales, doclens):
+ *                          pread (O_DIRECT where aligned) into two pinned
+ *                          buffers overlapped with H2D copies on `stream`;
+ *                          returns when the data is in HBM.
+ * cbv2_index_file_info   — dtype, doc count and id_base of a file.
+ * *_host variants: HOST pointers, no GPU involved.                          */
+int cbv2_index_file_info(const char* path, int32_t* dtype, int64_t* n, int64_t* id_base);
+int cbv2_index_file_write(const char* path, int32_t dtype, int64_t n, const void* tokens, const void* scales,
+                          const int32_t* doclens, int64_t id_base, void* stream);
+int cbv2_index_file_read(const char* path, int64_t begin, int64_t end, void* tokens, void* scales, int32_t* doclens,
+                         void* stream);
+int cbv2_index_file_write_host(const char* path, int32_t dtype, int64_t n, const void* tokens, const void* scales,
+                               const int32_t* doclens, int64_t id_base);
+int cbv2_index_file_read_host(const char* path, int64_t begin, int64_t end, void* tokens, void* scales,
+                              int32_t* doclens);
+
 /* Multi-GPU exchange (SURVEY.md §8(b) "cbv2_comm_init(ncclComm_t) +
  * cbv2_search_sharded", §8(e)).  No reference counterpart: the reference is
  * single-process.  One process per GPU, each holding the shard

@@ -270,3 +270,45 @@ def test_native_exchange_rccl_world1(dev, tmp_path):
         torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
+
+
+def test_native_index_file_roundtrip(dev, tmp_path):
+    """HBM -> native file -> HBM, whole and by rank shards (multi-chunk staging:
+    3000 docs = 98 MB > one 64 MiB pinned buffer), bf16 and MXFP8, and the
+    retriever's save_native / load_native."""
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.distributed import shard_range
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex, index_file_info
+    from hybrid_rag_colbertv2_amd.retriever import JinaColBERTRetriever
+    N = 3000
+    Qf = synth.make_queries(4, seed=9)
+    planted = synth.planted_ids(4, N, 10)
+    tokens, doclens = synth.make_shard(0, N, Qf, planted, dev)
+    doclens[::7] = torch.randint(0, 129, (len(doclens[::7]),), device=dev, dtype=torch.int32)
+    Q = Qf.to(dev, torch.bfloat16)
+    for fp8 in (False, True):
+        ix = ColbertIndex.mxfp8(tokens, doclens, id_base=50) if fp8 else ColbertIndex(tokens, doclens, id_base=50)
+        path = str(tmp_path / f"ix{int(fp8)}.cbv2")
+        ix.save(path)
+        assert index_file_info(path)[1:] == (N, 50)
+        full = ColbertIndex.load(path, device=dev)
+        assert full.fp8 == fp8 and full.id_base == 50
+        assert torch.equal(full.tokens, ix.tokens) and torch.equal(full.doclens, ix.doclens)
+        if fp8:
+            assert torch.equal(full.scales, ix.scales)
+        s0, i0 = ix.search(Q, 20)
+        s1, i1 = full.search(Q, 20)
+        assert torch.equal(s0, s1) and torch.equal(i0, i1)
+        for r in range(3):
+            a, b = shard_range(N, r, 3)
+            sh = ColbertIndex.load(path, device=dev, begin=a, end=b)
+            assert sh.id_base == 50 + a and torch.equal(sh.tokens, ix.tokens[a:b])
+            assert torch.equal(sh.doclens, ix.doclens[a:b])
+    cfg = RAGConfig()
+    cfg.colbert_index_path = str(tmp_path / "colbert")
+    r = JinaColBERTRetriever(cfg, encoder=FakeEncoder())
+    r.index_embeddings([torch.randn(int(k), 128) for k in torch.randint(1, 129, (40,))], corpus=[f"d{i}" for i in range(40)])
+    r.save_native()
+    r2 = JinaColBERTRetriever(cfg, encoder=FakeEncoder())
+    r2.load()                                   # no index.pt: the native file is loaded
+    assert r2.corpus == r.corpus and torch.equal(r2.corpus_embeddings.tokens, r.corpus_embeddings.tokens)

@@ -1,0 +1,83 @@
+"""CPU: the native index file (csrc/index_file.cpp) through its
+host-pointer entry points: layout, round trips of whole files and doc ranges,
+and validation.  The device entry points (HBM in/out) are covered by
+tests/test_gpu_api.py::test_native_index_file_roundtrip."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+
+def _lib():
+    from hybrid_rag_colbertv2_amd import _lib
+    return _lib
+
+
+def _write(path, dtype, tokens, scales, doclens, id_base=0):
+    L = _lib()
+    L.check(L.lib().cbv2_index_file_write_host(os.fsencode(path), dtype, len(doclens), tokens.ctypes.data,
+                                               scales.ctypes.data if scales is not None else None,
+                                               doclens.ctypes.data, id_base))
+
+
+def _read(path, begin, end, elem, fp8):
+    L = _lib()
+    m = end - begin
+    tok = np.zeros((m, 128, 128), elem)
+    sc = np.zeros((m, 128, 2), np.uint8) if fp8 else None
+    dl = np.zeros(m, np.int32)
+    L.check(L.lib().cbv2_index_file_read_host(os.fsencode(path), begin, end, tok.ctypes.data if m else None,
+                                              sc.ctypes.data if (fp8 and m) else None, dl.ctypes.data if m else None))
+    return tok, sc, dl
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_roundtrip_and_ranges(tmp_path, fp8):
+    L = _lib()
+    rng = np.random.default_rng(3)
+    n = 37
+    elem = np.uint8 if fp8 else np.uint16
+    tokens = rng.integers(0, 255 if fp8 else 65535, size=(n, 128, 128)).astype(elem)
+    scales = rng.integers(0, 255, size=(n, 128, 2)).astype(np.uint8) if fp8 else None
+    doclens = rng.integers(0, 129, size=n).astype(np.int32)
+    path = str(tmp_path / "ix.cbv2")
+    dt = L.DTYPE_MXFP8 if fp8 else L.DTYPE_BF16
+    _write(path, dt, tokens, scales, doclens, id_base=1000)
+    from hybrid_rag_colbertv2_amd.index import index_file_info
+    assert index_file_info(path) == (dt, n, 1000)
+    # header layout as documented in include/colbert_mi355x.h
+    with open(path, "rb") as f:
+        head = f.read(4096)
+    assert head[:8] == b"CBV2IDX1"
+    version, dtype, nn = struct.unpack_from("<IiQ", head, 8)
+    doclens_off, tokens_off, scales_off, file_bytes = struct.unpack_from("<QQQQ", head, 40)
+    assert (version, dtype, nn) == (1, dt, n) and doclens_off == 4096 and tokens_off % 4096 == 0
+    assert os.path.getsize(path) == file_bytes
+    assert (scales_off % 4096 == 0 and scales_off > 0) if fp8 else scales_off == 0
+    for a, b in [(0, n), (0, 1), (5, 17), (36, 37), (12, 12)]:
+        tok, sc, dl = _read(path, a, b, elem, fp8)
+        assert np.array_equal(tok, tokens[a:b]) and np.array_equal(dl, doclens[a:b])
+        if fp8:
+            assert np.array_equal(sc, scales[a:b])
+
+
+def test_validation(tmp_path):
+    L = _lib()
+    path = str(tmp_path / "ix.cbv2")
+    tokens = np.zeros((4, 128, 128), np.uint16)
+    doclens = np.full(4, 128, np.int32)
+    _write(path, L.DTYPE_BF16, tokens, None, doclens)
+    with pytest.raises(ValueError):
+        _read(path, 2, 5, np.uint16, False)                 # past the end
+    with pytest.raises(ValueError):
+        _write(str(tmp_path / "bad.cbv2"), 2, tokens, None, doclens)   # f32 is not a storable dtype
+    bad = tmp_path / "junk.cbv2"
+    bad.write_bytes(b"x" * 8192)
+    from hybrid_rag_colbertv2_amd.index import index_file_info
+    with pytest.raises(ValueError):
+        index_file_info(str(bad))
+    with open(path, "r+b") as f:                            # truncate the token section
+        f.truncate(4096 + 4096 + 100)
+    with pytest.raises(ValueError):
+        index_file_info(path)
