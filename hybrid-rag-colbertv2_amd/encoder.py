@@ -11,9 +11,10 @@ that ``encode`` method:
   per process).  It stands in for the Jina-ColBERT encoder in tests, golden
   fixtures and the config-1 toy corpus.  Same words → same token vectors, so
   late interaction behaves lexically and results are reproducible bit for bit.
-* ``load_local_encoder(path)`` — a SentenceTransformer-style model from a local
-  directory, if ``sentence_transformers`` is importable (it is not in this
-  image; the function raises a clear error rather than reaching a hub).
+* ``load_local_encoder(path)`` — the Jina-ColBERT-v2 architecture
+  (jina_encoder.py, PyTorch-ROCm) from a local ``model.safetensors``, or a
+  SentenceTransformer directory if that library is importable (it is not in
+  this image); never reaches a hub.
 """
 from __future__ import annotations
 
@@ -74,11 +75,20 @@ class FakeEncoder:
 
 
 def load_local_encoder(path: str, device: str = "cuda"):
-    """Jina-ColBERT (or any SentenceTransformer) from a LOCAL directory on PyTorch-ROCm."""
+    """The Jina-ColBERT encoder from a LOCAL directory on PyTorch-ROCm.
+
+    A directory with ``model.safetensors`` loads into this package's own
+    implementation of the architecture (jina_encoder.JinaColBERTEncoder);
+    otherwise a SentenceTransformer directory is tried if that library is
+    importable (it is not in this image).  Never reaches a hub."""
+    import os
+    if os.path.exists(os.path.join(path, "model.safetensors")):
+        from .jina_encoder import JinaColBERTEncoder
+        return JinaColBERTEncoder.from_local(path, device=device)
     try:
         from sentence_transformers import SentenceTransformer  # noqa: WPS433
     except ImportError as e:  # pragma: no cover - not installed in this image
         raise RuntimeError(
-            "sentence_transformers is not installed; pass an encoder object with an "
-            "encode(texts, convert_to_tensor=True) method (e.g. FakeEncoder) instead") from e
+            f"no local checkpoint at {path!r} and sentence_transformers is not installed; pass an encoder "
+            "object with an encode(texts, convert_to_tensor=True) method (e.g. FakeEncoder) instead") from e
     return SentenceTransformer(path, trust_remote_code=True, device=device, local_files_only=True)

@@ -55,7 +55,7 @@ class JinaColBERTRetriever:
         """LRC:728-746: encode the corpus, keep it in HBM, save index.pt."""
         self.corpus = corpus
         print(f"  Encoding {len(corpus)} documents...")
-        embeddings = self.model.encode(corpus, show_progress_bar=True, convert_to_tensor=True)
+        embeddings = self.model.encode(corpus, show_progress_bar=True, convert_to_tensor=True, is_query=False)
         self.corpus_embeddings = self._build(embeddings)
         os.makedirs(self.config.colbert_index_path, exist_ok=True)
         saved = embeddings.cpu() if isinstance(embeddings, torch.Tensor) else [e.cpu() for e in embeddings]
@@ -105,7 +105,7 @@ class JinaColBERTRetriever:
 
     # ------------------------------------------------------------ encoding
     def _encode_query(self, query: Union[str, torch.Tensor]) -> torch.Tensor:
-        q = query if isinstance(query, torch.Tensor) else self.model.encode(query, convert_to_tensor=True)
+        q = query if isinstance(query, torch.Tensor) else self.model.encode(query, convert_to_tensor=True, is_query=True)
         if q.dim() == 1:
             q = q.unsqueeze(0)
         return q
@@ -135,7 +135,7 @@ class JinaColBERTRetriever:
         if not documents:
             return []
         q = self._encode_query(query)
-        d = self.model.encode(documents, convert_to_tensor=True)
+        d = self.model.encode(documents, convert_to_tensor=True, is_query=False)
         tmp = self._build(d)
         kk = min(k, len(documents))
         if self.scorer == "maxsim":
