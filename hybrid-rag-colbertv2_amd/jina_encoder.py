@@ -146,7 +146,7 @@ _LAYER_KEYS = {
 
 
 class HashTokenizer:
-    """Stand-in tokenizer (no tokenizer.json offline): lower-case ``\w+`` words
+    r"""Stand-in tokenizer (no tokenizer.json offline): lower-case ``\w+`` words
     mapped to ids by crc32 into [3, vocab - 4).  Same ``encode(text).ids`` API
     as ``tokenizers.Tokenizer``; for tests and demos only."""
 
