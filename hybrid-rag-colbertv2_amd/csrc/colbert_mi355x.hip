@@ -527,17 +527,56 @@ __device__ __forceinline__ void iter4_ragged(const uint8_t* buf, int lane, int j
   }
 }
 
-template <int WAVES, int QW, int D = 2, int NBUF = 3>
+// Dynamic-tail task grab (one thread): writes (doc offset into the tail, size;
+// size 0 = done) to slot[0..1].  task_docs > 0: fixed tasks, the counter counts
+// tasks; task_docs < 0: guided, the counter counts docs and a task takes
+// max(-task_docs, remaining / (2 * workgroups per query group)) docs (CAS: every
+// failed CAS means another workgroup advanced, so the loop ends).
+__device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int P, int* slot) {
+  int o, sz;
+  if (task_docs > 0) {
+    o = atomicAdd(ctr, 1) * task_docs;
+    sz = o < dyn ? task_docs : 0;
+  } else {
+    o = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const int rem = dyn - o;
+      if (rem <= 0) { sz = 0; break; }
+      sz = ((rem / (2 * P)) + 15) & ~15;
+      sz = sz > -task_docs ? sz : -task_docs;
+      sz = sz < rem ? sz : rem;
+      const int prev = atomicCAS(ctr, o, o + sz);
+      if (prev == o) break;
+      o = prev;
+    }
+  }
+  slot[0] = o;
+  slot[1] = sz;
+}
+
+// Work split (per query group of QPB queries): docs [0, static_docs) in equal
+// chunks, one per workgroup, XCD-aware as above; then, if task_ctr is given,
+// docs [static_docs, n) as tasks of task_docs grabbed with one atomicAdd on
+// the query group's counter until exhausted.  The XCDs hold different clocks
+// under this load (1.98-2.11 GHz measured on one device, lab --stamps), so a
+// static split ends when the slowest XCD does; the dynamic tail lets the fast
+// ones take the remainder.  Every doc range runs the same pipelined loop.
+// STAMPS (lab only): per-workgroup s_memrealtime / s_memtime at start and end.
+template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false>
 __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
-    int64_t chunk_docs) {
+    int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr, int task_docs,
+    uint64_t* __restrict__ stamps) {
   constexpr int QPB = WAVES * QW;
   constexpr int kPieces = kDocBytes / 1024;  // 32 x 1 KiB per iteration
   constexpr int kPiecesPerWave = kPieces / WAVES;
   static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
   static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kDocBytes];
+  // one LDS object only: with a second __shared__ array hipcc starts putting
+  // vmcnt(0) before the ring's ds_reads (LDS-DMA alias tracking)
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kDocBytes + 16];
+  int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kDocBytes);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -548,11 +587,11 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
   const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
   const int qg = lin % nq_groups;
   const int64_t chunk = lin / nq_groups;
-  const int64_t d_begin = chunk * chunk_docs;
-  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
-  if (d_begin >= d_end) return;
-  const int nd = (int)(d_end - d_begin);
-  const int ngr = (nd + 3) >> 2;
+  uint64_t t_start = 0, r_start = 0;
+  if constexpr (STAMPS) {
+    t_start = __builtin_amdgcn_s_memtime();
+    r_start = __builtin_amdgcn_s_memrealtime();
+  }
 
   bf16x8 qf[QW][2][4];
 #pragma unroll
@@ -567,78 +606,108 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
     src_off[jj] = (R & 31) * kRowBytes + 16 * ((lane & 15) ^ swz4(R));
     src_doc[jj] = R >> 5;
   }
-  auto issue = [&](int it, int buf) {
-    const int G = it >> 2, j = it & 3;
-#pragma unroll
-    for (int jj = 0; jj < kPiecesPerWave; ++jj) {
-      const int piece = wave * kPiecesPerWave + jj;
-      int d = 4 * G + src_doc[jj];
-      d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-      const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * 32 * kRowBytes + src_off[jj];
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16, 0,
-                                       0);
-    }
-  };
 
-  float sc[QW];
-  float m[QW][2];
+  // the first range: this workgroup's static chunk (may be empty)
+  int64_t d_begin = chunk * chunk_docs;
+  int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
+  for (int k = 0;; ++k) {
+    if (d_begin < d_end) {
+      const int nd = (int)(d_end - d_begin);
+      const int ngr = (nd + 3) >> 2;
+      auto issue = [&](int it, int buf) {
+        const int G = it >> 2, j = it & 3;
 #pragma unroll
-  for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
-  int dl_g = 0, dl_min = 0, dl_max = 0;
-
-  const int nit = 4 * ngr;
-  issue(0, 0);
-  if (NBUF == 3 && nit > 1) issue(1, 1);
-  int cur = 0;           // ring slot of iteration it
-  bool stored = false;   // global stores issued last iteration (they count in vmcnt)
-  for (int it = 0; it < nit; ++it) {
-    if (NBUF == 3 && it + 1 < nit && !stored)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    stored = false;
-    if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
-    if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
-    const uint8_t* buf = smem + cur * kDocBytes;
-    cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
-
-    const int G = it >> 2, j = it & 3;
-    if (j == 0) {
-      int dl4[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int v = (4 * G + x < nd) ? doclens[d_begin + 4 * G + x] : 0;
-        dl4[x] = v < 0 ? 0 : (v > kLd ? kLd : v);
-      }
-      dl_min = min(min(dl4[0], dl4[1]), min(dl4[2], dl4[3]));
-      dl_max = max(max(dl4[0], dl4[1]), max(dl4[2], dl4[3]));
-      dl_g = g == 0 ? dl4[0] : (g == 1 ? dl4[1] : (g == 2 ? dl4[2] : dl4[3]));
-#pragma unroll
-      for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
-    }
-    if (32 * j + 32 <= dl_min)
-      iter4_full<QW, D>(buf, lane, qf, m);
-    else if (32 * j < dl_max)
-      iter4_ragged<QW>(buf, lane, j, dl_g, dl_max, qf, m);
-    if (j == 3) {
-      // doc 4G+g's score in every lane of group g; lane c of the 64-doc block
-      // register keeps doc group c, so lane (c, g) holds doc 4c+g of the block
-#pragma unroll
-      for (int q = 0; q < QW; ++q) {
-        const float v = dpp_row_sum16((c < lq ? m[q][0] : 0.0f) + (16 + c < lq ? m[q][1] : 0.0f));
-        sc[q] = (c == (G & 15)) ? v : sc[q];
-      }
-      if ((G & 15) == 15 || G == ngr - 1) {
-        const int dd = 64 * (G >> 4) + 4 * c + g;
-#pragma unroll
-        for (int q = 0; q < QW; ++q) {
-          const int qi = qg * QPB + wave * QW + q;
-          if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+        for (int jj = 0; jj < kPiecesPerWave; ++jj) {
+          const int piece = wave * kPiecesPerWave + jj;
+          int d = 4 * G + src_doc[jj];
+          d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
+          const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * 32 * kRowBytes + src_off[jj];
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16,
+                                           0, 0);
         }
-        stored = true;
+      };
+
+      float sc[QW];
+      float m[QW][2];
+#pragma unroll
+      for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
+      int dl_g = 0, dl_min = 0, dl_max = 0;
+
+      const int nit = 4 * ngr;
+      issue(0, 0);
+      if (NBUF == 3 && nit > 1) issue(1, 1);
+      int cur = 0;           // ring slot of iteration it
+      bool stored = false;   // global stores issued last iteration (they count in vmcnt)
+      for (int it = 0; it < nit; ++it) {
+        if (NBUF == 3 && it + 1 < nit && !stored)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stored = false;
+        if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
+        if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+        const uint8_t* buf = smem + cur * kDocBytes;
+        cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+
+        const int G = it >> 2, j = it & 3;
+        if (j == 0) {
+          int dl4[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const int v = (4 * G + x < nd) ? doclens[d_begin + 4 * G + x] : 0;
+            dl4[x] = v < 0 ? 0 : (v > kLd ? kLd : v);
+          }
+          dl_min = min(min(dl4[0], dl4[1]), min(dl4[2], dl4[3]));
+          dl_max = max(max(dl4[0], dl4[1]), max(dl4[2], dl4[3]));
+          dl_g = g == 0 ? dl4[0] : (g == 1 ? dl4[1] : (g == 2 ? dl4[2] : dl4[3]));
+#pragma unroll
+          for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+        }
+        if (32 * j + 32 <= dl_min)
+          iter4_full<QW, D>(buf, lane, qf, m);
+        else if (32 * j < dl_max)
+          iter4_ragged<QW>(buf, lane, j, dl_g, dl_max, qf, m);
+        if (j == 3) {
+          // doc 4G+g's score in every lane of group g; lane c of the 64-doc block
+          // register keeps doc group c, so lane (c, g) holds doc 4c+g of the block
+#pragma unroll
+          for (int q = 0; q < QW; ++q) {
+            const float v = dpp_row_sum16((c < lq ? m[q][0] : 0.0f) + (16 + c < lq ? m[q][1] : 0.0f));
+            sc[q] = (c == (G & 15)) ? v : sc[q];
+          }
+          if ((G & 15) == 15 || G == ngr - 1) {
+            const int dd = 64 * (G >> 4) + 4 * c + g;
+#pragma unroll
+            for (int q = 0; q < QW; ++q) {
+              const int qi = qg * QPB + wave * QW + q;
+              if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+            }
+            stored = true;
+          }
+        }
       }
+    }
+    if (task_ctr == nullptr) break;
+    // next dynamic task; the barrier also retires every wave's reads of the
+    // ring before the next range refills it (two slots: a slow wave may still
+    // read slot k&1 while thread 0 fills slot (k+1)&1).
+    if (threadIdx.x == 0) next_task(task_ctr + qg, task_docs, (int)(n - static_docs), nwg / nq_groups, task_slot + 2 * (k & 1));
+    __syncthreads();
+    const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1)]);
+    const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1) + 1]);
+    d_begin = static_docs + (int64_t)o;
+    if (sz <= 0 || d_begin >= n) break;
+    d_end = d_begin + sz < n ? d_begin + sz : n;
+  }
+  if constexpr (STAMPS) {
+    if (threadIdx.x == 0) {
+      uint64_t* st = stamps + 4 * (size_t)bid;
+      st[0] = r_start;
+      st[1] = __builtin_amdgcn_s_memrealtime();
+      st[2] = t_start;
+      st[3] = __builtin_amdgcn_s_memtime();
     }
   }
 }
@@ -1011,12 +1080,14 @@ template <int WAVES, int QW, int D = 1, int NBUF = 3>   // D = 2 spills at QW = 
 __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
-    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs) {
+    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr,
+    int task_docs) {
   constexpr int QPB = WAVES * QW;
   constexpr int kPieces = kF8IterBytes / 1024;  // 16 x 1 KiB per iteration
   constexpr int kPiecesPerWave = kPieces / WAVES;
   static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kF8IterStage + 256];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kF8IterStage + 256 + 16];
+  int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kF8IterStage + 256);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1027,11 +1098,6 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
   const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
   const int qg = lin % nq_groups;
   const int64_t chunk = lin / nq_groups;
-  const int64_t d_begin = chunk * chunk_docs;
-  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
-  if (d_begin >= d_end) return;
-  const int nd = (int)(d_end - d_begin);
-  const int ngr = (nd + 3) >> 2;
 
   i32x8 qa[QW][2];
   int qs[QW][2];
@@ -1047,6 +1113,13 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
     src_off[jj] = (R & 31) * kDim + 16 * ((lane & 7) ^ swz8x4(R));
     src_doc[jj] = R >> 5;
   }
+  // the same static chunks + guided dynamic tail as maxsim_scan16x4_kernel
+  int64_t d_begin = chunk * chunk_docs;
+  int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
+  for (int kt = 0;; ++kt) {
+  if (d_begin < d_end) {
+  const int nd = (int)(d_end - d_begin);
+  const int ngr = (nd + 3) >> 2;
   auto clamp_doc = [&](int d) { return d < nd ? d : nd - 1; };  // the last group's missing docs: rows masked
   auto issue = [&](int it, int buf) {
     const int G = it >> 2, j = it & 3;
@@ -1129,6 +1202,16 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
         stored = true;
       }
     }
+  }
+  }
+    if (task_ctr == nullptr) break;
+    if (threadIdx.x == 0) next_task(task_ctr + qg, task_docs, (int)(n - static_docs), nwg / nq_groups, task_slot + 2 * (kt & 1));
+    __syncthreads();
+    const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (kt & 1)]);
+    const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (kt & 1) + 1]);
+    d_begin = static_docs + (int64_t)o;
+    if (sz <= 0 || d_begin >= n) break;
+    d_end = d_begin + sz < n ? d_begin + sz : n;
   }
 }
 
@@ -1718,6 +1801,11 @@ struct cbv2_index {
   const float* doc_means;
   int32_t dtype;           // CBV2_DTYPE_BF16 or CBV2_DTYPE_MXFP8
   const uint8_t* scales;   // MXFP8: E8M0 [n][128][2]
+  // Dynamic-tail task counters of the B > 16 scans: a ring of slots, one per
+  // launch (zeroed on the launch's stream), owned by the handle; nullptr =
+  // static split only.
+  int* task_ring = nullptr;
+  uint32_t task_seq = 0;
 };
 
 namespace {
@@ -1754,6 +1842,19 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+constexpr int kRingSlots = 128;   // launches in flight before a slot is reused
+constexpr int kRingInts = 64;     // query groups per launch with a dynamic tail (B <= 64 * 32)
+
+// The handle's task-counter ring (index creation; failure leaves the static split).
+void alloc_task_ring(cbv2_index* ix) {
+  if (ix->n == 0) return;
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(ix->device) != hipSuccess) return;
+  void* p = nullptr;
+  if (hipMalloc(&p, (size_t)kRingSlots * kRingInts * sizeof(int)) == hipSuccess) ix->task_ring = (int*)p;
+  (void)hipSetDevice(prev);
+}
 
 int cu_count(int dev) {
   static int cache[64] = {0};
@@ -1810,6 +1911,60 @@ int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, flo
   return launch_check(name);
 }
 
+// The B > 16 doc-interleaved scan: one workgroup per CU; docs [0, static_docs)
+// split statically, the last ~dyn_frac of the corpus as dynamic tasks of
+// task_docs (see maxsim_scan16x4_kernel).  Defaults from tools/scan_lab.py on
+// MI355X (B=256): static 146.7 -> guided 10 % tail 142.7 ms at 1M docs,
+// 18.26 -> 17.73 ms at 125k (fixed 64-doc tasks: 143.1 / 17.92).
+constexpr float kScanDynFrac = 0.10f;
+constexpr int kScanTaskDocs = -16;     // guided: tasks shrink to 16 docs at the end
+
+// Work split of one launch: n_chunks static chunks of chunk_docs per query
+// group over [0, static_docs), the rest as dynamic tasks on a fresh counter slot.
+struct ScanSplit {
+  int64_t n_chunks = 1, chunk_docs = 0, static_docs = 0;
+  int* ctr = nullptr;
+  int task_docs = 0;
+};
+
+int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, int task_docs, hipStream_t st,
+               ScanSplit* sp) {
+  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  if (n_chunks < 1) n_chunks = 1;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  sp->task_docs = task_docs > 0 ? std::max(64, task_docs & ~63) : -std::max(16, (-task_docs) & ~15);
+  sp->ctr = nullptr;
+  if (ix->task_ring != nullptr && dyn_frac > 0.0f && nq_groups <= kRingInts &&
+      ix->n >= std::max<int64_t>(512, 4 * (int64_t)std::abs(sp->task_docs)) * n_chunks) {
+    sp->chunk_docs = ((int64_t)((double)ix->n * (1.0 - (double)dyn_frac)) / n_chunks) & ~(int64_t)63;
+    sp->static_docs = sp->chunk_docs * n_chunks;
+    const uint32_t slot = __atomic_fetch_add(&ix->task_seq, 1u, __ATOMIC_RELAXED) % kRingSlots;
+    sp->ctr = ix->task_ring + (size_t)slot * kRingInts;
+    CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sizeof(int), st));
+  } else {
+    sp->chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+    n_chunks = (ix->n + sp->chunk_docs - 1) / sp->chunk_docs;
+    sp->static_docs = ix->n;
+  }
+  sp->n_chunks = n_chunks;
+  if ((int64_t)nq_groups * n_chunks > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  return CBV2_OK;
+}
+
+template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS>
+int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
+                    float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr) {
+  constexpr int QPB = WAVES * QW;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  ScanSplit sp;
+  const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
+  if (rc != CBV2_OK) return rc;
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+                     dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, sp.chunk_docs,
+                     sp.static_docs, sp.ctr, sp.task_docs, stamps);
+  return launch_check("maxsim_scan16x4_kernel");
+}
+
 template <int QW>
 int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
   const int nq_groups = (B + QW - 1) / QW;
@@ -1857,11 +2012,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16W4Q2:
       return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
     case kScan16x4W8:
-      return launch_scan<8, 4, 1>(maxsim_scan16x4_kernel<8, 4>, ix, Q, B, lq, out, ld_out, st,
-                                  "maxsim_scan16x4_kernel");
+      return launch_scan16x4<8, 4, 1, 2, 3, false>(ix, Q, B, lq, out, ld_out, st);
     case kScan16x4W4:
-      return launch_scan<4, 4, 2>(maxsim_scan16x4_kernel<4, 4, 2, 2>, ix, Q, B, lq, out, ld_out, st,
-                                  "maxsim_scan16x4_kernel");
+      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st);
     default:
       return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
   }
@@ -1870,7 +2023,8 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
 constexpr int kF8DirectMaxB = 8;
 constexpr int kF8Waves = 8, kF8QW = 8;
 
-int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
+            float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs) {
   if (ix->n == 0) return CBV2_OK;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   if (B <= kF8DirectMaxB) {
@@ -1889,16 +2043,12 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   }
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;
-  const int64_t target = cu_count(ix->device);
-  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
-  if (n_chunks < 1) n_chunks = 1;
-  if (n_chunks > ix->n) n_chunks = ix->n;
-  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
-  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
-  const int64_t grid = (int64_t)nq_groups * n_chunks;
-  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW>), dim3((unsigned)grid), dim3(kF8Waves * 64), 0, st,
-                     ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
+  ScanSplit sp;
+  const int rc = plan_split(ix, nq_groups, cu_count(ix->device), dyn_frac, task_docs, st, &sp);
+  if (rc != CBV2_OK) return rc;
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+                     dim3(kF8Waves * 64), 0, st, ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out,
+                     ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs);
   return launch_check("maxsim_scan_f8x4_kernel");
 }
 
@@ -2009,6 +2159,7 @@ int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, 
   CBV2_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
   cbv2_index* ix = new cbv2_index{device, (const uint8_t*)tokens, n, ld, d, doclens, id_base, nullptr,
                                   CBV2_DTYPE_BF16, nullptr};
+  alloc_task_ring(ix);
   *out = ix;
   return CBV2_OK;
 }
@@ -2031,6 +2182,7 @@ int cbv2_index_create_mxfp8(int device, const void* tokens, const void* scales, 
   CBV2_REQUIRE(device >= 0 && device < ndev, "device %d out of range (%d devices)", device, ndev);
   *out = new cbv2_index{device, (const uint8_t*)tokens, n, ld, d, doclens, id_base, nullptr, CBV2_DTYPE_MXFP8,
                         (const uint8_t*)scales};
+  alloc_task_ring(*out);
   return CBV2_OK;
 }
 
@@ -2053,6 +2205,13 @@ int cbv2_quantize_mxfp8(const void* x, int32_t dtype, int64_t rows, void* q, voi
 }
 
 int cbv2_index_destroy(cbv2_index* index) {
+  if (index != nullptr && index->task_ring != nullptr) {
+    int prev = 0;
+    if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(index->device) == hipSuccess) {
+      (void)hipFree(index->task_ring);
+      (void)hipSetDevice(prev);
+    }
+  }
   delete index;
   return CBV2_OK;
 }

@@ -293,3 +293,51 @@ def test_sampled_topk_equals_exact(dev, dist, n, k):
     if n <= 300000:
         rs, ri = orc.topk(x.cpu().numpy(), k)
         assert np.array_equal(i1.cpu().numpy(), ri)
+
+
+def test_dynamic_tail_split_bit_identical(dev):
+    """B > 16 over a corpus large enough for the dynamic tail (static chunks +
+    atomically grabbed tasks): every doc's score equals the static-split score
+    of a small index over the same docs, bit for bit, and the oracle's."""
+    N, B = 24000, 200                       # 7 query groups -> 37 chunks; tail active from 18,944 docs
+    g = torch.Generator(device=dev).manual_seed(5)
+    docs = torch.randn(N, 128, 128, device=dev, generator=g)
+    docs = (docs / docs.norm(dim=-1, keepdim=True)).bfloat16()
+    doclens = torch.randint(1, 129, (N,), device=dev, generator=g, dtype=torch.int32)
+    doclens[::3] = 128
+    Q = torch.randn(B, 32, 128, device=dev, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16()
+    full = ColbertIndex(docs, doclens).score(Q)
+    for rep in range(2):                    # counters are reset per launch
+        assert torch.equal(ColbertIndex(docs, doclens).score(Q), full), rep
+    for a, b in [(0, 700), (N // 2, N // 2 + 900), (N - 2500, N)]:
+        part = ColbertIndex(docs[a:b].contiguous(), doclens[a:b].contiguous()).score(Q)
+        assert torch.equal(part, full[:, a:b]), (a, b)
+    sel = torch.cat([torch.arange(0, N, 211), torch.arange(N - 40, N)]).to(dev)
+    ref = orc.maxsim(Q[:6].float().cpu().numpy(), docs[sel].float().cpu().numpy(), doclens[sel].cpu().numpy())
+    np.testing.assert_allclose(full[:6, sel].cpu().numpy(), ref, atol=ATOL, rtol=0)
+
+
+def test_dynamic_tail_writes_every_score(dev):
+    """Through the C ABI into a NaN-filled buffer: the static chunks and the
+    dynamic tasks together cover every (query, doc) exactly as the small-index
+    static split scores it."""
+    import ctypes  # noqa: F401
+    from hybrid_rag_colbertv2_amd import _lib
+    from hybrid_rag_colbertv2_amd.index import _stream_ptr
+    N, B = 70000, 64                        # 2 query groups -> 128 chunks; tail active from 512 * 128 docs
+    g = torch.Generator(device=dev).manual_seed(9)
+    docs = torch.randn(N, 128, 128, device=dev, generator=g)
+    docs = (docs / docs.norm(dim=-1, keepdim=True)).bfloat16()
+    doclens = torch.randint(0, 129, (N,), device=dev, generator=g, dtype=torch.int32)
+    Q = torch.randn(B, 32, 128, device=dev, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16().contiguous()
+    ix = ColbertIndex(docs, doclens)
+    out = torch.full((B, N), float("nan"), device=dev)
+    _lib.check(_lib.lib().cbv2_score(ix._h, _lib.SCORERS["maxsim"], Q.data_ptr(), _lib.DTYPE_BF16, B, 32,
+                                     out.data_ptr(), N, _stream_ptr(dev)))
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any()
+    for a, b in [(0, 300), (N - 7000, N - 3000), (N - 3000, N)]:
+        part = ColbertIndex(docs[a:b].contiguous(), doclens[a:b].contiguous()).score(Q)
+        assert torch.equal(part, out[:, a:b]), (a, b)

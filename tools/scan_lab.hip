@@ -300,6 +300,18 @@ int launch_x(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64
 }
 }  // namespace
 
+// The production B > 16 scan with an explicit work split: dyn_frac of the
+// corpus as dynamic tasks of task_docs (0 = the static split); stamps != null
+// runs the STAMPS build (per-workgroup s_memrealtime / s_memtime, 4 x u64).
+extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float* out, int64_t ld, void* stream,
+                            float dyn_frac, int task_docs, void* stamps) {
+  const uint16_t* q = (const uint16_t*)Q;
+  hipStream_t st = (hipStream_t)stream;
+  if (stamps != nullptr)
+    return launch_scan16x4<8, 4, 1, 2, 3, true>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps);
+  return launch_scan16x4<8, 4, 1, 2, 3, false>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr);
+}
+
 extern "C" int lab_scan(cbv2_index* ix, int variant, const void* Q, int B, int lq, float* out, int64_t ld,
                         void* stream) {
   const uint16_t* q = (const uint16_t*)Q;
@@ -324,13 +336,15 @@ extern "C" int lab_scan(cbv2_index* ix, int variant, const void* Q, int B, int l
 }
 
 // MXFP8 scans: variant 0 = the per-doc maxsim_scan_f8_kernel (round-1
-// production), 1 = the doc-interleaved maxsim_scan_f8x4_kernel.
+// production), 1 = the doc-interleaved maxsim_scan_f8x4_kernel (production:
+// guided dynamic tail), 2 = the same with the static split only.
 extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B, int lq, float* out, int64_t ld,
                            void* stream) {
   const uint8_t* Qb = (const uint8_t*)Qbuf;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   hipStream_t st = (hipStream_t)stream;
   if (variant == 1 || B <= kF8DirectMaxB) return scan_f8(ix, Qb, B, lq, out, ld, st);
+  if (variant == 2) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.0f);  // doc-interleaved, static split only
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   int64_t n_chunks = (cu_count(ix->device) + nq_groups - 1) / nq_groups;

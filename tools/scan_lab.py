@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """A/B the scan-kernel variants in ONE process, interleaved rounds (guide §5.4
 rule 24), on the bench's synthetic corpus; check every variant's scores
-against variant 0 and the oracle.  usage: scan_lab.py [--docs N] [--batch B] [--rounds R] [--variants 0,1,2]"""
+against variant 0 and the oracle.  usage: scan_lab.py [--docs N] [--batch B] [--rounds R] [--variants 0,1,2]
+Variants: an int = a production/lab scan variant (lab_scan); "f<frac>t<docs>" =
+the production B > 16 scan with that dynamic-tail split (lab_scan16x4), e.g.
+f0t128 (static), f0.1t128."""
 import argparse
 import ctypes
 import os
@@ -38,6 +41,9 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16", help="fp8: lab_scan_f8 variants 0/1")
+    ap.add_argument("--stamps", default="",
+                    help="comma list of f<frac>t<docs> splits: after the A/B, run each with per-workgroup "
+                         "s_memtime/s_memrealtime stamps and report the duration spread, tail and in-kernel clock")
     a = ap.parse_args()
     build()
     if a.build_only:
@@ -46,6 +52,8 @@ def main():
     L.lab_scan.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.lab_scan_f8.argtypes = L.lab_scan.argtypes
+    L.lab_scan16x4.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
     dev = torch.device("cuda:0")
     Qf = synth.make_queries(a.batch, 32, seed=1)
     planted = synth.planted_ids(max(a.batch, 8), a.docs, 10, seed=2)[: a.batch]
@@ -66,12 +74,21 @@ def main():
         Q = Qf.to(dev, torch.bfloat16)
         qptr = Q.data_ptr()
     st = torch.cuda.current_stream()
-    variants = [int(v) for v in a.variants.split(",")]
+    variants = [v if v.startswith("f") else int(v) for v in a.variants.split(",")]
     outs = {v: torch.empty((a.batch, a.docs), device=dev) for v in variants}
 
-    def run(v):
-        fn = L.lab_scan_f8 if fp8 else L.lab_scan
-        rc = fn(ix._h, v, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
+    def split(v):
+        fr, td = v[1:].split("t")
+        return float(fr), int(td)
+
+    def run(v, stamps=None):
+        if isinstance(v, str):
+            fr, td = split(v)
+            rc = L.lab_scan16x4(ix._h, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream, fr, td,
+                                stamps)
+        else:
+            fn = L.lab_scan_f8 if fp8 else L.lab_scan
+            rc = fn(ix._h, v, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
         assert rc == 0, rc
 
     for v in variants:
@@ -109,6 +126,34 @@ def main():
               f"{flop / med / 1e9:.1f} TFLOP/s "
               f"({flop / med / 1e9 / (5000 if fp8 else 2500) * 100:.1f}% of {a.dtype} peak)  oracle_err {err:.2e} inf_ok {inf_ok} "
               f"max|d vs v{variants[0]}| {dv:.2e}", flush=True)
+    for v in [x for x in a.stamps.split(",") if x] if not fp8 else []:
+        outs.setdefault(v, torch.empty((a.batch, a.docs), device=dev))
+        print(f"split {v}:", flush=True)
+        stamps_report(lambda sp: run(v, sp))
+
+
+def stamps_report(run_stamped, n_wg_max=1 << 16):
+    """Per-workgroup [realtime start, end, memtime start, end] of the last of 3 stamped launches."""
+    buf = torch.zeros((n_wg_max, 4), dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        run_stamped(buf.data_ptr())
+    torch.cuda.synchronize()
+    st = buf.cpu().numpy()
+    st = st[st[:, 1] > 0]
+    r0, r1, t0, t1 = (st[:, i].astype(np.float64) for i in range(4))
+    dur = (r1 - r0) / 100.0                         # s_memrealtime: 100 MHz -> us
+    clk = (t1 - t0) / (r1 - r0) * 0.1               # GHz
+    span = (r1.max() - r0.min()) / 100.0
+    print(f"stamps: {len(st)} workgroups; duration us min {dur.min():.1f} median {np.median(dur):.1f} "
+          f"max {dur.max():.1f}; launch span {span:.1f} us; start skew {(r0.max() - r0.min()) / 100:.1f} us; "
+          f"tail loss (span/median - 1) {span / np.median(dur) - 1:.2%}; clock GHz min {clk.min():.3f} "
+          f"median {np.median(clk):.3f} max {clk.max():.3f}", flush=True)
+    bid = np.nonzero(buf.cpu().numpy()[:, 1] > 0)[0]
+    for x in range(8):
+        sel = (bid & 7) == x
+        if sel.any():
+            print(f"  blockIdx%8={x}: duration median {np.median(dur[sel]):.1f} max {dur[sel].max():.1f} us, "
+                  f"clock median {np.median(clk[sel]):.3f} GHz", flush=True)
 
 
 if __name__ == "__main__":
