@@ -470,6 +470,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16_kernel(
 __device__ __forceinline__ int swz4(int R) { return (((R >> 5) & 3) << 2) | (R & 3); }
 
 // Full iteration (all 4 docs valid for its 32 tokens): 8 tiles, pipelined.
+// (Moving chain k-D's max one MFMA later removes hipcc's s_nop pads for the
+// MFMA -> VALU hazard, 26 -> 2 per iteration, and gains nothing measurable:
+// the partner wave covers them.  Lab, round 1.)
 template <int QW, int D>
 __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
                                            float (&m)[QW][2]) {

@@ -51,6 +51,37 @@ class _DeviceOps:
         return select_topk(scores, k, ids=ids)
 
 
+class _PinnedStage:
+    """Host -> device uploads that do not block the host.
+
+    ``torch.from_numpy(x).to(dev)`` from pageable memory synchronises the
+    stream, i.e. waits for the scan queued ahead of it -- in the pipelined path
+    that stalls the host until batch j+1's scan ends before it can fuse batch j
+    and leaves the GPU idle for the host steps.  Here the array is copied into
+    a pinned buffer and uploaded with ``non_blocking=True``; buffers rotate
+    over ``slots`` calls (the pipeline keeps at most two batches in flight, and
+    a slot is reused only after the host has waited for a later batch)."""
+
+    def __init__(self, slots: int = 2):
+        self._bufs = [None] * slots
+        self._next = 0
+
+    def upload(self, arr: np.ndarray, device) -> torch.Tensor:
+        device = torch.device(device)
+        src = torch.from_numpy(np.ascontiguousarray(arr))
+        if device.type != "cuda":
+            return src.clone()
+        k = self._next
+        self._next = (k + 1) % len(self._bufs)
+        buf = self._bufs[k]
+        if buf is None or buf.numel() < src.numel() * src.element_size():
+            buf = torch.empty((src.numel() * src.element_size(),), dtype=torch.uint8, pin_memory=True)
+            self._bufs[k] = buf
+        h = buf[: src.numel() * src.element_size()].view(src.dtype).view(src.shape)
+        h.copy_(src)
+        return h.to(device, non_blocking=True)
+
+
 class NativeExchange:
     """The exchange inside libcolbert_mi355x.so (include/colbert_mi355x.h:
     cbv2_search_sharded_local/_exchange, cbv2_rerank_sharded) over the RCCL
@@ -76,6 +107,7 @@ class NativeExchange:
         _lib.check(_lib.lib().cbv2_comm_init(comm_ptr, rccl.encode() if os.path.exists(rccl) else None,
                                              ctypes.byref(h)))
         self._h, self._lib = h, _lib
+        self._stage = _PinnedStage(slots=4)               # ids + scores per call
         self.world = int(_lib.lib().cbv2_comm_size(h))
         self.rank = int(_lib.lib().cbv2_comm_rank(h))
         self._ws = None
@@ -112,8 +144,8 @@ class NativeExchange:
             kb = int(lex_i.shape[1])
             if lex_i.shape[0] != B or not 1 <= kb <= kb_cap:
                 raise ValueError(f"stage-1 lists must be [B, <= {kb_cap}] (got {lex_i.shape})")
-            li = torch.from_numpy(np.ascontiguousarray(lex_i, np.int32)).to(self.dev)
-            ls = torch.from_numpy(np.ascontiguousarray(lex_s, np.float32)).to(self.dev)
+            li = self._stage.upload(np.ascontiguousarray(lex_i, np.int32), self.dev)
+            ls = self._stage.upload(np.ascontiguousarray(lex_s, np.float32), self.dev)
             out_li = torch.empty((B, kb), dtype=torch.int32, device=self.dev)
         self._lib.check(L.cbv2_search_sharded_exchange(
             self.index._h, self._h, B, int(k), li.data_ptr() if li is not None else None,
@@ -147,6 +179,7 @@ class ShardedSearcher:
                  native: bool = False, lexical_k: int = 100):
         self.local = local
         self.group = group
+        self._stage = _PinnedStage()
         self.ops = ops if ops is not None else _DeviceOps()
         if world is None:
             world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -193,8 +226,8 @@ class ShardedSearcher:
         if self.world == 1:
             return s, i, np.ascontiguousarray(lex_i, np.int32)
         kb = lex_i.shape[1]
-        lex = torch.stack([torch.from_numpy(np.ascontiguousarray(lex_s, np.float32)).view(torch.int32),
-                           torch.from_numpy(np.ascontiguousarray(lex_i, np.int32))], dim=-1).to(i.device)
+        lex = self._stage.upload(np.stack([np.ascontiguousarray(lex_s, np.float32).view(np.int32),
+                                           np.ascontiguousarray(lex_i, np.int32)], axis=-1), i.device)
         packed = torch.cat([torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1), lex], dim=1)
         allp = self._all_gather(packed)                                                    # [G, B, k+kb, 2]
         S, I = self.ops.merge(allp[:, :, :k, 0].contiguous().view(torch.float32), allp[:, :, :k, 1].contiguous(), k)

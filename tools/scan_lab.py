@@ -4,7 +4,7 @@ rule 24), on the bench's synthetic corpus; check every variant's scores
 against variant 0 and the oracle.  usage: scan_lab.py [--docs N] [--batch B] [--rounds R] [--variants 0,1,2]
 Variants: an int = a production/lab scan variant (lab_scan); "f<frac>t<docs>" =
 the production B > 16 scan with that dynamic-tail split (lab_scan16x4), e.g.
-f0t128 (static), f0.1t128."""
+f0t128 (static), f0.1t128; a suffix k<kind> selects a lab kernel build of lab_scan16x4."""
 import argparse
 import ctypes
 import os
@@ -53,7 +53,8 @@ def main():
                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.lab_scan_f8.argtypes = L.lab_scan.argtypes
     L.lab_scan16x4.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_int]
     dev = torch.device("cuda:0")
     Qf = synth.make_queries(a.batch, 32, seed=1)
     planted = synth.planted_ids(max(a.batch, 8), a.docs, 10, seed=2)[: a.batch]
@@ -78,14 +79,17 @@ def main():
     outs = {v: torch.empty((a.batch, a.docs), device=dev) for v in variants}
 
     def split(v):
+        kind = 0
+        if "k" in v:
+            v, kind = v.split("k")
         fr, td = v[1:].split("t")
-        return float(fr), int(td)
+        return float(fr), int(td), int(kind)
 
     def run(v, stamps=None):
         if isinstance(v, str):
-            fr, td = split(v)
+            fr, td, kind = split(v)
             rc = L.lab_scan16x4(ix._h, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream, fr, td,
-                                stamps)
+                                stamps, kind)
         else:
             fn = L.lab_scan_f8 if fp8 else L.lab_scan
             rc = fn(ix._h, v, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
