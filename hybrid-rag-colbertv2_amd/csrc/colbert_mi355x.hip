@@ -473,13 +473,13 @@ __device__ __forceinline__ int swz4(int R) { return (((R >> 5) & 3) << 2) | (R &
 // (Moving chain k-D's max one MFMA later removes hipcc's s_nop pads for the
 // MFMA -> VALU hazard, 26 -> 2 per iteration, and gains nothing measurable:
 // the partner wave covers them.  Lab, round 1.)
-template <int QW, int D>
+template <int QW, int D, int NT = 8>
 __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
                                            float (&m)[QW][2]) {
   constexpr int NC = 2 * QW;
-  constexpr int NK = 8 * NC;
+  constexpr int NK = NT * NC;
   const int c = lane & 15, g = lane >> 4;
-  const uint8_t* rowp = buf + (32 * (c >> 2) + (c & 3)) * kRowBytes;  // row of tile t: + 4t rows
+  const uint8_t* rowp = buf + (4 * NT * (c >> 2) + (c & 3)) * kRowBytes;  // row of tile t: + 4t rows
   auto frag = [&](int t, bf16x8 (&a)[4]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -492,7 +492,7 @@ __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const b
   for (int k = 0; k < NK + D; ++k) {
     if (k < NK) {
       const int t = k / NC, cc = k % NC;
-      if (cc == 0 && t + 1 < 8) frag(t + 1, a[(t + 1) & 1]);
+      if (cc == 0 && t + 1 < NT) frag(t + 1, a[(t + 1) & 1]);
       f32x4 x = f32x4{};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -510,14 +510,14 @@ __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const b
 }
 
 // Iteration j with ragged docs: per-lane-group -inf C-init masks padding rows.
-template <int QW>
+template <int QW, int NT = 8>
 __device__ __forceinline__ void iter4_ragged(const uint8_t* buf, int lane, int j, int dl_g, int dl_max,
                                              const bf16x8 (&qf)[QW][2][4], float (&m)[QW][2]) {
   const int c = lane & 15, g = lane >> 4;
-  const uint8_t* rowp = buf + (32 * (c >> 2) + (c & 3)) * kRowBytes;
+  const uint8_t* rowp = buf + (4 * NT * (c >> 2) + (c & 3)) * kRowBytes;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int tok0 = 32 * j + 4 * t;
+  for (int t = 0; t < NT; ++t) {
+    const int tok0 = 4 * NT * j + 4 * t;
     if (tok0 >= dl_max) break;
     bf16x8 a[4];
 #pragma unroll
@@ -565,21 +565,25 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
 // static split ends when the slowest XCD does; the dynamic tail lets the fast
 // ones take the remainder.  Every doc range runs the same pipelined loop.
 // STAMPS (lab only): per-workgroup s_memrealtime / s_memtime at start and end.
-template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false>
+template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32>
 __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
     int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr, int task_docs,
     uint64_t* __restrict__ stamps) {
+  // TPI tokens of 4 docs per iteration (32: 32 KiB, 64: 64 KiB), IPG per group
   constexpr int QPB = WAVES * QW;
-  constexpr int kPieces = kDocBytes / 1024;  // 32 x 1 KiB per iteration
+  constexpr int kIterBytes = 4 * TPI * kRowBytes;
+  constexpr int IPG = kLd / TPI, NT = TPI / 4;
+  constexpr int kPieces = kIterBytes / 1024;
   constexpr int kPiecesPerWave = kPieces / WAVES;
+  static_assert(TPI == 32 || TPI == 64, "32 or 64 tokens per iteration");
   static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
   static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
   // one LDS object only: with a second __shared__ array hipcc starts putting
   // vmcnt(0) before the ring's ds_reads (LDS-DMA alias tracking)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kDocBytes + 16];
-  int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kDocBytes);
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterBytes + 16];
+  int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterBytes);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -600,14 +604,16 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
 #pragma unroll
   for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QPB + wave * QW + q, B, lq, lane, qf[q]);
 
-  // LDS-DMA piece p = rows 4p..4p+3 of the image = doc p>>3, tokens 32j + 4(p&7) + 0..3
+  // LDS-DMA piece p = rows 4p..4p+3 of the image [4 docs][TPI tokens] = doc
+  // 4p / TPI, tokens TPI*j + 4p % TPI + 0..3; slot XOR (doc << 2 | R & 3)
   uint32_t src_off[kPiecesPerWave];
   int src_doc[kPiecesPerWave];
 #pragma unroll
   for (int jj = 0; jj < kPiecesPerWave; ++jj) {
     const int R = 4 * (wave * kPiecesPerWave + jj) + (lane >> 4);
-    src_off[jj] = (R & 31) * kRowBytes + 16 * ((lane & 15) ^ swz4(R));
-    src_doc[jj] = R >> 5;
+    const int doc = R / TPI;
+    src_off[jj] = (R % TPI) * kRowBytes + 16 * ((lane & 15) ^ ((doc << 2) | (R & 3)));
+    src_doc[jj] = doc;
   }
 
   // the first range: this workgroup's static chunk (may be empty)
@@ -618,14 +624,14 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
       const int nd = (int)(d_end - d_begin);
       const int ngr = (nd + 3) >> 2;
       auto issue = [&](int it, int buf) {
-        const int G = it >> 2, j = it & 3;
+        const int G = it / IPG, j = it % IPG;
 #pragma unroll
         for (int jj = 0; jj < kPiecesPerWave; ++jj) {
           const int piece = wave * kPiecesPerWave + jj;
           int d = 4 * G + src_doc[jj];
           d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-          const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * 32 * kRowBytes + src_off[jj];
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kDocBytes + piece * 1024), 16,
+          const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * TPI * kRowBytes + src_off[jj];
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
                                            0, 0);
         }
       };
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
       for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
       int dl_g = 0, dl_min = 0, dl_max = 0;
 
-      const int nit = 4 * ngr;
+      const int nit = IPG * ngr;
       issue(0, 0);
       if (NBUF == 3 && nit > 1) issue(1, 1);
       int cur = 0;           // ring slot of iteration it
@@ -651,10 +657,10 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
         stored = false;
         if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
         if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
-        const uint8_t* buf = smem + cur * kDocBytes;
+        const uint8_t* buf = smem + cur * kIterBytes;
         cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
 
-        const int G = it >> 2, j = it & 3;
+        const int G = it / IPG, j = it % IPG;
         if (j == 0) {
           int dl4[4];
 #pragma unroll
@@ -668,11 +674,11 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
 #pragma unroll
           for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
         }
-        if (32 * j + 32 <= dl_min)
-          iter4_full<QW, D>(buf, lane, qf, m);
-        else if (32 * j < dl_max)
-          iter4_ragged<QW>(buf, lane, j, dl_g, dl_max, qf, m);
-        if (j == 3) {
+        if (TPI * j + TPI <= dl_min)
+          iter4_full<QW, D, NT>(buf, lane, qf, m);
+        else if (TPI * j < dl_max)
+          iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
+        if (j == IPG - 1) {
           // doc 4G+g's score in every lane of group g; lane c of the 64-doc block
           // register keeps doc group c, so lane (c, g) holds doc 4c+g of the block
 #pragma unroll
@@ -1009,36 +1015,39 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8_kernel(
 }
 
 // Doc-interleaved f8 scan (the production B > 8 MXFP8 path; same design as
-// maxsim_scan16x4_kernel): each iteration stages 32 tokens of 4 docs (16 KiB
-// of e4m3 + 256 B of scales) into a 3-deep LDS ring; row tile t holds tokens
-// 4t..4t+3 of docs 0..3 in rows 4g..4g+3, so output lane group g is doc g and
-// the epilogue is one 16-lane DPP sum per query per 4 docs.  Image: row R =
-// 32*doc + token, 8 slots of 16 B with slot s at s ^ swz8x4(R) (the 8 rows of
-// one parity a lane group reads get 8 distinct slots); scales [128 rows][2].
-__device__ __forceinline__ int swz8x4(int R) { return (((R >> 5) & 3) << 1) | ((R >> 1) & 1); }
-constexpr int kF8IterBytes = 32 * 4 * kDim;        // 16 KiB of e4m3 per iteration
-constexpr int kF8IterStage = kF8IterBytes + 256;   // + 4 docs x 32 tokens x 2 scale bytes
+// maxsim_scan16x4_kernel): each iteration stages TPI tokens of 4 docs (TPI x
+// 512 B of e4m3 + TPI x 8 B of scales) into an LDS ring; row tile t holds
+// tokens 4t..4t+3 of docs 0..3 in rows 4g..4g+3, so output lane group g is doc
+// g and the epilogue is one 16-lane DPP sum per query per 4 docs.  Image: row
+// R = TPI*doc + token, 8 slots of 16 B with slot s at s ^ swz_f8(R) =
+// s ^ (doc << 1 | (R >> 1) & 1) (the 8 rows of one parity a lane group reads
+// get 8 distinct slots); then the 2 scale bytes of every row at
+// 4 * TPI * 128 + 2R.
+template <int TPI>
+__device__ __forceinline__ int swz_f8(int R) { return (((R / TPI) & 3) << 1) | ((R >> 1) & 1); }
 
+template <int TPI = 32>
 __device__ __forceinline__ void lds_afrag_f8x4(const uint8_t* buf, int t, int lane, i32x8& a, int& as) {
   const int c = lane & 15, g = lane >> 4;
-  const int R = 32 * (c >> 2) + 4 * t + (c & 3);
+  const int R = TPI * (c >> 2) + 4 * t + (c & 3);
   const uint8_t* row = buf + R * kDim;
-  const int sw = swz8x4(R);
+  const int sw = swz_f8<TPI>(R);
   const u32x4 lo = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g) ^ sw));
   const u32x4 hi = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g + 1) ^ sw));
   a = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-  as = buf[kF8IterBytes + R * 2 + (g & 1)];
+  as = buf[4 * TPI * kDim + R * 2 + (g & 1)];
 }
 
-template <int QW, int D>
+template <int QW, int D, int TPI = 32>
 __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, const i32x8 (&qa)[QW][2],
                                                const int (&qs)[QW][2], float (&m)[QW][2]) {
   constexpr int NC = 2 * QW;
   static_assert(D >= 1 && NC % (D + 1) == 0, "ring slot of chain k must be k % (D+1) across tiles");
+  constexpr int NT = TPI / 4;
   i32x8 a[2];
   int as[2];
   f32x4 acc[D + 1];
-  lds_afrag_f8x4(buf, 0, lane, a[0], as[0]);
+  lds_afrag_f8x4<TPI>(buf, 0, lane, a[0], as[0]);
   auto fold = [&](int k) {  // row max of chain k (k = t * NC + cc), issued D chains later
     const int pc = k % NC;
     const f32x4& y = acc[k % (D + 1)];
@@ -1046,11 +1055,11 @@ __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, con
     mm = fmaxf(fmaxf(fmaxf(fmaxf(mm, y[0]), y[1]), y[2]), y[3]);
   };
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
+  for (int t = 0; t < NT; ++t) {
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc) {
       const int k = t * NC + cc;
-      if (cc == 0 && t + 1 < 8) lds_afrag_f8x4(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
+      if (cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
       acc[k % (D + 1)] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
           a[t & 1], qa[cc >> 1][cc & 1], f32x4{}, 0, 0, 0, as[t & 1], 0, qs[cc >> 1][cc & 1]);
       if (k >= D) fold(k - D);
@@ -1058,20 +1067,20 @@ __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, con
     }
   }
 #pragma unroll
-  for (int k = 8 * NC - D; k < 8 * NC; ++k) fold(k);
+  for (int k = NT * NC - D; k < NT * NC; ++k) fold(k);
 }
 
-template <int QW>
+template <int QW, int TPI = 32>
 __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, int j, int dl_g, int dl_max,
                                                  const i32x8 (&qa)[QW][2], const int (&qs)[QW][2],
                                                  float (&m)[QW][2]) {
-  const int nt = min(8, (dl_max - 32 * j + 3) >> 2);
+  const int nt = min(TPI / 4, (dl_max - TPI * j + 3) >> 2);
 #pragma unroll 1
   for (int t = 0; t < nt; ++t) {
-    const int tok0 = 32 * j + 4 * t;
+    const int tok0 = TPI * j + 4 * t;
     i32x8 a;
     int as;
-    lds_afrag_f8x4(buf, t, lane, a, as);
+    lds_afrag_f8x4<TPI>(buf, t, lane, a, as);
     f32x4 init;
 #pragma unroll
     for (int r = 0; r < 4; ++r) init[r] = (tok0 + r < dl_g) ? 0.0f : neg_inf();
@@ -1079,18 +1088,24 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
   }
 }
 
-template <int WAVES, int QW, int D = 1, int NBUF = 3>   // D = 2 spills at QW = 8 (hipcc 7.2)
+template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32>   // D = 2 spills at QW = 8 (hipcc 7.2)
 __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
     float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr,
     int task_docs) {
   constexpr int QPB = WAVES * QW;
-  constexpr int kPieces = kF8IterBytes / 1024;  // 16 x 1 KiB per iteration
+  constexpr int kIterBytes = 4 * TPI * kDim;                 // e4m3 bytes per iteration
+  constexpr int kIterStage = kIterBytes + 4 * TPI * 2;        // + 2 scale bytes per row
+  constexpr int IPG = kLd / TPI;
+  constexpr int kScaleDma = 4 * TPI * 2 / 256;                // 256-B scale DMAs per iteration
+  constexpr int kPieces = kIterBytes / 1024;
   constexpr int kPiecesPerWave = kPieces / WAVES;
-  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kF8IterStage + 256 + 16];
-  int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kF8IterStage + 256);
+  static_assert(TPI == 32 || TPI == 64 || TPI == 128, "32, 64 or 128 tokens per iteration");
+  static_assert(kPieces % WAVES == 0 && kScaleDma <= WAVES, "pieces must split evenly over waves");
+  static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterStage + 256 + 16];
+  int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterStage + 256);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1107,15 +1122,9 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
 #pragma unroll
   for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, qg * QPB + wave * QW + q, B, lq, lane, qa[q], qs[q]);
 
-  // piece p = image rows 8p..8p+7 (128 B each) = doc p>>2, tokens 32j + 8(p&3) + 0..7
-  uint32_t src_off[kPiecesPerWave];
-  int src_doc[kPiecesPerWave];
-#pragma unroll
-  for (int jj = 0; jj < kPiecesPerWave; ++jj) {
-    const int R = 8 * (wave * kPiecesPerWave + jj) + (lane >> 3);
-    src_off[jj] = (R & 31) * kDim + 16 * ((lane & 7) ^ swz8x4(R));
-    src_doc[jj] = R >> 5;
-  }
+  // piece p = image rows 8p..8p+7 (128 B each) = doc 8p / TPI (uniform per
+  // piece), tokens TPI*j + 8p % TPI + 0..7.  Offsets are recomputed per issue
+  // (a few VALU) rather than held: at 8 queries per wave the VGPR file is full.
   // the same static chunks + guided dynamic tail as maxsim_scan16x4_kernel
   int64_t d_begin = chunk * chunk_docs;
   int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
@@ -1125,23 +1134,26 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
   const int ngr = (nd + 3) >> 2;
   auto clamp_doc = [&](int d) { return d < nd ? d : nd - 1; };  // the last group's missing docs: rows masked
   auto issue = [&](int it, int buf) {
-    const int G = it >> 2, j = it & 3;
-    uint8_t* sbuf = smem + buf * kF8IterStage;
+    const int G = it / IPG, j = it % IPG;
+    uint8_t* sbuf = smem + buf * kIterStage;
 #pragma unroll
     for (int jj = 0; jj < kPiecesPerWave; ++jj) {
       const int piece = wave * kPiecesPerWave + jj;
-      const int d = clamp_doc(4 * G + src_doc[jj]);
-      const uint8_t* src = tokens + (size_t)(d_begin + d) * kF8DocBytes + (size_t)j * 32 * kDim + src_off[jj];
+      const int R = 8 * piece + (lane >> 3);
+      const uint32_t off = (R % TPI) * kDim + 16 * ((lane & 7) ^ swz_f8<TPI>(R));
+      const int d = clamp_doc(4 * G + 8 * piece / TPI);
+      const uint8_t* src = tokens + (size_t)(d_begin + d) * kF8DocBytes + (size_t)j * TPI * kDim + off;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + piece * 1024), 16, 0, 0);
     }
-    if (wave == 0) {  // 4 docs x 64 scale bytes: lane L -> doc L>>4, bytes 4(L&15)
-      const int d = clamp_doc(4 * G + (lane >> 4));
-      const uint8_t* src = tscales + (size_t)(d_begin + d) * kF8ScaleBytes + (size_t)j * 64 + 4 * (lane & 15);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + kF8IterBytes), 4, 0, 0);
+    if (wave < kScaleDma) {  // scale bytes b = 256 * wave + 4L: row b/2 = TPI * doc + token
+      const int R = (256 * wave + 4 * lane) / 2;
+      const int d = clamp_doc(4 * G + R / TPI);
+      const uint8_t* src = tscales + (size_t)(d_begin + d) * kF8ScaleBytes + (size_t)(j * TPI + R % TPI) * 2;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + kIterBytes + 256 * wave), 4, 0, 0);
     }
   };
   // vector-memory ops per wave per iteration (the vmcnt that leaves one iteration in flight)
-  const bool loader = wave == 0;
+  const bool loader = wave < kScaleDma;
 
   float sc[QW];
   float m[QW][2];
@@ -1149,7 +1161,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
   for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
   int dl_g = 0, dl_min = 0, dl_max = 0;
 
-  const int nit = 4 * ngr;
+  const int nit = IPG * ngr;
   issue(0, 0);
   if (NBUF == 3 && nit > 1) issue(1, 1);
   int cur = 0;
@@ -1168,10 +1180,10 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
     stored = false;
     if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
     if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
-    const uint8_t* buf = smem + cur * kF8IterStage;
+    const uint8_t* buf = smem + cur * kIterStage;
     cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
 
-    const int G = it >> 2, j = it & 3;
+    const int G = it / IPG, j = it % IPG;
     if (j == 0) {
       int dl4[4];
 #pragma unroll
@@ -1185,11 +1197,11 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
 #pragma unroll
       for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     }
-    if (32 * j + 32 <= dl_min)
-      iter_f8x4_full<QW, D>(buf, lane, qa, qs, m);
-    else if (32 * j < dl_max)
-      iter_f8x4_ragged<QW>(buf, lane, j, dl_g, dl_max, qa, qs, m);
-    if (j == 3) {
+    if (TPI * j + TPI <= dl_min)
+      iter_f8x4_full<QW, D, TPI>(buf, lane, qa, qs, m);
+    else if (TPI * j < dl_max)
+      iter_f8x4_ragged<QW, TPI>(buf, lane, j, dl_g, dl_max, qa, qs, m);
+    if (j == IPG - 1) {
 #pragma unroll
       for (int q = 0; q < QW; ++q) {
         const float v = dpp_row_sum16((c < lq ? m[q][0] : 0.0f) + (16 + c < lq ? m[q][1] : 0.0f));
@@ -1954,7 +1966,7 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
   return CBV2_OK;
 }
 
-template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS>
+template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -1962,7 +1974,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
   ScanSplit sp;
   const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI>), dim3((unsigned)(nq_groups * sp.n_chunks)),
                      dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, sp.chunk_docs,
                      sp.static_docs, sp.ctr, sp.task_docs, stamps);
   return launch_check("maxsim_scan16x4_kernel");
@@ -2015,7 +2027,7 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16W4Q2:
       return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
     case kScan16x4W8:
-      return launch_scan16x4<8, 4, 1, 2, 3, false>(ix, Q, B, lq, out, ld_out, st);
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, Q, B, lq, out, ld_out, st);
     case kScan16x4W4:
       return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st);
     default:
@@ -2026,8 +2038,22 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
 constexpr int kF8DirectMaxB = 8;
 constexpr int kF8Waves = 8, kF8QW = 8;
 
+template <int TPI, int NBUF>
+int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
+                hipStream_t st, float dyn_frac, int task_docs) {
+  constexpr int QPB = kF8Waves * kF8QW;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  ScanSplit sp;
+  const int rc = plan_split(ix, nq_groups, cu_count(ix->device), dyn_frac, task_docs, st, &sp);
+  if (rc != CBV2_OK) return rc;
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW, 1, NBUF, TPI>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+                     dim3(kF8Waves * 64), 0, st, ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out,
+                     ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs);
+  return launch_check("maxsim_scan_f8x4_kernel");
+}
+
 int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
-            float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs) {
+            float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, int shape = 0) {
   if (ix->n == 0) return CBV2_OK;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   if (B <= kF8DirectMaxB) {
@@ -2044,15 +2070,15 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                        ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
     return launch_check("maxsim_scan_f8_direct_kernel");
   }
-  constexpr int QPB = kF8Waves * kF8QW;
-  const int nq_groups = (B + QPB - 1) / QPB;
-  ScanSplit sp;
-  const int rc = plan_split(ix, nq_groups, cu_count(ix->device), dyn_frac, task_docs, st, &sp);
-  if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW>), dim3((unsigned)(nq_groups * sp.n_chunks)),
-                     dim3(kF8Waves * 64), 0, st, ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out,
-                     ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs);
-  return launch_check("maxsim_scan_f8x4_kernel");
+  // shape (lab A/B): 0 production, 1 = 32-token iterations / 3-deep ring,
+  // 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 / 2-deep
+  switch (shape) {
+    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    default: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+  }
 }
 
 int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {

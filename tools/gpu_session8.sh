@@ -1,0 +1,7 @@
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests8.log 2>&1 || exit 1
+timeout -k 10 400 python -u tools/scan_lab.py --docs 1000000 --batch 256 --rounds 5 --variants f0.1t-16,f0.1t-16k1 > gpurun_out/lab8.log 2>&1 || exit 2
+timeout -k 10 300 python -u tools/scan_lab.py --docs 125000 --batch 256 --rounds 9 --variants f0.1t-16,f0.1t-16k1 > gpurun_out/lab8_125k.log 2>&1 || exit 3
+echo done

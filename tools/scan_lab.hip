@@ -307,12 +307,16 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
                             float dyn_frac, int task_docs, void* stamps, int kind) {
   const uint16_t* q = (const uint16_t*)Q;
   hipStream_t st = (hipStream_t)stream;
-  // kind: a slot for lab-only kernel builds (round 1: max placement one MFMA
-  // later, D = 1/2/3 -> 73.3 / 76.3 / 76.1 % vs product 76.3 %; removed)
+  // kind: lab-only kernel builds (round 1: max placement one MFMA later,
+  // D = 1/2/3 -> 73.3 / 76.3 / 76.1 % vs product 76.3 %; removed)
+  //   kind 0 = production (64-token iterations, 2-deep ring: 142.5 -> 139.1 ms
+  //   at 1M vs 32-token iterations with a 3-deep ring, which is kind 1)
+  if (kind == 1) return launch_scan16x4<8, 4, 1, 2, 3, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
   if (kind != 0) return -1;
   if (stamps != nullptr)
-    return launch_scan16x4<8, 4, 1, 2, 3, true>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps);
-  return launch_scan16x4<8, 4, 1, 2, 3, false>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr);
+    return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
+                                                    (uint64_t*)stamps);
+  return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr);
 }
 
 extern "C" int lab_scan(cbv2_index* ix, int variant, const void* Q, int B, int lq, float* out, int64_t ld,
@@ -348,6 +352,8 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
   hipStream_t st = (hipStream_t)stream;
   if (variant == 1 || B <= kF8DirectMaxB) return scan_f8(ix, Qb, B, lq, out, ld, st);
   if (variant == 2) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.0f);  // doc-interleaved, static split only
+  if (variant >= 10 && variant <= 14) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
+                                                     variant - 10);  // iteration shapes, see scan_f8
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   int64_t n_chunks = (cu_count(ix->device) + nq_groups - 1) / nq_groups;
