@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="time unpipelined steps")
     ap.add_argument("--native-exchange", action="store_true",
                     help="N>1: run the all-gather / all-reduce inside the C ABI (cbv2_*_sharded) on torch's RCCL comm")
-    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+    ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="index tokens: bf16 (config 3) or MXFP8 e4m3 + E8M0 (config 5)")
     args = ap.parse_args()
 
@@ -132,15 +132,20 @@ def main():
     log(f"host BM25 shard built in {time.time() - t_bm:.1f}s ({lex.n_docs} docs, {len(lex.doc_terms)} terms)")
     bm_all = lambda: lex.search(qt, qo, args.k)                 # noqa: E731  stage 1, whole batch
     bm_one = lambda: lex.search(qt[:qo[1]], qo[:2], args.k)     # noqa: E731  stage 1, query 0
-    tokens, doclens = synth.make_shard(begin, end, Qf, planted, dev, seed=0)
-    if args.dtype == "fp8":
+    faithful = args.dtype == "fp32"
+    tokens, doclens = synth.make_shard(begin, end, Qf, planted, dev, seed=0,
+                                       dtype=torch.float32 if faithful else torch.bfloat16)
+    if faithful:
+        # fp32-faithful index: bf16 hi scanned, bf16 residual gathered for the band (HIP split)
+        ix = ColbertIndex.faithful_f32(tokens, doclens, id_base=begin)
+    elif args.dtype == "fp8":
         ix = ColbertIndex.mxfp8(tokens, doclens, id_base=begin)   # quantized on the GPU (HIP kernel)
         tokens_ref = tokens                                          # kept only for the spot parity check
     else:
         ix = ColbertIndex(tokens, doclens, id_base=begin)
     searcher = ShardedSearcher(ix, native=args.native_exchange and world > 1 and backend == "nccl",
                                lexical_k=args.k)
-    Q = Qf.to(dev, torch.bfloat16)
+    Q = Qf.to(dev, torch.float32 if faithful else torch.bfloat16)
     Q1 = Q[:1].contiguous()
     torch.cuda.synchronize()
     log(f"setup {time.time() - t_setup:.1f}s: rank {rank}/{world} docs [{begin},{end}) B={B}")
@@ -206,10 +211,12 @@ def main():
     # ---- dominant kernel: MaxSim scan, timed with HIP events on its stream
     scan_ms = []
     st = torch.cuda.current_stream()
+    # (fp32-faithful: the scan is the bf16 scan of hi; score() there is the full faithful rescoring)
+    scan_ix, Qs = (ColbertIndex(ix.tokens, ix.doclens, id_base=begin), Q.bfloat16()) if faithful else (ix, Q)
     for _ in range(3):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        ix.score(Q)
+        scan_ix.score(Qs)
         e1.record(st)
         e1.synchronize()
         scan_ms.append(e0.elapsed_time(e1))
@@ -241,10 +248,10 @@ def main():
             qq, qs = quantize_mxfp8(Q[b:b + 1])
             qd = orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy())
             tol = 2e-3
-        else:
+        else:                            # bf16: the stored bf16 values; fp32: the fp32 values themselves
             d = tokens[sel].float().cpu().numpy()
             qd = Q[b:b + 1].float().cpu().numpy()
-            tol = 1e-3
+            tol = 1e-4 if faithful else 1e-3
         ref = orc.maxsim(qd, d)[0]
         got = fs[b, : len(ids_b)].cpu().numpy()
         bad += int(np.abs(got - ref).max() > tol)
@@ -253,6 +260,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(Q, tokens, n_total, args.cpu_budget)
 
+    band = None
+    if faithful:                         # the certified band each query rescored (last search call)
+        bs = ix.last_band.float()
+        band = {"mean": round(float(bs.mean()), 1), "max": int(bs.max()), "uncertified_rows": int((bs < 0).sum())}
     fp8 = args.dtype == "fp8"
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     kern = "maxsim_scan_f8x4_kernel" if fp8 else SCAN_KERNEL
@@ -263,7 +274,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (unit-norm N(0,I) tokens, Zipf term-id corpus for BM25, 10 planted positives/query)",
-            "config": {"workload": ("config 5 (MXFP8 e4m3 tokens, block-scaled fp8 MFMA)" if fp8 else "config 3") +
+            "config": {"workload": ("config 5 (MXFP8 e4m3 tokens, block-scaled fp8 MFMA)" if fp8 else
+                                    "config 3, fp32-faithful index (bf16 scan + certified hi/lo band rescoring)"
+                                    if faithful else "config 3") +
                                    f": {n_total} chunks x 128 tokens x 128-d, host BM25 top-100 + "
                                    "ColBERT MaxSim top-100 + RRF + rerank top-10",
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
@@ -278,6 +291,8 @@ def main():
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad},
         }
+        if band is not None:
+            line["faithful_band"] = band
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

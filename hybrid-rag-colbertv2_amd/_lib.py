@@ -21,6 +21,7 @@ SCORER_MAXSIM = 0
 SCORER_REF_MEANPOOL_COSINE = 1
 SCORERS = {"maxsim": SCORER_MAXSIM, "ref_meanpool_cosine": SCORER_REF_MEANPOOL_COSINE}
 ERR_EINVAL, ERR_EUNSUPPORTED, ERR_EHIP, ERR_ESTATE = -1, -2, -3, -4
+F32_SCORE, F32_SEARCH, F32_RERANK = 0, 1, 2
 
 _p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
 _SIGS = {
@@ -65,6 +66,12 @@ _SIGS = {
     "cbv2_search_sharded_exchange": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _p, _i32, _p, _sz, _p, _p, _p, _p]),
     "cbv2_rerank_sharded": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
     "cbv2_bm25_destroy": (ctypes.c_int, [_p]),
+    "cbv2_split_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _p]),
+    "cbv2_index_attach_residual": (ctypes.c_int, [_p, _p, ctypes.c_float, ctypes.c_float]),
+    "cbv2_f32_workspace_bytes": (_sz, [_p, _i32, _i32, _i32, _i32]),
+    "cbv2_score_f32": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _sz, _p, _i64, _p]),
+    "cbv2_search_f32": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
+    "cbv2_rerank_f32": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
 }
 
 _lib = None

@@ -565,8 +565,8 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
 // static split ends when the slowest XCD does; the dynamic tail lets the fast
 // ones take the remainder.  Every doc range runs the same pipelined loop.
 // STAMPS (lab only): per-workgroup s_memrealtime / s_memtime at start and end.
-template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32>
-__global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan16x4_kernel(
+template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2>
+__global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
     int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr, int task_docs,
@@ -1685,6 +1685,227 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// fp32-faithful path (an index built from fp32 embeddings, as the reference
+// stores them: local_rag_complete.py:735-746).  Each fp32 token x is split
+// into hi = bf16(x) (round to nearest even; the index tokens every scan reads)
+// and lo = bf16(x - hi) (the residual, read only for candidates).  A
+// candidate's faithful score takes three bf16 MFMAs per product
+// (lo.qhi + hi.qlo first, then hi.qhi; only lo.qlo ~2^-16 is dropped), fp32
+// accumulate.  The bf16 scan's score T of any doc is within beta(q) of its
+// exact score (Cauchy-Schwarz on the residuals, bounds below), so every doc
+// of the exact top-k has T >= T_k - 2 beta(q): the band the search rescores.
+// ---------------------------------------------------------------------------
+constexpr float kBoundUp = 1.0f + 1.0f / 1024.0f;  // rounds fp32 norm sums up
+constexpr float kAccSlack = 1.0f / 4096.0f;        // MFMA accumulation + dropped terms, per |q||d|
+
+// 16 lanes per 128-value row, 8 values per lane: split into hi/lo, return the
+// lane-group sums of x^2, (x - hi)^2 and hi^2 in every lane of the group.
+__device__ __forceinline__ void split_row8(const float* __restrict__ src, uint16_t* __restrict__ hi,
+                                           uint16_t* __restrict__ lo, int sub, float& xx, float& rr, float& hh) {
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src + 8 * sub);
+  const f32x4 v0 = s4[0], v1 = s4[1];
+  float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  uint16_t h[8], l[8];
+  xx = rr = hh = 0.0f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 bh = (__bf16)x[e];
+    const float fh = (float)bh;
+    const float r = x[e] - fh;  // exact: hi is the rounding of x
+    const __bf16 bl = (__bf16)r;
+    h[e] = __builtin_bit_cast(uint16_t, bh);
+    l[e] = __builtin_bit_cast(uint16_t, bl);
+    xx += x[e] * x[e];
+    rr += r * r;
+    hh += fh * fh;
+  }
+  u32x4 ph, pl;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ph[e] = (uint32_t)h[2 * e] | ((uint32_t)h[2 * e + 1] << 16);
+    pl[e] = (uint32_t)l[2 * e] | ((uint32_t)l[2 * e + 1] << 16);
+  }
+  *reinterpret_cast<u32x4*>(hi + 8 * sub) = ph;
+  *reinterpret_cast<u32x4*>(lo + 8 * sub) = pl;
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    xx += __shfl_xor(xx, off);
+    rr += __shfl_xor(rr, off);
+    hh += __shfl_xor(hh, off);
+  }
+}
+
+// Index split: rows of 128 f32 -> hi, lo; bounds[0] = max ||x - hi||, bounds[1]
+// = max ||hi|| over the rows that score (rounded up; atomic max on the
+// non-negative bits).  doclens (nullable): rows are docs of ld rows and row t
+// of doc i scores iff t < doclens[i] (padding is split but never bounds).
+__global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict__ x, int64_t rows, int ld,
+                                                        const int32_t* __restrict__ doclens,
+                                                        uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
+                                                        float* __restrict__ bounds) {
+  const int sub = threadIdx.x & 15;
+  float rmax = 0.0f, hmax = 0.0f;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; r < rows;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+    float xx, rr, hh;
+    split_row8(x + r * kDim, hi + r * kDim, lo + r * kDim, sub, xx, rr, hh);
+    if (doclens == nullptr || (int)(r % ld) < doclens[r / ld]) {
+      rmax = fmaxf(rmax, sqrtf(rr) * kBoundUp);
+      hmax = fmaxf(hmax, sqrtf(hh) * kBoundUp);
+    }
+  }
+#pragma unroll
+  for (int off = 16; off < 64; off <<= 1) {
+    rmax = fmaxf(rmax, __shfl_xor(rmax, off));
+    hmax = fmaxf(hmax, __shfl_xor(hmax, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(reinterpret_cast<unsigned int*>(bounds), __float_as_uint(rmax));
+    atomicMax(reinterpret_cast<unsigned int*>(bounds) + 1, __float_as_uint(hmax));
+  }
+}
+
+// Query split: one wave per query, 4 rows at a time.  beta[b] bounds
+// |T - S| for every doc: sum_i ||q_i|| E + ||q_i - qhi_i|| M + slack (||q_i|| + ||q_i - qhi_i||) M
+// with E = max ||x - hi||, M = max ||hi|| of the index.
+__global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict__ Q, int lq,
+                                                         uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
+                                                         float E, float M, float* __restrict__ beta) {
+  const int b = blockIdx.x, lane = threadIdx.x, grp = lane >> 4, sub = lane & 15;
+  float acc = 0.0f;
+  for (int r = grp; r < lq; r += 4) {
+    const size_t row = (size_t)b * lq + r;
+    float xx, rr, hh;
+    split_row8(Q + row * kDim, qhi + row * kDim, qlo + row * kDim, sub, xx, rr, hh);
+    const float nq = sqrtf(xx) * kBoundUp, eq = sqrtf(rr) * kBoundUp;
+    acc += nq * E + eq * M + kAccSlack * (nq + eq) * M;
+  }
+  acc = sub == 0 ? acc : 0.0f;
+#pragma unroll
+  for (int off = 16; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) beta[b] = acc * kBoundUp;
+}
+
+// One row tile, faithful product: acc = init + lo.qhi + hi.qlo + hi.qhi.
+__device__ __forceinline__ void tile16_x3(const bf16x8 (&ah)[4], const bf16x8 (&al)[4], const bf16x8 (&qh)[2][4],
+                                          const bf16x8 (&ql)[2][4], const f32x4& init, float (&m)[2]) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    f32x4 acc = init;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s], qh[ct][s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s], ql[ct][s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s], qh[ct][s], acc, 0, 0, 0);
+    m[ct] = fmaxf(fmaxf(m[ct], fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
+  }
+}
+
+// Faithful rescoring: query b = blockIdx.y against candidates c (cand == null:
+// c is the local doc index), each wave kRsPerWave candidates; out[b*ld_out + c].
+// count (nullable) bounds c per query (the band collected by the search).
+constexpr int kRsPerWave = 4;
+__global__ __launch_bounds__(256) void rescore_x3_kernel(
+    const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
+    int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
+    const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
+    float* __restrict__ out, int64_t ld_out) {
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  int64_t lim = limit;
+  if (count != nullptr) {
+    const int64_t cb = count[b];
+    lim = cb < lim ? cb : lim;
+  }
+  const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * kRsPerWave;
+  if (c0 >= lim) return;  // wave-uniform; no block-level sync below
+  bf16x8 qh[2][4], ql[2][4];
+  load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+  load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+  for (int64_t c = c0; c < c0 + kRsPerWave && c < lim; ++c) {
+    const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
+    const int64_t loc = id - id_base;
+    float v = neg_inf();
+    if (id >= 0 && loc >= 0 && loc < n) {
+      int dl = doclens[loc];
+      dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+      const uint8_t* dh = hi + (size_t)loc * kDocBytes;
+      const uint8_t* dlo = lo + (size_t)loc * kDocBytes;
+      float m[2] = {neg_inf(), neg_inf()};
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        bf16x8 ah[4][4], al[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int rt = 4 * half + t;
+          if (16 * rt < dl) {
+            gbl_afrag16(dh, rt, lane, ah[t]);
+            gbl_afrag16(dlo, rt, lane, al[t]);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int rt = 4 * half + t;
+          if (16 * rt < dl) {
+            const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+            tile16_x3(ah[t], al[t], qh, ql, init, m);
+          }
+        }
+      }
+      v = reduce16(m[0], m[1], lane, lq);
+    }
+    if (lane == 0) out[(size_t)b * ld_out + c] = v;
+  }
+}
+
+// Band collect: row b of the bf16 scan's scores T; every doc with T >= T_k -
+// 2 beta(b) is appended (global id) to cand[b][0..cap); count[b] = the band
+// size (may exceed cap: the search then reports the row as not certified).
+__global__ __launch_bounds__(256) void band_collect_kernel(const float* __restrict__ T, int64_t n,
+                                                           const float* __restrict__ topk_s, int k,
+                                                           const float* __restrict__ beta, int64_t id_base,
+                                                           int cap, int32_t* __restrict__ cand,
+                                                           int32_t* __restrict__ count) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const float thr = topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b];
+  const float* row = T + (size_t)b * n;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += step) {  // uniform trip count per wave
+    const int64_t i = i0 + threadIdx.x;
+    const bool take = i < n && row[i] >= thr;
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) continue;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(count + b, __popcll(mask));
+    base = __shfl(base, 0);
+    const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+    if (take && pos < cap) cand[(size_t)b * cap + pos] = (int32_t)(id_base + i);
+  }
+}
+
+// Band select: exact top-k of the rescored band (score desc, id asc);
+// status[b] = band size when certified, -1 when the band overflowed cap.
+constexpr int kBandCapMax = 16384;
+__global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __restrict__ F,
+                                                                 const int32_t* __restrict__ cand,
+                                                                 const int32_t* __restrict__ count, int cap, int k,
+                                                                 int64_t id_base, float* __restrict__ out_s,
+                                                                 int32_t* __restrict__ out_i,
+                                                                 int32_t* __restrict__ status) {
+  __shared__ uint64_t keys[kBandCapMax];
+  const int b = blockIdx.x;
+  const int total = count[b];
+  const int cnt = total < cap ? total : cap;
+  for (int t = threadIdx.x; t < cnt; t += blockDim.x)
+    keys[t] = rank_key(F[(size_t)b * cap + t], (uint32_t)((int64_t)cand[(size_t)b * cap + t] - id_base));
+  __syncthreads();
+  sort_and_write(keys, cnt, k, id_base, out_s + (size_t)b * k, out_i + (size_t)b * k);
+  if (threadIdx.x == 0) status[b] = total > cap ? -1 : total;
+}
+
+// ---------------------------------------------------------------------------
 // Merge G sorted per-shard lists: rank = own position + #greater keys in every
 // other list (binary search); ids are unique across shards so ranks are too.
 // ---------------------------------------------------------------------------
@@ -1821,6 +2042,11 @@ struct cbv2_index {
   // static split only.
   int* task_ring = nullptr;
   uint32_t task_seq = 0;
+  // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
+  // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
+  // max ||hi||); nullptr = plain bf16 index.
+  const uint8_t* resid = nullptr;
+  float resid_max = 0.0f, norm_max = 0.0f;
 };
 
 namespace {
@@ -1966,7 +2192,7 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
   return CBV2_OK;
 }
 
-template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32>
+template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -1974,7 +2200,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
   ScanSplit sp;
   const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC>), dim3((unsigned)(nq_groups * sp.n_chunks)),
                      dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, sp.chunk_docs,
                      sp.static_docs, sp.ctr, sp.task_docs, stamps);
   return launch_check("maxsim_scan16x4_kernel");
@@ -2159,6 +2385,76 @@ int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
                      cand, out_s, out_i);
   return launch_check("topk_select_kernel");
 }
+
+// ---------------------------------------------------------------------------
+// fp32-faithful path: workspace layout and the three operations.
+// ---------------------------------------------------------------------------
+struct F32Ws {
+  uint16_t* qhi = nullptr;
+  uint16_t* qlo = nullptr;
+  float* beta = nullptr;
+  int32_t* count = nullptr;
+  int32_t* cand = nullptr;
+  float* F = nullptr;
+  void* tk = nullptr;
+  size_t tk_bytes = 0;
+  float* T = nullptr;
+};
+
+// op SCORE: split queries; RERANK: + F [B][C]; SEARCH: + band [B][cap] + scan.
+size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8_t* base, F32Ws* w) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> uint8_t* {
+    uint8_t* p = base ? base + off : nullptr;
+    off += (bytes + 255) & ~(size_t)255;
+    return p;
+  };
+  const size_t qbytes = (size_t)B * lq * kDim * sizeof(uint16_t);
+  w->qhi = (uint16_t*)take(qbytes);
+  w->qlo = (uint16_t*)take(qbytes);
+  w->beta = (float*)take((size_t)B * sizeof(float));
+  if (op == CBV2_F32_RERANK) w->F = (float*)take((size_t)B * cap * sizeof(float));
+  if (op == CBV2_F32_SEARCH) {
+    w->count = (int32_t*)take((size_t)B * sizeof(int32_t));
+    w->cand = (int32_t*)take((size_t)B * cap * sizeof(int32_t));
+    w->F = (float*)take((size_t)B * cap * sizeof(float));
+    w->tk_bytes = topk_ws_bytes(B, ix->n);
+    w->tk = take(w->tk_bytes);
+    w->T = (float*)take((size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float));
+  }
+  return off;
+}
+
+int check_f32(cbv2_index* ix, int op, const float* Q, int32_t B, int32_t lq, int32_t cap, void* ws, size_t wsb,
+              F32Ws* w) {
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  if (ix->resid == nullptr) return fail(CBV2_ESTATE, "index has no fp32 residual (cbv2_index_attach_residual)");
+  CBV2_REQUIRE(Q != nullptr && aligned16(Q), "query pointer must be non-null and 16-byte aligned");
+  CBV2_REQUIRE(B >= 1 && B <= 65535, "B must be in [1, 65535] (got %d)", B);
+  CBV2_REQUIRE(lq >= 1 && lq <= kLqMax, "lq must be in [1, %d] (got %d)", kLqMax, lq);
+  const size_t need = f32_ws_layout(ix, op, B, lq, cap, nullptr, w);
+  CBV2_REQUIRE(ws != nullptr && wsb >= need && aligned16(ws), "workspace too small or misaligned (%zu < %zu)",
+               wsb, need);
+  f32_ws_layout(ix, op, B, lq, cap, (uint8_t*)ws, w);
+  return CBV2_OK;
+}
+
+int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st) {
+  hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(64), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
+                     ix->norm_max, w->beta);
+  return launch_check("split_query_kernel");
+}
+
+int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t* cand, const int32_t* count,
+                   int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st) {
+  if (limit <= 0) return CBV2_OK;
+  const int64_t per_wg = 4LL * kRsPerWave;
+  const int64_t gx = (limit + per_wg - 1) / per_wg;
+  if (gx > 0x7fffffffLL) return fail(CBV2_EUNSUPPORTED, "rescore grid too large");
+  hipLaunchKernelGGL(rescore_x3_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, st, ix->tokens, ix->resid,
+                     ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out);
+  return launch_check("rescore_x3_kernel");
+}
 }  // namespace
 
 extern "C" {
@@ -2333,6 +2629,113 @@ int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t
   CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
   hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, scores, ids, C, k,
                      out_scores, out_ids, out_pos);
+  return launch_check("select_small_kernel");
+}
+
+int cbv2_split_f32(const float* x, int64_t rows, int32_t ld, const int32_t* doclens, void* hi, void* lo,
+                   float* bounds, void* stream) {
+  CBV2_REQUIRE(rows >= 0, "rows must be >= 0");
+  CBV2_REQUIRE(doclens == nullptr || (ld >= 1 && rows % ld == 0), "with doclens, rows must be docs of ld rows");
+  if (rows == 0) return CBV2_OK;
+  CBV2_REQUIRE(x && hi && lo && bounds, "null pointer");
+  CBV2_REQUIRE(aligned16(x) && aligned16(hi) && aligned16(lo), "x, hi and lo must be 16-byte aligned");
+  const int64_t want = (rows * 16 + 255) / 256;
+  const unsigned grid = (unsigned)(want < 65536 ? want : 65536);  // grid-stride beyond
+  hipLaunchKernelGGL(split_f32_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, rows, ld, doclens,
+                     (uint16_t*)hi,
+                     (uint16_t*)lo, bounds);
+  return launch_check("split_f32_kernel");
+}
+
+int cbv2_index_attach_residual(cbv2_index* ix, const void* lo, float resid_max, float norm_max) {
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  CBV2_REQUIRE(ix->dtype == CBV2_DTYPE_BF16, "a residual attaches to a bf16 index");
+  CBV2_REQUIRE(ix->n == 0 || (lo != nullptr && aligned16(lo)), "residual must be non-null and 16-byte aligned");
+  CBV2_REQUIRE(resid_max >= 0.0f && norm_max >= 0.0f && resid_max < 3.0e38f && norm_max < 3.0e38f,
+               "bounds must be finite and >= 0");
+  ix->resid = (const uint8_t*)lo;
+  ix->resid_max = resid_max;
+  ix->norm_max = norm_max;
+  return CBV2_OK;
+}
+
+size_t cbv2_f32_workspace_bytes(const cbv2_index* ix, int32_t op, int32_t B, int32_t lq, int32_t cap) {
+  if (!ix || B < 1 || lq < 1 || cap < 0 || op < CBV2_F32_SCORE || op > CBV2_F32_RERANK) return 0;
+  F32Ws w;
+  return f32_ws_layout(ix, op, B, lq, cap, nullptr, &w);
+}
+
+int cbv2_score_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, void* ws, size_t wsb, float* out,
+                   int64_t ld_out, void* stream) {
+  F32Ws w;
+  int rc = check_f32(ix, CBV2_F32_SCORE, Q, B, lq, 0, ws, wsb, &w);
+  if (rc) return rc;
+  CBV2_REQUIRE(ix->n == 0 || out != nullptr, "null output");
+  CBV2_REQUIRE(ld_out >= ix->n, "ld_out (%lld) < n (%lld)", (long long)ld_out, (long long)ix->n);
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipStream_t st = (hipStream_t)stream;
+  if (ix->n == 0) return CBV2_OK;
+  rc = split_queries(ix, Q, B, lq, &w, st);
+  if (rc) return rc;
+  return launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, out, ld_out, st);
+}
+
+int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
+                    size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_status, void* stream) {
+  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(cap >= k && cap <= kBandCapMax, "cap must be in [k, %d] (got %d)", kBandCapMax, cap);
+  F32Ws w;
+  int rc = check_f32(ix, CBV2_F32_SEARCH, Q, B, lq, cap, ws, wsb, &w);
+  if (rc) return rc;
+  CBV2_REQUIRE(out_scores && out_ids && out_status, "null outputs");
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipStream_t st = (hipStream_t)stream;
+  if (ix->n == 0) {
+    CBV2_HIP(hipMemsetAsync(out_status, 0, (size_t)B * sizeof(int32_t), st));
+    return topk_impl_empty(B, k, out_scores, out_ids, st);
+  }
+  if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
+  // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
+  if ((rc = scan_maxsim(ix, w.qhi, B, lq, w.T, ix->n, st))) return rc;
+  if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
+    return rc;
+  // 2. band T >= T_k - 2 beta, 3. faithful rescoring, 4. exact top-k of the band
+  CBV2_HIP(hipMemsetAsync(w.count, 0, (size_t)B * sizeof(int32_t), st));
+  int64_t splits = (2LL * cu_count(ix->device) + B - 1) / B;
+  const int64_t max_splits = (ix->n + 4095) / 4096;
+  splits = splits < max_splits ? splits : max_splits;
+  splits = splits < 1 ? 1 : splits;
+  hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
+                     out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count);
+  if ((rc = launch_check("band_collect_kernel"))) return rc;
+  if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) return rc;
+  hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
+                     ix->id_base, out_scores, out_ids, out_status);
+  return launch_check("band_select_kernel");
+}
+
+int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C,
+                    int32_t k, void* ws, size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                    void* stream) {
+  CBV2_REQUIRE(cand != nullptr, "null candidates");
+  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
+  CBV2_REQUIRE(k >= 0 && k <= kTopkMax, "k must be in [0, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(out_scores != nullptr, "null out_scores");
+  CBV2_REQUIRE(k == 0 || out_ids != nullptr, "null out_ids");
+  F32Ws w;
+  int rc = check_f32(ix, CBV2_F32_RERANK, Q, B, lq, C, ws, wsb, &w);
+  if (rc) return rc;
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
+  float* raw = k == 0 ? out_scores : w.F;
+  if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
+  if (k == 0) return CBV2_OK;
+  hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
+                     out_pos);
   return launch_check("select_small_kernel");
 }
 

@@ -9,6 +9,7 @@ the MI355X scan kernel:
     tokens   bf16 [n, 128, 128]  (32 KiB per doc, rows >= doclen are padding)
     doclens  int32 [n]
     means    f32  [n, 128]       (optional: literal-reference scorer only)
+    residual bf16 [n, 128, 128]  (optional: fp32-faithful index, lo = bf16(x - tokens))
 
 All compute goes through libcolbert_mi355x.so (``_lib``); the tensors are
 owned here and borrowed by the C handle.
@@ -26,6 +27,7 @@ from . import _lib
 LD = 128
 DIM = 128
 LQ_MAX = 32
+BAND_CAP = 16384   # fp32-faithful search: largest band rescored per query
 
 
 def _stream_ptr(device: torch.device) -> int:
@@ -95,7 +97,8 @@ class ColbertIndex:
     ``scales`` uint8 E8M0 [n, 128, 2]; see ``ColbertIndex.mxfp8``)."""
 
     def __init__(self, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0,
-                 scales: Optional[torch.Tensor] = None):
+                 scales: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+                 bounds: Optional[Tuple[float, float]] = None):
         _require_cuda(tokens, "tokens")
         _require_cuda(doclens, "doclens")
         self.fp8 = tokens.dtype == torch.uint8
@@ -127,6 +130,49 @@ class ColbertIndex:
                 dev, self.tokens.data_ptr(), _lib.DTYPE_BF16, self.n, LD, DIM, self.doclens.data_ptr(),
                 self.id_base, ctypes.byref(h)))
         self._h = h
+        self.residual: Optional[torch.Tensor] = None
+        self.bounds: Optional[Tuple[float, float]] = None
+        if residual is not None:
+            if self.fp8 or residual.dtype != torch.bfloat16 or residual.shape != self.tokens.shape \
+                    or residual.device != self.device or bounds is None:
+                raise ValueError("a residual is bf16 [n, 128, 128] on the index device, with (resid_max, norm_max)")
+            self.residual = residual.contiguous()
+            self.bounds = (float(bounds[0]), float(bounds[1]))
+            _lib.check(_lib.lib().cbv2_index_attach_residual(self._h, self.residual.data_ptr(), self.bounds[0],
+                                                             self.bounds[1]))
+
+    @property
+    def faithful(self) -> bool:
+        """fp32-faithful index (built by ``ColbertIndex.faithful_f32``)."""
+        return self.residual is not None
+
+    @classmethod
+    def faithful_f32(cls, tokens_f32: torch.Tensor, doclens: torch.Tensor, id_base: int = 0) -> "ColbertIndex":
+        """Index fp32 [n, 128, 128] device tokens (as the reference stores them) so that
+        scores match fp32 arithmetic within ~1e-5: hi = bf16(x) is scanned, lo =
+        bf16(x - hi) is gathered for the candidates (cbv2_split_f32, HIP)."""
+        _require_cuda(tokens_f32, "tokens_f32")
+        if tokens_f32.dtype != torch.float32 or tokens_f32.dim() != 3 or tuple(tokens_f32.shape[1:]) != (LD, DIM):
+            raise ValueError(f"tokens_f32 must be f32 [n, {LD}, {DIM}] (got {tokens_f32.dtype} "
+                             f"{tuple(tokens_f32.shape)})")
+        x = tokens_f32.contiguous()
+        hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        lo = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        bounds = torch.zeros(2, dtype=torch.float32, device=x.device)
+        _require_cuda(doclens, "doclens")
+        if doclens.dtype != torch.int32 or doclens.shape != (x.shape[0],):
+            raise ValueError("doclens must be int32 [n]")
+        doclens = doclens.contiguous()
+        _lib.check(_lib.lib().cbv2_split_f32(x.data_ptr(), x.numel() // DIM, LD, doclens.data_ptr(), hi.data_ptr(),
+                                             lo.data_ptr(), bounds.data_ptr(), _stream_ptr(x.device)))
+        b = bounds.tolist()  # synchronises: x may be freed after this
+        return cls(hi, doclens, id_base=id_base, residual=lo, bounds=(b[0], b[1]))
+
+    def _f32_ws(self, op: int, B: int, lq: int, cap: int) -> torch.Tensor:
+        need = int(_lib.lib().cbv2_f32_workspace_bytes(self._h, op, B, lq, cap))
+        if self._ws is None or self._ws.numel() * 4 < need:
+            self._ws = torch.empty(((need + 3) // 4,), dtype=torch.float32, device=self.device)
+        return self._ws
 
     @classmethod
     def mxfp8(cls, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0) -> "ColbertIndex":
@@ -154,6 +200,8 @@ class ColbertIndex:
     # ----------------------------------------------------------------- native file
     def save(self, path: str) -> None:
         """Write this shard to the native index file (include/colbert_mi355x.h)."""
+        if self.faithful:
+            raise ValueError("the native file holds bf16/MXFP8 tokens; save an fp32-faithful index's fp32 source")
         dt = _lib.DTYPE_MXFP8 if self.fp8 else _lib.DTYPE_BF16
         torch.cuda.current_stream(self.device).synchronize()
         _lib.check(_lib.lib().cbv2_index_file_write(
@@ -221,6 +269,11 @@ class ColbertIndex:
             raise ValueError(f"queries must be [B, lq, {DIM}] (got {tuple(Q.shape)})")
         B, lq = int(Q.shape[0]), int(Q.shape[1])
         Q = Q.to(self.device)
+        if scorer == "maxsim" and self.faithful:
+            if lq > LQ_MAX:
+                raise ValueError(f"maxsim takes at most {LQ_MAX} query tokens (got {lq})")
+            Qd = Q.to(torch.float32).contiguous()
+            return Qd, Qd.data_ptr(), _lib.DTYPE_F32, B, lq
         if scorer == "maxsim" and self.fp8:
             if lq > LQ_MAX:
                 raise ValueError(f"maxsim takes at most {LQ_MAX} query tokens (got {lq})")
@@ -244,6 +297,11 @@ class ColbertIndex:
         sid = self._scorer(scorer)
         _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
         out = torch.empty((B, max(self.n, 1)), dtype=torch.float32, device=self.device)
+        if self.faithful and scorer == "maxsim":
+            ws = self._f32_ws(_lib.F32_SCORE, B, lq, 0)
+            _lib.check(_lib.lib().cbv2_score_f32(self._h, qptr, B, lq, ws.data_ptr(), ws.numel() * 4,
+                                                 out.data_ptr(), out.shape[1], _stream_ptr(self.device)))
+            return out[:, : self.n]
         _lib.check(_lib.lib().cbv2_score(self._h, sid, qptr, qdt, B, lq, out.data_ptr(),
                                          out.shape[1], _stream_ptr(self.device)))
         return out[:, : self.n]
@@ -252,6 +310,8 @@ class ColbertIndex:
         """Top-k over the shard: (f32 [B, k] scores, int32 [B, k] global ids), -inf/-1 padded."""
         sid = self._scorer(scorer)
         _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
+        if self.faithful and scorer == "maxsim":
+            return self._search_f32(_keep, B, lq, k)
         L = _lib.lib()
         need = int(L.cbv2_search_workspace_bytes(self._h, B))
         if self._ws is None or self._ws.numel() * 4 < need:
@@ -261,6 +321,25 @@ class ColbertIndex:
         _lib.check(L.cbv2_search(self._h, sid, qptr, qdt, B, lq, int(k), self._ws.data_ptr(),
                                  self._ws.numel() * 4, out_s.data_ptr(), out_i.data_ptr(),
                                  _stream_ptr(self.device)))
+        return out_s, out_i
+
+    def _search_f32(self, Qd: torch.Tensor, B: int, lq: int, k: int, cap: int = BAND_CAP):
+        """Faithful search (cbv2_search_f32); rows whose band overflowed ``cap``
+        (status -1) are recomputed exactly over the whole shard."""
+        cap = max(int(cap), int(k))
+        ws = self._f32_ws(_lib.F32_SEARCH, B, lq, cap)
+        out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+        out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        status = torch.empty((B,), dtype=torch.int32, device=self.device)
+        _lib.check(_lib.lib().cbv2_search_f32(self._h, Qd.data_ptr(), B, lq, int(k), cap, ws.data_ptr(),
+                                              ws.numel() * 4, out_s.data_ptr(), out_i.data_ptr(),
+                                              status.data_ptr(), _stream_ptr(self.device)))
+        self.last_band = status
+        bad = torch.nonzero(status < 0).flatten().tolist()
+        for b in bad:  # rare: the band was wider than cap
+            full = self.score(Qd[b: b + 1])
+            s1, i1 = topk_rows(full, k, id_base=self.id_base)
+            out_s[b], out_i[b] = s1[0], i1[0]
         return out_s, out_i
 
     def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
@@ -275,6 +354,16 @@ class ColbertIndex:
         B, C = int(cand.shape[0]), int(cand.shape[1])
         if Bq != B:
             raise ValueError(f"{Bq} queries but {B} candidate rows")
+        if self.faithful:
+            ws = self._f32_ws(_lib.F32_RERANK, B, lq, C)
+            out_s = torch.empty((B, C if k == 0 else k), dtype=torch.float32, device=self.device)
+            out_i = torch.empty((B, k), dtype=torch.int32, device=self.device) if k else None
+            out_p = torch.empty((B, k), dtype=torch.int32, device=self.device) if k else None
+            _lib.check(_lib.lib().cbv2_rerank_f32(
+                self._h, _keep.data_ptr(), B, lq, cand.data_ptr(), C, int(k), ws.data_ptr(), ws.numel() * 4,
+                out_s.data_ptr(), out_i.data_ptr() if k else None, out_p.data_ptr() if k else None,
+                _stream_ptr(self.device)))
+            return out_s if k == 0 else (out_s, out_i, out_p)
         if k == 0:
             out_s = torch.empty((B, C), dtype=torch.float32, device=self.device)
             _lib.check(_lib.lib().cbv2_rerank(self._h, qptr, B, lq, cand.data_ptr(), C, 0,

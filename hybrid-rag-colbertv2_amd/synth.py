@@ -51,17 +51,18 @@ def bm25_lists(B: int, n_total: int, planted: np.ndarray, k: int = 100, hits: in
 
 
 def make_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, device, seed: int = 0,
-               sigma: float = 0.1) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Docs [begin, end) of the synthetic corpus: (bf16 [n, 128, 128], int32 doclens [n]) on ``device``."""
+               sigma: float = 0.1, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Docs [begin, end) of the synthetic corpus: (``dtype`` [n, 128, 128], int32 doclens [n]) on ``device``
+    (bf16 = the fp32 draw rounded, so both dtypes describe the same corpus)."""
     n = end - begin
-    tokens = torch.empty((n, LD, DIM), dtype=torch.bfloat16, device=device)
+    tokens = torch.empty((n, LD, DIM), dtype=dtype, device=device)
     doclens = torch.full((n,), LD, dtype=torch.int32, device=device)
     c0, c1 = begin // CHUNK, (end + CHUNK - 1) // CHUNK
     for c in range(c0, c1):
         g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + c)
         x = _unit(torch.randn((CHUNK, LD, DIM), generator=g, device=device, dtype=torch.float32))
         lo, hi = max(begin, c * CHUNK), min(end, (c + 1) * CHUNK)
-        tokens[lo - begin: hi - begin] = x[lo - c * CHUNK: hi - c * CHUNK].to(torch.bfloat16)
+        tokens[lo - begin: hi - begin] = x[lo - c * CHUNK: hi - c * CHUNK].to(dtype)
         del x
     lq = Q.shape[1]
     flat = planted.reshape(-1)
@@ -73,7 +74,7 @@ def make_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, devic
         gen = torch.Generator().manual_seed(seed + 17)
         noise = torch.randn(len(flat), lq, DIM, generator=gen)[torch.from_numpy(mine)]
         docs = _unit(Q[torch.from_numpy(qb)] + sigma * _unit(noise))
-        tokens[torch.from_numpy(ids - begin).to(device), :lq] = docs.to(device=device, dtype=torch.bfloat16)
+        tokens[torch.from_numpy(ids - begin).to(device), :lq] = docs.to(device=device, dtype=dtype)
     return tokens, doclens
 
 

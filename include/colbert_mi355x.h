@@ -126,6 +126,49 @@ int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const i
                 int32_t C, int32_t k, float* out_scores, int32_t* out_ids, int32_t* out_pos,
                 void* stream);
 
+/* fp32-faithful index ---------------------------------------------------------
+ * The reference keeps fp32 embeddings (local_rag_complete.py:735-746: the
+ * encode output, torch.save'd as is) and scores them in fp32 (:802-831).  A
+ * bf16 index alone is within ~5e-3 of those scores; this mode returns scores
+ * within ~1e-5 and the top-k of those scores over the WHOLE corpus.
+ *  - cbv2_split_f32: x f32 [rows][128] -> hi = bf16(x) (RNE; the index
+ *    tokens) and lo = bf16(x - hi) (the residual), both bf16 [rows][128];
+ *    bounds f32[2] (DEVICE, zeroed by the caller) receive max ||x - hi||_2 and
+ *    max ||hi||_2 over the rows, rounded up (atomic max).  doclens (nullable,
+ *    device int32 [rows / ld]): rows are docs of ld rows and padding rows
+ *    (t >= doclens[doc]) are split but left out of the bounds.
+ *  - cbv2_index_attach_residual: a bf16 index built on hi borrows lo and
+ *    keeps the two bounds (host floats read back from cbv2_split_f32).
+ * Queries are f32 [B][lq][128] (lq <= 32); every call needs a workspace of
+ * cbv2_f32_workspace_bytes(index, op, B, lq, cap) bytes (16-B aligned), with
+ * cap = the band capacity (SEARCH) or C (RERANK), 0 for SCORE.
+ *  - cbv2_score_f32: faithful scores of every doc, out[b * ld_out + i]
+ *    (lo.qhi + hi.qlo + hi.qhi on the bf16 MFMA, fp32 accumulate).
+ *  - cbv2_search_f32: bf16 scan of hi (T), the k-th T of each query, then
+ *    every doc with T >= T_k - 2 beta(q) is rescored faithfully and the exact
+ *    top-k of that band is returned.  beta(q) bounds |T - S| for every doc
+ *    (Cauchy-Schwarz on the residuals of docs and query, plus accumulation
+ *    slack), so the band holds the faithful top-k of the whole corpus.
+ *    out_status int32 [B]: the band size (certified), or -1 when the band
+ *    exceeded `cap` (k <= cap <= 16384): that row is NOT certified; recompute
+ *    it with cbv2_score_f32 + cbv2_topk_rows.
+ *  - cbv2_rerank_f32: cbv2_rerank with faithful scores.                      */
+#define CBV2_F32_SCORE 0
+#define CBV2_F32_SEARCH 1
+#define CBV2_F32_RERANK 2
+int cbv2_split_f32(const float* x, int64_t rows, int32_t ld, const int32_t* doclens, void* hi, void* lo,
+                   float* bounds, void* stream);
+int cbv2_index_attach_residual(cbv2_index* index, const void* lo, float resid_max, float norm_max);
+size_t cbv2_f32_workspace_bytes(const cbv2_index* index, int32_t op, int32_t B, int32_t lq, int32_t cap);
+int cbv2_score_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, void* workspace,
+                   size_t workspace_bytes, float* out, int64_t ld_out, void* stream);
+int cbv2_search_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap,
+                    void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids,
+                    int32_t* out_status, void* stream);
+int cbv2_rerank_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, const int32_t* cand,
+                    int32_t C, int32_t k, void* workspace, size_t workspace_bytes, float* out_scores,
+                    int32_t* out_ids, int32_t* out_pos, void* stream);
+
 /* Selection -----------------------------------------------------------------
  * cbv2_select_topk — top-k of each row of a small score matrix (rows of
  * C <= 1024 entries: rerank after the cross-shard all-reduce).  ids (nullable)

@@ -17,6 +17,9 @@ reference line it follows (LRC = /root/reference/local_rag_complete.py):
   rrf               LRC:960-978 reciprocal rank fusion, float64, stable sort
   merge_topk        cross-shard merge (no reference counterpart; exact by the
                     same tie rule)
+  split_f32 /       the fp32-faithful index (LRC:735-746 keeps fp32 embeddings):
+  band_beta         hi/lo split and the bound |T - S| <= beta(q) the faithful
+                    search's band rests on
 
 Pinning: meanpool_cosine, rrf and the search/rerank
 dict pipeline are checked against golden vectors produced by the reference's
@@ -143,6 +146,37 @@ def meanpool_cosine(Q: np.ndarray, docs: np.ndarray, doclens: np.ndarray | None 
     dn = dmean / np.maximum(np.linalg.norm(dmean, axis=1, keepdims=True), eps)
     qn = qmean / np.maximum(np.linalg.norm(qmean, axis=1, keepdims=True), eps)
     return qn @ dn.T
+
+
+# ------------------------------------------------------------------ fp32-faithful index
+def split_f32(x: np.ndarray, doclens: np.ndarray | None = None):
+    """cbv2_split_f32: fp32 [N, L, D] -> (hi = bf16(x), lo = bf16(x - hi), (max ||x - hi||, max ||hi||)),
+    the maxima over the scoring rows (t < doclens[n])."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    hi = bf16_round(x)
+    r = x - hi                                      # exact in fp32
+    lo = bf16_round(r)
+    rn = np.linalg.norm(r.astype(np.float64), axis=-1)
+    hn = np.linalg.norm(hi.astype(np.float64), axis=-1)
+    if doclens is not None:
+        valid = np.arange(x.shape[1])[None, :] < np.asarray(doclens)[:, None]
+        rn, hn = rn[valid], hn[valid]
+    return hi, lo, (float(rn.max(initial=0.0)), float(hn.max(initial=0.0)))
+
+
+def band_beta(Q: np.ndarray, resid_max: float, norm_max: float, slack: float = 2.0 ** -12) -> np.ndarray:
+    """split_query_kernel's beta(q) (without its fp32 round-up):
+    sum_i ||q_i|| E + ||q_i - bf16(q_i)|| M + slack (||q_i|| + ||q_i - bf16(q_i)||) M.
+
+    For every doc, |maxsim(bf16 Q, hi) - maxsim(Q, x)| <= beta (Cauchy-Schwarz on
+    <q, x - hi> and <q - bf16(q), hi>; slack covers fp32/MFMA accumulation)."""
+    Q = np.asarray(Q, np.float32)
+    if Q.ndim == 2:
+        Q = Q[None]
+    q = Q.astype(np.float64)
+    nq = np.linalg.norm(q, axis=-1)
+    eq = np.linalg.norm(q - bf16_round(Q).astype(np.float64), axis=-1)
+    return (nq * resid_max + eq * norm_max + slack * (nq + eq) * norm_max).sum(axis=-1)
 
 
 # ------------------------------------------------------------------ selection

@@ -1,0 +1,138 @@
+"""GPU parity of the fp32-faithful index (cbv2_split_f32 / _score_f32 /
+_search_f32 / _rerank_f32) against the exact fp64 MaxSim of the fp32 values
+the reference stores (local_rag_complete.py:735-746, scored at :802-831).
+
+Tolerances (north_star: MaxSim within 1e-3 of fp32, ranks identical): faithful
+scores within 1e-4 of the fp64 oracle and within 1e-3 of the reference's own
+fp32 arithmetic; top-k ids identical wherever neighbouring oracle scores are
+more than 1e-4 apart.  The band certificate: every row status >= 0 (band size)
+on these inputs, and rows forced past the band cap fall back to the full
+faithful scan with identical results.
+"""
+import numpy as np
+import pytest
+import torch
+
+from hybrid_rag_colbertv2_amd import _lib
+from hybrid_rag_colbertv2_amd.index import ColbertIndex
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+
+
+def rand_unit(g, *shape):
+    x = torch.randn(*shape, generator=g)
+    return x / x.norm(dim=-1, keepdim=True)
+
+
+def make_case(seed, N, B, lq, ragged=True, planted=True):
+    g = torch.Generator().manual_seed(seed)
+    docs = rand_unit(g, N, 128, 128)
+    doclens = torch.randint(1, 129, (N,), generator=g, dtype=torch.int32) if ragged \
+        else torch.full((N,), 128, dtype=torch.int32)
+    Q = rand_unit(g, B, lq, 128)
+    if planted:
+        for b in range(B):
+            for j in range(3):
+                d = (97 * b + 31 * j) % N
+                docs[d, :lq] = Q[b] + 0.2 * rand_unit(g, lq, 128)
+                doclens[d] = 128
+    return docs, doclens, Q
+
+
+def assert_ids_match_separated(ids, ref_ids, ref_scores, gap=ATOL):
+    for b in range(ids.shape[0]):
+        s = ref_scores[b]
+        for j in range(ids.shape[1]):
+            lo = s[j - 1] - s[j] if j > 0 else np.inf
+            hi = s[j] - s[j + 1] if j + 1 < len(s) else np.inf
+            if min(lo, hi) > gap:
+                assert ids[b, j] == ref_ids[b, j], (b, j, ids[b, j], ref_ids[b, j])
+
+
+def test_split_matches_oracle(dev):
+    docs, doclens, _ = make_case(1, 300, 2, 32)
+    docs[5, 100:] = 1e6            # garbage padding: split, but outside the bounds
+    doclens[5] = 100
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    hi, lo, (E, M) = orc.split_f32(docs.numpy(), doclens.numpy())
+    np.testing.assert_array_equal(ix.tokens.float().cpu().numpy(), hi)
+    np.testing.assert_array_equal(ix.residual.float().cpu().numpy(), lo)
+    assert E <= ix.bounds[0] <= E * (1 + 2 ** -9) and M <= ix.bounds[1] <= M * (1 + 2 ** -9)
+
+
+@pytest.mark.parametrize("N,B,lq", [(1, 1, 32), (257, 3, 32), (2000, 9, 20)])
+def test_score_f32(dev, N, B, lq):
+    docs, doclens, Q = make_case(N + B, N, B, lq)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    got = ix.score(Q.to(dev)).cpu().numpy()
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    ref32 = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy(), dtype=np.float32)
+    np.testing.assert_allclose(got, exact, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(got, ref32, atol=1e-3, rtol=0)
+
+
+def test_faithful_beats_bf16_on_fp32_inputs(dev):
+    docs, doclens, Q = make_case(7, 3000, 8, 32)
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    fx = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    bx = ColbertIndex(docs.bfloat16().to(dev), doclens.to(dev))
+    e_f = np.abs(fx.score(Q.to(dev)).cpu().numpy() - exact).max()
+    e_b = np.abs(bx.score(Q.bfloat16().to(dev)).cpu().numpy() - exact).max()
+    assert e_f < ATOL < e_b, (e_f, e_b)
+
+
+@pytest.mark.parametrize("N,B,k", [(5, 2, 10), (3000, 7, 100), (70000, 3, 100)])
+def test_search_f32_certified(dev, N, B, k):
+    docs, doclens, Q = make_case(N * 3 + k, N, B, 32)
+    doclens[::11] = 0                                   # empty docs score -inf
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=1000)
+    s, i = ix.search(Q.to(dev), k)
+    status = ix.last_band.cpu().numpy()
+    assert (status >= 0).all(), status
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    rs, ri = orc.topk(exact, k, id_base=1000)
+    fin = np.isfinite(rs)
+    np.testing.assert_allclose(s.cpu().numpy()[fin], rs[fin], atol=ATOL, rtol=0)
+    assert_ids_match_separated(i.cpu().numpy(), ri, rs)
+
+
+def test_search_f32_overflow_falls_back(dev):
+    docs, doclens, Q = make_case(9, 4000, 4, 32)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    s_full, i_full = ix.search(Q.to(dev), 20)
+    assert (ix.last_band >= 0).all()
+    s_cap, i_cap = ix._search_f32(Q.to(dev).contiguous(), 4, 32, 20, cap=20)   # band > 20 -> status -1
+    assert (ix.last_band < 0).any()
+    torch.testing.assert_close(s_cap, s_full, atol=0, rtol=0)
+    assert torch.equal(i_cap, i_full)
+
+
+def test_rerank_f32(dev):
+    docs, doclens, Q = make_case(13, 900, 5, 32)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=50)
+    g = torch.Generator().manual_seed(3)
+    cand = torch.randint(40, 960, (5, 50), generator=g, dtype=torch.int32)   # some out of shard
+    s, i, p = ix.rerank(Q.to(dev), cand.to(dev), 10)
+    rs, ri, rp = orc.rerank(Q.numpy(), docs.numpy(), doclens.numpy(), cand.numpy(), 10, id_base=50)
+    np.testing.assert_allclose(s.cpu().numpy(), rs, atol=ATOL, rtol=0)
+    assert_ids_match_separated(i.cpu().numpy(), ri, rs)
+    raw = ix.rerank(Q.to(dev), cand.to(dev), 0).cpu().numpy()
+    assert raw.shape == (5, 50)
+
+
+def test_f32_abi_validation(dev):
+    docs, doclens, Q = make_case(2, 10, 1, 32)
+    bx = ColbertIndex(docs.bfloat16().to(dev), doclens.to(dev))
+    L = _lib.lib()
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    out = torch.empty((1, 10), device=dev)
+    q = Q.to(dev).contiguous()
+    assert L.cbv2_score_f32(bx._h, q.data_ptr(), 1, 32, ws.data_ptr(), ws.numel(), out.data_ptr(), 10,
+                            None) == _lib.ERR_ESTATE
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    assert L.cbv2_score_f32(ix._h, q.data_ptr(), 1, 33, ws.data_ptr(), ws.numel(), out.data_ptr(), 10,
+                            None) == _lib.ERR_EINVAL
+    assert L.cbv2_score_f32(ix._h, q.data_ptr(), 1, 32, ws.data_ptr(), 16, out.data_ptr(), 10,
+                            None) == _lib.ERR_EINVAL

@@ -312,6 +312,12 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   //   kind 0 = production (64-token iterations, 2-deep ring: 142.5 -> 139.1 ms
   //   at 1M vs 32-token iterations with a 3-deep ring, which is kind 1)
   if (kind == 1) return launch_scan16x4<8, 4, 1, 2, 3, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  // kinds 2-5: one wave per SIMD (4 waves x 8 queries, 512-register budget):
+  // half the ds_read bytes per MFMA (each doc fragment feeds 16 chains)
+  if (kind == 2) return launch_scan16x4<4, 8, 1, 2, 3, false, 32, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 3) return launch_scan16x4<4, 8, 1, 2, 2, false, 64, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 4) return launch_scan16x4<4, 8, 1, 3, 3, false, 32, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 5) return launch_scan16x4<4, 8, 1, 1, 3, false, 32, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
