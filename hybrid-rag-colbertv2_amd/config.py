@@ -14,7 +14,9 @@ Added fields (no reference counterpart):
   * ``fused_candidates`` — the ``[:50]`` hard-coded at local_rag_complete.py:916.
   * ``rrf_k``          — the ``k=60`` default at local_rag_complete.py:964.
   * ``doc_maxlen`` / ``query_maxlen`` / ``dim`` — index geometry.
-  * ``index_dtype``    — "bf16" (fp8 is a later row of SURVEY §8).
+  * ``index_dtype``    — "bf16" (default), "fp8" (MXFP8, config 5) or "fp32"
+                          (fp32-faithful: the reference's fp32 scores within
+                          ~1e-5 and their exact top-k).
 """
 from dataclasses import dataclass
 

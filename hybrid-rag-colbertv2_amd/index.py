@@ -40,8 +40,8 @@ def _require_cuda(t: torch.Tensor, name: str):
 
 
 def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
-                ld: int = LD) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Token matrices -> (bf16 [n, ld, 128] padded with zeros, int32 doclens [n]).
+                ld: int = LD, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Token matrices -> (``dtype`` [n, ld, 128] padded with zeros, int32 doclens [n]).
 
     Accepts a dense ``[n, L, D]`` tensor (every doc has L tokens, as the
     reference's stacked encode output), a pooled ``[n, D]`` tensor (one token
@@ -55,19 +55,19 @@ def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
         n, L, D = embs.shape
         if D != DIM or L > ld:
             raise ValueError(f"doc embeddings must be [n, L<={ld}, {DIM}] (got {tuple(embs.shape)})")
-        tokens = torch.zeros((n, ld, DIM), dtype=torch.bfloat16, device=device)
-        tokens[:, :L] = embs.to(device=device, dtype=torch.bfloat16)
+        tokens = torch.zeros((n, ld, DIM), dtype=dtype, device=device)
+        tokens[:, :L] = embs.to(device=device, dtype=dtype)
         doclens = torch.full((n,), L, dtype=torch.int32, device=device)
         return tokens, doclens
     embs = list(embs)
     n = len(embs)
-    tokens = torch.zeros((n, ld, DIM), dtype=torch.bfloat16, device=device)
+    tokens = torch.zeros((n, ld, DIM), dtype=dtype, device=device)
     lens = []
     for i, e in enumerate(embs):
         e = e if e.dim() == 2 else e.unsqueeze(0)
         if e.shape[-1] != DIM or e.shape[0] > ld:
             raise ValueError(f"doc {i}: expected [L<={ld}, {DIM}] tokens, got {tuple(e.shape)}")
-        tokens[i, : e.shape[0]] = e.to(device=device, dtype=torch.bfloat16)
+        tokens[i, : e.shape[0]] = e.to(device=device, dtype=dtype)
         lens.append(e.shape[0])
     doclens = torch.tensor(lens, dtype=torch.int32, device=device)
     return tokens, doclens
@@ -181,10 +181,21 @@ class ColbertIndex:
         return cls(q, doclens, id_base=id_base, scales=sc)
 
     @classmethod
-    def from_embeddings(cls, embs, device="cuda", id_base: int = 0, build_means: bool = False):
+    def from_embeddings(cls, embs, device="cuda", id_base: int = 0, build_means: bool = False,
+                        dtype: str = "bf16"):
+        """Index encoder output.  dtype: "bf16" (default), "fp8" (MXFP8, HIP
+        quantizer) or "fp32" (fp32-faithful: scores as fp32 arithmetic gives them)."""
         device = torch.device(device)
-        tokens, doclens = pack_tokens(embs, device)
-        ix = cls(tokens, doclens, id_base=id_base)
+        if dtype not in ("bf16", "fp8", "fp32"):
+            raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
+        tokens, doclens = pack_tokens(embs, device, dtype=torch.float32 if dtype == "fp32" else torch.bfloat16)
+        if dtype == "fp32":
+            ix = cls.faithful_f32(tokens, doclens, id_base=id_base)
+        elif dtype == "fp8":
+            ix = cls.mxfp8(tokens, doclens, id_base=id_base)
+        else:
+            ix = cls(tokens, doclens, id_base=id_base)
+        del tokens
         if build_means:
             if isinstance(embs, torch.Tensor):
                 f32 = embs if embs.dim() == 3 else embs.unsqueeze(1)

@@ -49,7 +49,8 @@ class JinaColBERTRetriever:
     # ------------------------------------------------------------ index / load
     def _build(self, embeddings) -> ColbertIndex:
         return ColbertIndex.from_embeddings(embeddings, device=self.device,
-                                            build_means=(self.scorer == "ref_meanpool_cosine"))
+                                            build_means=(self.scorer == "ref_meanpool_cosine"),
+                                            dtype=getattr(self.config, "index_dtype", "bf16"))
 
     def index(self, corpus: List[str]) -> None:
         """LRC:728-746: encode the corpus, keep it in HBM, save index.pt."""

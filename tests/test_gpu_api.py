@@ -31,9 +31,9 @@ class RecordedBM25:
         return np.array([bm["ids"][:k]]), np.array([bm["scores"][:k]])
 
 
-def _system(tmp_path, scorer):
+def _system(tmp_path, scorer, index_dtype="bf16"):
     cfg = RAGConfig(scorer=scorer, colbert_index_path=str(tmp_path / "colbert"),
-                    bm25_index_path=str(tmp_path / "bm25"))
+                    bm25_index_path=str(tmp_path / "bm25"), index_dtype=index_dtype)
     ind = DualIndexer(cfg, encoder=FakeEncoder(**TOY["encoder"]))
     ind.colbert_retriever.index(TOY["corpus"])
     ind.bm25_retriever = RecordedBM25()
@@ -94,6 +94,28 @@ def test_maxsim_pipeline_matches_oracle(dev, tmp_path):
         fin = hyb.retrieve(q)
         assert [f["chunk_id"] for f in fin] == [cand[p] for p, _, _ in order]
         assert [f["rank"] for f in fin] == list(range(1, len(fin) + 1))
+
+
+def test_fp32_index_pipeline_matches_exact_fp32(dev, tmp_path):
+    """index_dtype="fp32": search / rerank / retrieve on the encoder's fp32
+    values themselves (no bf16 rounding), scores within 1e-4 of fp64."""
+    cfg, ind, hyb = _system(tmp_path, "maxsim", index_dtype="fp32")
+    assert ind.colbert_retriever.corpus_embeddings.faithful
+    enc = FakeEncoder(**TOY["encoder"])
+    docs = np.asarray(enc.encode(TOY["corpus"], convert_to_tensor=False), np.float32)
+    for i, q in enumerate(TOY["queries"]):
+        qe = np.asarray(enc.encode(q, convert_to_tensor=False), np.float32)
+        s = orc.maxsim(qe, docs)
+        es, ei = orc.topk(s, 10)
+        got = ind.colbert_retriever.search(q, k=10)
+        assert [g["document_id"] for g in got] == list(ei[0])
+        np.testing.assert_allclose([g["score"] for g in got], es[0], atol=1e-4)
+        fused = orc.rrf(TOY["bm25"][i]["ids"], list(orc.topk(s, 100)[1][0]))[:50]
+        cand = [c for c, _ in fused]
+        order = orc.rerank_select(s[0, cand], 10)
+        fin = hyb.retrieve(q)
+        assert [f["chunk_id"] for f in fin] == [cand[p] for p, _, _ in order]
+        np.testing.assert_allclose([f["score"] for f in fin], [sc for _, sc, _ in order], atol=1e-4)
 
 
 def test_index_save_load_roundtrip_and_reference_format(dev, tmp_path):
