@@ -1436,10 +1436,12 @@ __device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, f
 __global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __restrict__ scores, int64_t n,
                                                                int64_t ld, int k, int64_t id_base,
                                                                float* __restrict__ out_s,
-                                                               int32_t* __restrict__ out_i) {
+                                                               int32_t* __restrict__ out_i,
+                                                               const int32_t* __restrict__ only_neg = nullptr) {
   __shared__ uint32_t hist[2048];
   __shared__ uint64_t sel[kTopkMax];
   __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+  if (only_neg != nullptr && only_neg[blockIdx.x] >= 0) return;  // block-uniform: rows flagged < 0 only
   const float* x = scores + (size_t)blockIdx.x * ld;
   const int kk = (int)((int64_t)k < n ? k : n);
   topk_exact_row(x, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
@@ -1803,27 +1805,32 @@ __device__ __forceinline__ void tile16_x3(const bf16x8 (&ah)[4], const bf16x8 (&
 }
 
 // Faithful rescoring: query b = blockIdx.y against candidates c (cand == null:
-// c is the local doc index), each wave kRsPerWave candidates; out[b*ld_out + c].
-// count (nullable) bounds c per query (the band collected by the search).
+// c is the local doc index), kRsPerWave consecutive candidates per wave step,
+// grid-stride over blockIdx.x; out[b*ld_out + c].  count (nullable) bounds c
+// per query (the band collected by the search); only_neg (nullable) skips
+// every query whose status is >= 0 (the search's full-scan fallback).
 constexpr int kRsPerWave = 4;
 __global__ __launch_bounds__(256) void rescore_x3_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
-    float* __restrict__ out, int64_t ld_out) {
+    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg) {
   const int lane = threadIdx.x & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
+  if (only_neg != nullptr && only_neg[b] >= 0) return;  // block-uniform; no block-level sync below
   int64_t lim = limit;
   if (count != nullptr) {
     const int64_t cb = count[b];
     lim = cb < lim ? cb : lim;
   }
-  const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * kRsPerWave;
-  if (c0 >= lim) return;  // wave-uniform; no block-level sync below
+  const int64_t step = (int64_t)gridDim.x * 4 * kRsPerWave;
+  int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * kRsPerWave;
+  if (c0 >= lim) return;  // wave-uniform
   bf16x8 qh[2][4], ql[2][4];
   load_qfrag16(qhi, b, b + 1, lq, lane, qh);
   load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+  for (; c0 < lim; c0 += step)
   for (int64_t c = c0; c < c0 + kRsPerWave && c < lim; ++c) {
     const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
     const int64_t loc = id - id_base;
@@ -1862,27 +1869,59 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
 
 // Band collect: row b of the bf16 scan's scores T; every doc with T >= T_k -
 // 2 beta(b) is appended (global id) to cand[b][0..cap); count[b] = the band
-// size (may exceed cap: the search then reports the row as not certified).
+// size (may exceed cap: the search then recomputes that row in full).  Hits
+// gather in an LDS list (LDS atomics; the global counter of a row is hit by
+// one atomic per workgroup, not one per wave hit), flushed once at the end.
+constexpr int kBandLds = 2048;
 __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restrict__ T, int64_t n,
                                                            const float* __restrict__ topk_s, int k,
                                                            const float* __restrict__ beta, int64_t id_base,
                                                            int cap, int32_t* __restrict__ cand,
                                                            int32_t* __restrict__ count) {
+  __shared__ int32_t s_ids[kBandLds];
+  __shared__ int s_n, s_base;
   const int b = blockIdx.y, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
   const float thr = topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b];
   const float* row = T + (size_t)b * n;
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += step) {  // uniform trip count per wave
-    const int64_t i = i0 + threadIdx.x;
-    const bool take = i < n && row[i] >= thr;
-    const uint64_t mask = __ballot(take);
-    if (mask == 0) continue;
-    int base = 0;
-    if (lane == 0) base = atomicAdd(count + b, __popcll(mask));
-    base = __shfl(base, 0);
-    const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-    if (take && pos < cap) cand[(size_t)b * cap + pos] = (int32_t)(id_base + i);
+  int32_t* crow = cand + (size_t)b * cap;
+  constexpr int U = 8;  // 8 coalesced loads in flight per thread, then the ballots
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * U;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U; i0 < n; i0 += step) {  // uniform trip count per wave
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x + threadIdx.x;
+      v[u] = i < n ? row[i] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x + threadIdx.x;
+      const bool take = i < n && v[u] >= thr;
+      const uint64_t mask = __ballot(take);
+      if (mask == 0) continue;
+      const int nh = __popcll(mask);
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&s_n, nh);
+      base = __shfl(base, 0);
+      const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+      if (take) {
+        if (pos < kBandLds) {
+          s_ids[pos] = (int32_t)(id_base + i);
+        } else {  // LDS list full (a very wide band): straight to the global list
+          const int gp = atomicAdd(count + b, 1);
+          if (gp < cap) crow[gp] = (int32_t)(id_base + i);
+        }
+      }
+    }
   }
+  __syncthreads();
+  const int nl = s_n < kBandLds ? s_n : kBandLds;
+  if (threadIdx.x == 0) s_base = nl > 0 ? atomicAdd(count + b, nl) : 0;
+  __syncthreads();
+  for (int t = threadIdx.x; t < nl; t += blockDim.x)
+    if (s_base + t < cap) crow[s_base + t] = s_ids[t];
 }
 
 // Band select: exact top-k of the rescored band (score desc, id asc);
@@ -2367,7 +2406,7 @@ int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   const size_t need = topk_ws_bytes(B, n);
   if (need == 0 || ws == nullptr || ws_bytes < need || B > 65535) {  // grid.y of the filter launch
     hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
-                       out_s, out_i);
+                       out_s, out_i, nullptr);
     return launch_check("topk_rows_kernel");
   }
   uint64_t* cand = (uint64_t*)ws;
@@ -2446,13 +2485,17 @@ int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipSt
 }
 
 int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t* cand, const int32_t* count,
-                   int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st) {
+                   int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
+                   const int32_t* only_neg = nullptr) {
   if (limit <= 0) return CBV2_OK;
   const int64_t per_wg = 4LL * kRsPerWave;
-  const int64_t gx = (limit + per_wg - 1) / per_wg;
-  if (gx > 0x7fffffffLL) return fail(CBV2_EUNSUPPORTED, "rescore grid too large");
+  int64_t gx = (limit + per_wg - 1) / per_wg;
+  // at most 1024 workgroups per row (4096 waves: a lone fallback row still
+  // streams at full rate), grid-stride beyond; rows that skip exit at once
+  gx = gx < 1024 ? gx : 1024;
   hipLaunchKernelGGL(rescore_x3_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, st, ix->tokens, ix->resid,
-                     ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out);
+                     ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out,
+                     only_neg);
   return launch_check("rescore_x3_kernel");
 }
 }  // namespace
@@ -2703,8 +2746,8 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
     return rc;
   // 2. band T >= T_k - 2 beta, 3. faithful rescoring, 4. exact top-k of the band
   CBV2_HIP(hipMemsetAsync(w.count, 0, (size_t)B * sizeof(int32_t), st));
-  int64_t splits = (2LL * cu_count(ix->device) + B - 1) / B;
-  const int64_t max_splits = (ix->n + 4095) / 4096;
+  int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
+  const int64_t max_splits = (ix->n + 8191) / 8192;
   splits = splits < max_splits ? splits : max_splits;
   splits = splits < 1 ? 1 : splits;
   hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
@@ -2713,7 +2756,13 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) return rc;
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
                      ix->id_base, out_scores, out_ids, out_status);
-  return launch_check("band_select_kernel");
+  if ((rc = launch_check("band_select_kernel"))) return rc;
+  // 5. rows whose band overflowed cap (status -1): the full faithful scan over
+  //    every doc and an exact top-k, on the device (other rows exit at once)
+  if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st, out_status))) return rc;
+  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.T, ix->n, ix->n, k, ix->id_base,
+                     out_scores, out_ids, out_status);
+  return launch_check("topk_rows_kernel");
 }
 
 int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C,

@@ -335,8 +335,9 @@ class ColbertIndex:
         return out_s, out_i
 
     def _search_f32(self, Qd: torch.Tensor, B: int, lq: int, k: int, cap: int = BAND_CAP):
-        """Faithful search (cbv2_search_f32); rows whose band overflowed ``cap``
-        (status -1) are recomputed exactly over the whole shard."""
+        """Faithful search (cbv2_search_f32, asynchronous): rows whose band
+        overflowed ``cap`` (``last_band`` -1) are recomputed on the device by
+        the full faithful scan; ``last_band`` holds each row's band size."""
         cap = max(int(cap), int(k))
         ws = self._f32_ws(_lib.F32_SEARCH, B, lq, cap)
         out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
@@ -346,11 +347,6 @@ class ColbertIndex:
                                               ws.numel() * 4, out_s.data_ptr(), out_i.data_ptr(),
                                               status.data_ptr(), _stream_ptr(self.device)))
         self.last_band = status
-        bad = torch.nonzero(status < 0).flatten().tolist()
-        for b in bad:  # rare: the band was wider than cap
-            full = self.score(Qd[b: b + 1])
-            s1, i1 = topk_rows(full, k, id_base=self.id_base)
-            out_s[b], out_i[b] = s1[0], i1[0]
         return out_s, out_i
 
     def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):

@@ -149,9 +149,11 @@ int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const i
  *    top-k of that band is returned.  beta(q) bounds |T - S| for every doc
  *    (Cauchy-Schwarz on the residuals of docs and query, plus accumulation
  *    slack), so the band holds the faithful top-k of the whole corpus.
- *    out_status int32 [B]: the band size (certified), or -1 when the band
- *    exceeded `cap` (k <= cap <= 16384): that row is NOT certified; recompute
- *    it with cbv2_score_f32 + cbv2_topk_rows.
+ *    out_status int32 [B]: the band size, or -1 when the band exceeded `cap`
+ *    (k <= cap <= 16384): that row was then recomputed on the device by the
+ *    full faithful scan (cbv2_score_f32's arithmetic) and an exact top-k.
+ *    Either way the result is the faithful top-k of the whole corpus; the
+ *    call stays asynchronous (no host round trip).
  *  - cbv2_rerank_f32: cbv2_rerank with faithful scores.                      */
 #define CBV2_F32_SCORE 0
 #define CBV2_F32_SEARCH 1
