@@ -100,7 +100,8 @@ def main():
     ap.add_argument("--native-exchange", action="store_true",
                     help="N>1: run the all-gather / all-reduce inside the C ABI (cbv2_*_sharded) on torch's RCCL comm")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
-                    help="index tokens: bf16 (config 3) or MXFP8 e4m3 + E8M0 (config 5)")
+                    help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
+                         "(bf16 hi scanned + residual-certified band, DESIGN 3.12)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

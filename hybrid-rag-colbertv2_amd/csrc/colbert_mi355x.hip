@@ -2360,6 +2360,8 @@ int check_query(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   CBV2_REQUIRE(lq >= 1, "lq must be >= 1 (got %d)", lq);
   CBV2_REQUIRE(aligned16(Q), "query pointer must be 16-byte aligned");
   if (scorer == CBV2_SCORER_MAXSIM) {
+    if (ix->resid != nullptr && q_dtype == CBV2_DTYPE_F32)
+      return fail(CBV2_EINVAL, "f32 queries on an fp32-faithful index go through cbv2_score_f32/_search_f32/_rerank_f32");
     if (ix->dtype == CBV2_DTYPE_MXFP8)
       CBV2_REQUIRE(q_dtype == CBV2_DTYPE_MXFP8, "an MXFP8 index takes MXFP8 queries (cbv2_quantize_mxfp8)");
     else

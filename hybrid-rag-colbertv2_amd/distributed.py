@@ -94,6 +94,9 @@ class NativeExchange:
         import os
 
         from . import _lib
+        if getattr(index, "faithful", False):
+            raise ValueError("the native exchange scans bf16/MXFP8 shards; an fp32-faithful shard uses the "
+                             "torch.distributed exchange (ShardedSearcher(native=False))")
         self.index, self.dev, self.lexical_k = index, index.device, int(lexical_k)
         pg = group if group is not None else dist.distributed_c10d._get_default_group()
         if dist.get_backend(pg) != "nccl":

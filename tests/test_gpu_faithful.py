@@ -136,3 +136,16 @@ def test_f32_abi_validation(dev):
                             None) == _lib.ERR_EINVAL
     assert L.cbv2_score_f32(ix._h, q.data_ptr(), 1, 32, ws.data_ptr(), 16, out.data_ptr(), 10,
                             None) == _lib.ERR_EINVAL
+
+
+def test_faithful_shards_merge_equal_unsharded(dev):
+    """Per-shard faithful top-k lists + the HIP merge == the unsharded faithful
+    search (what each rank of the torch.distributed exchange returns)."""
+    from hybrid_rag_colbertv2_amd.index import merge_topk
+    docs, doclens, Q = make_case(21, 5000, 6, 32)
+    full = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    fs, fi = full.search(Q.to(dev), 50)
+    parts = [ColbertIndex.faithful_f32(docs[a:b].to(dev), doclens[a:b].to(dev), id_base=a).search(Q.to(dev), 50)
+             for a, b in ((0, 1800), (1800, 5000))]
+    ms, mi = merge_topk(torch.stack([p[0] for p in parts]), torch.stack([p[1] for p in parts]), 50)
+    assert torch.equal(mi, fi) and torch.equal(ms, fs)
