@@ -312,12 +312,14 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   //   kind 0 = production (64-token iterations, 2-deep ring: 142.5 -> 139.1 ms
   //   at 1M vs 32-token iterations with a 3-deep ring, which is kind 1)
   if (kind == 1) return launch_scan16x4<8, 4, 1, 2, 3, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
-  // kinds 2-5: one wave per SIMD (4 waves x 8 queries, 512-register budget):
-  // half the ds_read bytes per MFMA (each doc fragment feeds 16 chains)
-  if (kind == 2) return launch_scan16x4<4, 8, 1, 2, 3, false, 32, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
-  if (kind == 3) return launch_scan16x4<4, 8, 1, 2, 2, false, 64, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
-  if (kind == 4) return launch_scan16x4<4, 8, 1, 3, 3, false, 32, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
-  if (kind == 5) return launch_scan16x4<4, 8, 1, 1, 3, false, 32, 1>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  // (kinds 2-5, round 1: one wave per SIMD, 4 waves x 8 queries, 163 vs 142 ms: removed)
+  // mid-batch shapes (B = 16 / 64): 6 = production 4-wave x 4 queries (2 WGs/CU, 32-token ring),
+  // 7 = 8 waves x 2 queries (one WG/CU, 64-token ring), 8 = 4 x 4 with 64-token iterations,
+  // 9 = 8 waves x 2 queries, 32-token 3-deep ring
+  if (kind == 6) return launch_scan16x4<4, 4, 2, 2, 2, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 7) return launch_scan16x4<8, 2, 1, 2, 2, false, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 8) return launch_scan16x4<4, 4, 2, 2, 2, false, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 9) return launch_scan16x4<8, 2, 1, 2, 3, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
