@@ -1038,7 +1038,12 @@ __device__ __forceinline__ void lds_afrag_f8x4(const uint8_t* buf, int t, int la
   as = buf[4 * TPI * kDim + R * 2 + (g & 1)];
 }
 
-template <int QW, int D, int TPI = 32>
+// PF (prefetch-after-first-MFMA): tile t+1's LDS reads issue after tile t's
+// first MFMA, so the lgkmcnt wait that tile t's fragments need does not also
+// wait for them (hipcc waits lgkmcnt(0) there), and the fold of chain k-D is
+// fenced after MFMA k (hipcc otherwise hoists the fold above it and pads the
+// MFMA -> VALU hazard with s_nop).
+template <int QW, int D, int TPI = 32, bool PF = false>
 __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, const i32x8 (&qa)[QW][2],
                                                const int (&qs)[QW][2], float (&m)[QW][2]) {
   constexpr int NC = 2 * QW;
@@ -1059,9 +1064,13 @@ __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, con
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc) {
       const int k = t * NC + cc;
-      if (cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
+      if (!PF && cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
       acc[k % (D + 1)] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
           a[t & 1], qa[cc >> 1][cc & 1], f32x4{}, 0, 0, 0, as[t & 1], 0, qs[cc >> 1][cc & 1]);
+      if constexpr (PF) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
+      }
       if (k >= D) fold(k - D);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1088,7 +1097,7 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
   }
 }
 
-template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32>   // D = 2 spills at QW = 8 (hipcc 7.2)
+template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false>   // D = 2 spills at QW = 8
 __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1198,7 +1207,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
       for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     }
     if (TPI * j + TPI <= dl_min)
-      iter_f8x4_full<QW, D, TPI>(buf, lane, qa, qs, m);
+      iter_f8x4_full<QW, D, TPI, PF>(buf, lane, qa, qs, m);
     else if (TPI * j < dl_max)
       iter_f8x4_ragged<QW, TPI>(buf, lane, j, dl_g, dl_max, qa, qs, m);
     if (j == IPG - 1) {
@@ -2303,7 +2312,7 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
 constexpr int kF8DirectMaxB = 8;
 constexpr int kF8Waves = 8, kF8QW = 8;
 
-template <int TPI, int NBUF>
+template <int TPI, int NBUF, bool PF = false>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs) {
   constexpr int QPB = kF8Waves * kF8QW;
@@ -2311,7 +2320,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
   ScanSplit sp;
   const int rc = plan_split(ix, nq_groups, cu_count(ix->device), dyn_frac, task_docs, st, &sp);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW, 1, NBUF, TPI>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW, 1, NBUF, TPI, PF>), dim3((unsigned)(nq_groups * sp.n_chunks)),
                      dim3(kF8Waves * 64), 0, st, ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out,
                      ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs);
   return launch_check("maxsim_scan_f8x4_kernel");
@@ -2335,14 +2344,18 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                        ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
     return launch_check("maxsim_scan_f8_direct_kernel");
   }
-  // shape (lab A/B): 0 production, 1 = 32-token iterations / 3-deep ring,
-  // 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 / 2-deep
+  // shape (lab A/B): 0 production = 32-token iterations / 3-deep ring with the
+  // prefetch after each tile's first MFMA (PF: 75.7 -> 73.5 ms at 1M, B=256);
+  // 1 = the same without PF, 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 /
+  // 2-deep (2-4 spill at 8 queries per wave), 5 = 0, 6 = 2 with PF
   switch (shape) {
     case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
     case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
     case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
     case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    default: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 5: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
   }
 }
 
