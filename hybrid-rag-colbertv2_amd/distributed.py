@@ -37,6 +37,55 @@ def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
     return begin, begin + base + (1 if rank < rem else 0)
 
 
+def encode_queries_sharded(encoder, queries, device=None, dtype=torch.bfloat16,
+                           group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Query embeddings ``[B, Lq, D]`` for a batch of query strings, the
+    encoder's work split over the ranks instead of replicated on each.
+
+    The reference encodes every query in-process before scoring
+    (local_rag_complete.py:758 ``search``, :782 ``rerank``).  With the corpus
+    sharded, every rank needs the whole batch's embeddings, so each rank
+    encodes its contiguous slice ``shard_range(B, rank, G)`` (``is_query=True``:
+    the ColBERT query augmentation pads to Lq) and ONE all-gather of
+    ``[G, ceil(B/G), Lq, D]`` (2 MiB at B=256 in bf16) rebuilds the batch on
+    every rank, in query order.  The result equals ``encoder.encode(queries)``
+    on one process cast to ``dtype`` (gloo-tested at world size 2).  Without an
+    initialised process group this is that single encode."""
+    queries = [queries] if isinstance(queries, str) else list(queries)
+    B = len(queries)
+
+    def enc(rows):
+        try:
+            out = encoder.encode(rows, convert_to_tensor=True, is_query=True)
+        except TypeError:                       # encoders without the is_query keyword (FakeEncoder-like)
+            out = encoder.encode(rows, convert_to_tensor=True)
+        out = out if isinstance(out, torch.Tensor) else torch.as_tensor(np.asarray(out))
+        return out.to(device=device, dtype=dtype) if device is not None else out.to(dtype)
+
+    if not (dist.is_available() and dist.is_initialized()) or B == 0:
+        return enc(queries)
+    G, r = dist.get_world_size(group), dist.get_rank(group)
+    per = (B + G - 1) // G
+    b0, b1 = shard_range(B, r, G)
+    mine = enc(queries[b0:b1]) if b1 > b0 else None
+    # every rank must learn Lq and D even when its slice is empty
+    shape = torch.tensor(list(mine.shape[1:]) if mine is not None else [0, 0], dtype=torch.int64,
+                         device=device if device is not None else "cpu")
+    dist.all_reduce(shape, op=dist.ReduceOp.MAX, group=group)
+    lq, d = int(shape[0]), int(shape[1])
+    dev = mine.device if mine is not None else (device if device is not None else "cpu")
+    send = torch.zeros((per, lq, d), dtype=dtype, device=dev)
+    if mine is not None:
+        send[: b1 - b0].copy_(mine)
+    out = torch.empty((G, per, lq, d), dtype=dtype, device=dev)
+    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+        dist.all_gather_into_tensor(out, send, group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), send, group=group)
+    parts = [out[g, : shard_range(B, g, G)[1] - shard_range(B, g, G)[0]] for g in range(G)]
+    return torch.cat(parts, 0)
+
+
 class _DeviceOps:
     """HIP merge / select (libcolbert_mi355x.so)."""
 

@@ -160,3 +160,43 @@ def test_hybrid_exchange_world2_equals_unsharded():
     for _, s, i, li in res:
         assert np.array_equal(i, ei) and np.array_equal(li, bi)
         np.testing.assert_allclose(s, es, atol=1e-5)
+
+
+_QUERIES = ["what is late interaction", "colbert maxsim on mi355x", "bm25 and rrf fusion",
+            "hbm3e bandwidth", "rerank the top fifty chunks"]
+
+
+def _encode_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hybrid_rag_colbertv2_amd.distributed import encode_queries_sharded
+        from hybrid_rag_colbertv2_amd.encoder import FakeEncoder
+        enc = FakeEncoder()
+        # B = 5 (ragged over the ranks), 1 (empty slices on some ranks), 0
+        outs = [encode_queries_sharded(enc, _QUERIES[:n]).float().numpy() for n in (5, 1, 0)]
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_query_encoding_equals_single_process():
+    """Each rank encodes its slice of the batch; one all-gather rebuilds it in order."""
+    from hybrid_rag_colbertv2_amd.encoder import FakeEncoder
+    for world in (2, 3):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_encode_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        enc = FakeEncoder()
+        want = [enc.encode(_QUERIES[:n]).to(torch.bfloat16).float().numpy() for n in (5, 1)]
+        for _, outs in res:
+            assert np.array_equal(outs[0], want[0]) and np.array_equal(outs[1], want[1])
+            assert outs[2].shape[0] == 0

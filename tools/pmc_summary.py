@@ -7,8 +7,8 @@ averaged over the kernel's dispatches.  Derived (MI355X_MICROARCH.md):
   hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
       (gfx950: FETCH_SIZE reports half of a wide coalesced read; both in KB)
   clock_ghz = GRBM_GUI_ACTIVE / 8 / launch duration (summed over 8 XCDs)
-The output file holds one entry per (kernel, dtype); an existing entry for
-the same pair is replaced.
+The output file holds one entry per (kernel, dtype, batch, docs); an existing
+entry for the same key is replaced.
 """
 import csv
 import json
@@ -43,7 +43,9 @@ doc = {"entries": []}
 if os.path.exists(out_path):
     with open(out_path) as f:
         old = json.load(f)
-    doc["entries"] = [x for x in old.get("entries", []) if (x["kernel"], x.get("dtype")) != (kernel, dtype)]
+    key = (kernel, dtype, batch, docs)
+    doc["entries"] = [x for x in old.get("entries", [])
+                      if (x["kernel"], x.get("dtype"), x.get("batch"), x.get("docs_per_gpu")) != key]
 doc["entries"].append(e)
 with open(out_path, "w") as f:
     json.dump(doc, f, indent=1)
