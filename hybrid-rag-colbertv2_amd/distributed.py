@@ -67,18 +67,20 @@ def encode_queries_sharded(encoder, queries, device=None, dtype=torch.bfloat16,
     G, r = dist.get_world_size(group), dist.get_rank(group)
     per = (B + G - 1) // G
     b0, b1 = shard_range(B, r, G)
-    mine = enc(queries[b0:b1]) if b1 > b0 else None
+    nccl = dist.get_backend(group) == "nccl"
+    # the collectives' device: RCCL needs device tensors, gloo takes host ones
+    dev = torch.device(device) if device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu"))
+    mine = enc(queries[b0:b1]).to(dev) if b1 > b0 else None
     # every rank must learn Lq and D even when its slice is empty
-    shape = torch.tensor(list(mine.shape[1:]) if mine is not None else [0, 0], dtype=torch.int64,
-                         device=device if device is not None else "cpu")
+    shape = torch.tensor(list(mine.shape[1:]) if mine is not None else [0, 0], dtype=torch.int64, device=dev)
     dist.all_reduce(shape, op=dist.ReduceOp.MAX, group=group)
     lq, d = int(shape[0]), int(shape[1])
-    dev = mine.device if mine is not None else (device if device is not None else "cpu")
     send = torch.zeros((per, lq, d), dtype=dtype, device=dev)
     if mine is not None:
         send[: b1 - b0].copy_(mine)
     out = torch.empty((G, per, lq, d), dtype=dtype, device=dev)
-    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+    if nccl:
         dist.all_gather_into_tensor(out, send, group=group)
     else:
         dist.all_gather(list(out.unbind(0)), send, group=group)

@@ -289,6 +289,13 @@ def test_native_exchange_rccl_world1(dev, tmp_path):
         ref = PipelinedRetriever(ix, dev).run(batches)
         for (gs, gi), (rs, ri) in zip(got, ref):
             assert torch.equal(gi, ri) and torch.equal(gs, rs)
+        # sharded query encoding over RCCL (device tensors through the all-gather)
+        from hybrid_rag_colbertv2_amd.distributed import encode_queries_sharded
+        from hybrid_rag_colbertv2_amd.encoder import FakeEncoder
+        texts = ["late interaction on mi355x", "bm25 plus colbert", "top fifty to top ten"]
+        qe = encode_queries_sharded(FakeEncoder(), texts)
+        assert qe.device.type == "cuda" and qe.dtype == torch.bfloat16
+        assert torch.equal(qe.cpu(), FakeEncoder().encode(texts).to(torch.bfloat16))
         torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
