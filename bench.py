@@ -173,12 +173,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ix.time_scans(True)      # HIP events around each scan launch, on its own stream (C ABI)
     t0 = time.perf_counter()
     outs = run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    scan_ms = ix.scan_times()                           # the K scans of the timed region
     if world > 1:
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -214,18 +216,21 @@ def main():
         bm_all()
         bm_ms.append((time.perf_counter() - t) * 1e3)
 
-    # ---- dominant kernel: MaxSim scan, timed with HIP events on its stream
-    scan_ms = []
-    st = torch.cuda.current_stream()
-    # (fp32-faithful: the scan is the bf16 scan of hi; score() there is the full faithful rescoring)
-    scan_ix, Qs = (ColbertIndex(ix.tokens, ix.doclens, id_base=begin), Q.bfloat16()) if faithful else (ix, Q)
-    for _ in range(3):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        scan_ix.score(Qs)
-        e1.record(st)
-        e1.synchronize()
-        scan_ms.append(e0.elapsed_time(e1))
+    # ---- dominant kernel: the MaxSim scan launches of the timed region above,
+    # each bracketed by HIP events recorded on the scan's own stream by the C
+    # ABI (cbv2_index_time_scans); fp32-faithful: the bf16 scan of hi
+    if len(scan_ms) != args.steps:
+        log(f"warning: {len(scan_ms)} timed scans recorded for {args.steps} steps")
+    if not scan_ms:                      # (not expected) time 3 launches after the region instead
+        st = torch.cuda.current_stream()
+        scan_ix, Qs = (ColbertIndex(ix.tokens, ix.doclens, id_base=begin), Q.bfloat16()) if faithful else (ix, Q)
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            scan_ix.score(Qs)
+            e1.record(st)
+            e1.synchronize()
+            scan_ms.append(e0.elapsed_time(e1))
     scan_avg = sum(scan_ms) / len(scan_ms)
     n_local = end - begin
     achieved = B * n_local * FLOP_PER_PAIR / (scan_avg * 1e-3) / 1e12
@@ -288,7 +293,7 @@ def main():
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
             "roofline": {"bound": "mfma", "kernel": kern, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "traffic": traffic, "avg_ms": round(scan_avg, 3),
+                         "traffic": traffic, "avg_ms": round(scan_avg, 3), "launches_timed": len(scan_ms),
                          "clock_ghz_under_load": round(clock, 3) if clock else None},
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad},

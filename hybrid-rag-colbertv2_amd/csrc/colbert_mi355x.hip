@@ -2095,6 +2095,12 @@ struct cbv2_index {
   // max ||hi||); nullptr = plain bf16 index.
   const uint8_t* resid = nullptr;
   float resid_max = 0.0f, norm_max = 0.0f;
+  // Scan timing (cbv2_index_time_scans): while enabled, every MaxSim scan
+  // launch is bracketed by a pair of HIP events recorded on its own stream;
+  // the pairs are reused across enable cycles and destroyed with the handle.
+  bool time_scans = false;
+  size_t scan_ev_used = 0;
+  std::vector<hipEvent_t> scan_ev;  // [2 * i] start, [2 * i + 1] stop
 };
 
 namespace {
@@ -2389,11 +2395,39 @@ int check_query(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   return CBV2_OK;
 }
 
+// Start/stop events of the next timed scan (nullptr when timing is off or an
+// event cannot be created: the scan then runs untimed).
+bool scan_event_pair(cbv2_index* ix, hipEvent_t* e0, hipEvent_t* e1) {
+  if (!ix->time_scans) return false;
+  const size_t i = ix->scan_ev_used;
+  while (ix->scan_ev.size() < 2 * i + 2) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return false;
+    ix->scan_ev.push_back(e);
+  }
+  *e0 = ix->scan_ev[2 * i];
+  *e1 = ix->scan_ev[2 * i + 1];
+  return true;
+}
+
+int scan_maxsim_timed(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, float* out, int64_t ld_out,
+                      hipStream_t st) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  const bool timed = scan_event_pair(ix, &e0, &e1);
+  if (timed && hipEventRecord(e0, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
+  const int rc = ix->dtype == CBV2_DTYPE_MXFP8 ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st)
+                                               : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st);
+  if (rc) return rc;
+  if (timed) {
+    if (hipEventRecord(e1, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
+    ++ix->scan_ev_used;
+  }
+  return CBV2_OK;
+}
+
 int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t lq, float* out,
                int64_t ld_out, hipStream_t st) {
-  if (scorer == CBV2_SCORER_MAXSIM && ix->dtype == CBV2_DTYPE_MXFP8)
-    return scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st);
-  if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st);
+  if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim_timed(ix, Q, B, lq, out, ld_out, st);
   return scan_meanpool(ix, (const float*)Q, B, lq, out, ld_out, st);
 }
 
@@ -2588,14 +2622,37 @@ int cbv2_quantize_mxfp8(const void* x, int32_t dtype, int64_t rows, void* q, voi
 }
 
 int cbv2_index_destroy(cbv2_index* index) {
-  if (index != nullptr && index->task_ring != nullptr) {
+  if (index != nullptr && (index->task_ring != nullptr || !index->scan_ev.empty())) {
     int prev = 0;
     if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(index->device) == hipSuccess) {
-      (void)hipFree(index->task_ring);
+      if (index->task_ring != nullptr) (void)hipFree(index->task_ring);
+      for (hipEvent_t e : index->scan_ev) (void)hipEventDestroy(e);
       (void)hipSetDevice(prev);
     }
   }
   delete index;
+  return CBV2_OK;
+}
+
+int cbv2_index_time_scans(cbv2_index* ix, int32_t enable) {
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  if (enable) ix->scan_ev_used = 0;
+  ix->time_scans = enable != 0;
+  return CBV2_OK;
+}
+
+int cbv2_index_scan_times(cbv2_index* ix, float* ms, int32_t max, int32_t* count) {
+  CBV2_REQUIRE(ix != nullptr && count != nullptr, "null index or count");
+  CBV2_REQUIRE(max >= 0 && (max == 0 || ms != nullptr), "bad output buffer");
+  CBV2_REQUIRE(!ix->time_scans, "disable timing (cbv2_index_time_scans(ix, 0)) before reading the times");
+  *count = (int32_t)ix->scan_ev_used;
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  for (size_t i = 0; i < ix->scan_ev_used && i < (size_t)max; ++i) {
+    if (hipEventSynchronize(ix->scan_ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(ms + i, ix->scan_ev[2 * i], ix->scan_ev[2 * i + 1]) != hipSuccess)
+      return fail(CBV2_EHIP, "scan event %zu: %s", i, hipGetErrorString(hipGetLastError()));
+  }
   return CBV2_OK;
 }
 
@@ -2756,7 +2813,7 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   }
   if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
-  if ((rc = scan_maxsim(ix, w.qhi, B, lq, w.T, ix->n, st))) return rc;
+  if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st))) return rc;
   if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
     return rc;
   // 2. band T >= T_k - 2 beta, 3. faithful rescoring, 4. exact top-k of the band

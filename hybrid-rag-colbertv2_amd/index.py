@@ -246,6 +246,22 @@ class ColbertIndex:
             _lib.lib().cbv2_index_destroy(self._h)
             self._h = ctypes.c_void_p()
 
+    # ------------------------------------------------------------ measurement
+    def time_scans(self, enable: bool) -> None:
+        """Bracket every following MaxSim scan launch of this index with HIP
+        events on its own stream (cbv2_index_time_scans); enable clears the
+        previous record."""
+        _lib.check(_lib.lib().cbv2_index_time_scans(self._h, 1 if enable else 0))
+
+    def scan_times(self, max_launches: int = 4096) -> List[float]:
+        """Durations (ms) of the scans recorded since ``time_scans(True)``;
+        disables timing first.  Waits for the recorded launches to finish."""
+        self.time_scans(False)
+        ms = (ctypes.c_float * max_launches)()
+        cnt = ctypes.c_int32(0)
+        _lib.check(_lib.lib().cbv2_index_scan_times(self._h, ms, int(max_launches), ctypes.byref(cnt)))
+        return [float(ms[i]) for i in range(min(cnt.value, max_launches))]
+
     def __del__(self):
         try:
             self.close()

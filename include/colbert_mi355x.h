@@ -73,6 +73,17 @@ int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, 
                       int32_t d, const int32_t* doclens, int64_t id_base, cbv2_index** out);
 int cbv2_index_destroy(cbv2_index* index);
 
+/* Scan timing (measurement only; no reference counterpart -- the reference
+ * prints wall-clock stage timings, local_rag_complete.py:905-933).  While
+ * enabled, every MaxSim scan launch of this handle (cbv2_score / cbv2_search /
+ * cbv2_search_f32) is bracketed by HIP events recorded on the launch's own
+ * stream, so a benchmark can time the dominant kernel inside its timed region
+ * without a side launch.  enable=1 clears the previous record.
+ * cbv2_index_scan_times (timing disabled first) waits for the recorded launches
+ * and writes min(count, max) durations in ms; *count = launches recorded.  */
+int cbv2_index_time_scans(cbv2_index* index, int32_t enable);
+int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
+
 /* MXFP8 index (config 5: half the HBM bytes of bf16, scored on the
  * block-scaled fp8 MFMA): tokens e4m3 [n][128][128] (16-B aligned), scales
  * E8M0 [n][128][2] (byte h scales dims 64h .. 64h+63 by 2^(byte-127)).

@@ -341,3 +341,24 @@ def test_dynamic_tail_writes_every_score(dev):
     for a, b in [(0, 300), (N - 7000, N - 3000), (N - 3000, N)]:
         part = ColbertIndex(docs[a:b].contiguous(), doclens[a:b].contiguous()).score(Q)
         assert torch.equal(part, out[:, a:b]), (a, b)
+
+
+@pytest.mark.gpu
+def test_scan_timing_events(dev):
+    """cbv2_index_time_scans / cbv2_index_scan_times: one positive duration per
+    scan launch while enabled, none while disabled; scores unchanged."""
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    g = torch.Generator().manual_seed(3)
+    tok = torch.randn(3000, 128, 128, generator=g).to(dev, torch.bfloat16)
+    dl = torch.full((3000,), 128, dtype=torch.int32, device=dev)
+    Q = torch.randn(40, 32, 128, generator=g).to(dev, torch.bfloat16)
+    ix = ColbertIndex(tok, dl)
+    ref = ix.score(Q).clone()
+    ix.time_scans(True)
+    s1 = ix.score(Q)
+    _, _ = ix.search(Q, 10)
+    t = ix.scan_times()
+    assert len(t) == 2 and all(x > 0 for x in t)
+    assert torch.equal(s1, ref)
+    ix.score(Q)                                   # timing disabled by scan_times()
+    assert ix.scan_times() == []
