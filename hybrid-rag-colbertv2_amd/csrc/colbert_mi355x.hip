@@ -2653,6 +2653,7 @@ int cbv2_index_scan_times(cbv2_index* ix, float* ms, int32_t max, int32_t* count
         hipEventElapsedTime(ms + i, ix->scan_ev[2 * i], ix->scan_ev[2 * i + 1]) != hipSuccess)
       return fail(CBV2_EHIP, "scan event %zu: %s", i, hipGetErrorString(hipGetLastError()));
   }
+  ix->scan_ev_used = 0;  // read once: the record is consumed
   return CBV2_OK;
 }
 

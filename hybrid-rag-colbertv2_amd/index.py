@@ -255,7 +255,8 @@ class ColbertIndex:
 
     def scan_times(self, max_launches: int = 4096) -> List[float]:
         """Durations (ms) of the scans recorded since ``time_scans(True)``;
-        disables timing first.  Waits for the recorded launches to finish."""
+        disables timing first, then clears the record.  Waits for the recorded
+        launches to finish."""
         self.time_scans(False)
         ms = (ctypes.c_float * max_launches)()
         cnt = ctypes.c_int32(0)

@@ -80,7 +80,8 @@ int cbv2_index_destroy(cbv2_index* index);
  * stream, so a benchmark can time the dominant kernel inside its timed region
  * without a side launch.  enable=1 clears the previous record.
  * cbv2_index_scan_times (timing disabled first) waits for the recorded launches
- * and writes min(count, max) durations in ms; *count = launches recorded.  */
+ * and writes min(count, max) durations in ms; *count = launches recorded;
+ * the record is then cleared.  */
 int cbv2_index_time_scans(cbv2_index* index, int32_t enable);
 int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
 
