@@ -1097,8 +1097,8 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
   }
 }
 
-template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false>   // D = 2 spills at QW = 8
-__global__ __launch_bounds__(WAVES * 64, 2) void maxsim_scan_f8x4_kernel(
+template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2>   // D = 2 spills at QW = 8
+__global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
     float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr,
@@ -2318,17 +2318,20 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
 constexpr int kF8DirectMaxB = 8;
 constexpr int kF8Waves = 8, kF8QW = 8;
 
-template <int TPI, int NBUF, bool PF = false>
+// QW queries per wave, PER_CU workgroups per CU in the split, OCC the
+// launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
+template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs) {
-  constexpr int QPB = kF8Waves * kF8QW;
+  constexpr int QPB = WAVES * QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   ScanSplit sp;
-  const int rc = plan_split(ix, nq_groups, cu_count(ix->device), dyn_frac, task_docs, st, &sp);
+  const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<kF8Waves, kF8QW, 1, NBUF, TPI, PF>), dim3((unsigned)(nq_groups * sp.n_chunks)),
-                     dim3(kF8Waves * 64), 0, st, ix->tokens, ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out,
-                     ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs);
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC>),
+                     dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
+                     ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
+                     sp.task_docs);
   return launch_check("maxsim_scan_f8x4_kernel");
 }
 
@@ -2361,6 +2364,13 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
     case 5: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
     case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+#ifdef CBV2_LAB
+    // lab, 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave,
+    // three workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two
+    // workgroups per CU (2 waves per SIMD from independent barrier domains)
+    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+#endif
     default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
   }
 }

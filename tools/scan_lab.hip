@@ -12,6 +12,7 @@
 // (maxsim_scan16x4_kernel, variants 11/12); its lab history: pipeline depth
 // D=1/2/3 70.8/74.2/74.1 %, 3-deep LDS ring +0.4 %, without doc streaming 76.0 %.
 //   109: no doc streaming and no barrier (doc 0's LDS image reused; INVALID)  110: same with the per-doc barrier
+#define CBV2_LAB 1
 #include "../hybrid-rag-colbertv2_amd/csrc/colbert_mi355x.hip"
 
 namespace {
@@ -360,7 +361,7 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
   hipStream_t st = (hipStream_t)stream;
   if (variant == 1 || B <= kF8DirectMaxB) return scan_f8(ix, Qb, B, lq, out, ld, st);
   if (variant == 2) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.0f);  // doc-interleaved, static split only
-  if (variant >= 10 && variant <= 16) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
+  if (variant >= 10 && variant <= 18) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
                                                      variant - 10);  // iteration shapes, see scan_f8
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;
