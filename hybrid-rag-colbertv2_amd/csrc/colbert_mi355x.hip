@@ -473,9 +473,15 @@ __device__ __forceinline__ int swz4(int R) { return (((R >> 5) & 3) << 2) | (R &
 // (Moving chain k-D's max one MFMA later removes hipcc's s_nop pads for the
 // MFMA -> VALU hazard, 26 -> 2 per iteration, and gains nothing measurable:
 // the partner wave covers them.  Lab, round 1.)
-template <int QW, int D, int NT = 8>
+struct NoTileHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+// hook(t) runs right after tile t's first MFMA chain has issued (SPREAD: the
+// next iteration's DMA pieces; NoTileHook = nothing).
+template <int QW, int D, int NT = 8, typename Hook = NoTileHook>
 __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
-                                           float (&m)[QW][2]) {
+                                           float (&m)[QW][2], Hook hook = Hook{}) {
   constexpr int NC = 2 * QW;
   constexpr int NK = NT * NC;
   const int c = lane & 15, g = lane >> 4;
@@ -498,6 +504,7 @@ __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const b
       for (int s = 0; s < 4; ++s)
         x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t & 1][s], qf[cc >> 1][cc & 1][s], x, 0, 0, 0);
       acc[k % (D + 1)] = x;
+      if (cc == 0) hook(t);
     }
     if (k >= D) {
       const int kk = k - D, pc = kk % NC;
@@ -565,7 +572,12 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
 // static split ends when the slowest XCD does; the dynamic tail lets the fast
 // ones take the remainder.  Every doc range runs the same pipelined loop.
 // STAMPS (lab only): per-workgroup s_memrealtime / s_memtime at start and end.
-template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2>
+// SPREAD (2-deep ring): a full iteration issues its wave's DMA pieces of the
+// next iteration one per tile from inside the MFMA stream, instead of all at
+// once after the barrier, where every wave of the CU queues on the address
+// path at the same moment (lab phase stamps: ~1.2k issue cycles/iteration).
+template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
+          bool SPREAD = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -616,6 +628,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     src_doc[jj] = doc;
   }
 
+  // STAMPS (lab only): per-wave s_memtime cycles in three phases of the ring
+  // loop -- wait (vmcnt + barrier), issue (next DMA + doc lengths), compute
+  // (tiles + epilogue, to the next iteration's top) -- and the iteration count
+  uint64_t ph_wait = 0, ph_issue = 0, ph_comp = 0, ph_n = 0, ph_t = 0;
+
   // the first range: this workgroup's static chunk (may be empty)
   int64_t d_begin = chunk * chunk_docs;
   int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
@@ -623,17 +640,18 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     if (d_begin < d_end) {
       const int nd = (int)(d_end - d_begin);
       const int ngr = (nd + 3) >> 2;
-      auto issue = [&](int it, int buf) {
+      auto issue_piece = [&](int it, int buf, int jj) {
         const int G = it / IPG, j = it % IPG;
+        const int piece = wave * kPiecesPerWave + jj;
+        int d = 4 * G + src_doc[jj];
+        d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
+        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * TPI * kRowBytes + src_off[jj];
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
+                                         0, 0);
+      };
+      auto issue = [&](int it, int buf) {
 #pragma unroll
-        for (int jj = 0; jj < kPiecesPerWave; ++jj) {
-          const int piece = wave * kPiecesPerWave + jj;
-          int d = 4 * G + src_doc[jj];
-          d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-          const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * TPI * kRowBytes + src_off[jj];
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
-                                           0, 0);
-        }
+        for (int jj = 0; jj < kPiecesPerWave; ++jj) issue_piece(it, buf, jj);
       };
 
       float sc[QW];
@@ -648,14 +666,25 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       int cur = 0;           // ring slot of iteration it
       bool stored = false;   // global stores issued last iteration (they count in vmcnt)
       for (int it = 0; it < nit; ++it) {
+        uint64_t ph_a = 0;
+        if constexpr (STAMPS) {
+          ph_a = __builtin_amdgcn_s_memtime();
+          if (ph_t) ph_comp += ph_a - ph_t;
+        }
         if (NBUF == 3 && it + 1 < nit && !stored)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        uint64_t ph_b = 0;
+        if constexpr (STAMPS) {
+          ph_b = __builtin_amdgcn_s_memtime();
+          ph_wait += ph_b - ph_a;
+        }
         stored = false;
-        if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
+        const int nslot = cur ^ 1;  // 2-deep ring: iteration it+1's slot
+        if (NBUF == 2 && !SPREAD && it + 1 < nit) issue(it + 1, nslot);
         if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
         const uint8_t* buf = smem + cur * kIterBytes;
         cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
@@ -674,9 +703,28 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
 #pragma unroll
           for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
         }
-        if (TPI * j + TPI <= dl_min)
-          iter4_full<QW, D, NT>(buf, lane, qf, m);
-        else if (TPI * j < dl_max)
+        if constexpr (STAMPS) {
+          ph_t = __builtin_amdgcn_s_memtime();
+          ph_issue += ph_t - ph_b;
+          ++ph_n;
+        }
+        const bool full = TPI * j + TPI <= dl_min;
+        if constexpr (SPREAD && NBUF == 2) {
+          static_assert(NT >= kPiecesPerWave, "one piece per tile");
+          if (it + 1 < nit && !full) issue(it + 1, nslot);   // ragged or empty iteration: all at once
+        }
+        if (full) {
+          if constexpr (SPREAD && NBUF == 2) {
+            if (it + 1 < nit)
+              iter4_full<QW, D, NT>(buf, lane, qf, m, [&](int t) {
+                if (t < kPiecesPerWave) issue_piece(it + 1, nslot, t);
+              });
+            else
+              iter4_full<QW, D, NT>(buf, lane, qf, m);
+          } else {
+            iter4_full<QW, D, NT>(buf, lane, qf, m);
+          }
+        } else if (TPI * j < dl_max)
           iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
         if (j == IPG - 1) {
           // doc 4G+g's score in every lane of group g; lane c of the 64-doc block
@@ -711,12 +759,20 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     d_end = d_begin + sz < n ? d_begin + sz : n;
   }
   if constexpr (STAMPS) {
+    if (ph_t) ph_comp += __builtin_amdgcn_s_memtime() - ph_t;
     if (threadIdx.x == 0) {
       uint64_t* st = stamps + 4 * (size_t)bid;
       st[0] = r_start;
       st[1] = __builtin_amdgcn_s_memrealtime();
       st[2] = t_start;
       st[3] = __builtin_amdgcn_s_memtime();
+    }
+    if (lane == 0) {  // phase sums: rows 16384 + 8 * bid + wave of the [rows][4] stamp buffer
+      uint64_t* ph = stamps + 4 * ((size_t)16384 + 8 * (size_t)bid + wave);
+      ph[0] = ph_wait;
+      ph[1] = ph_issue;
+      ph[2] = ph_comp;
+      ph[3] = ph_n;
     }
   }
 }
@@ -2246,7 +2302,7 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
   return CBV2_OK;
 }
 
-template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2>
+template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -2254,7 +2310,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
   ScanSplit sp;
   const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC>), dim3((unsigned)(nq_groups * sp.n_chunks)),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD>), dim3((unsigned)(nq_groups * sp.n_chunks)),
                      dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, sp.chunk_docs,
                      sp.static_docs, sp.ctr, sp.task_docs, stamps);
   return launch_check("maxsim_scan16x4_kernel");

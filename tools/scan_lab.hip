@@ -321,6 +321,12 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   if (kind == 7) return launch_scan16x4<8, 2, 1, 2, 2, false, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
   if (kind == 8) return launch_scan16x4<4, 4, 2, 2, 2, false, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
   if (kind == 9) return launch_scan16x4<8, 2, 1, 2, 3, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  // kind 10: production shape with the spread DMA issue (SPREAD); kind 11: its
+  // phase-stamped build (STAMPS + SPREAD; the stamps buffer is required)
+  if (kind == 10) return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, true>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 11 && stamps != nullptr)
+    return launch_scan16x4<8, 4, 1, 2, 2, true, 64, 2, true>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
+                                                             (uint64_t*)stamps);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,

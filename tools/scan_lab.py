@@ -152,6 +152,15 @@ def stamps_report(run_stamped, n_wg_max=1 << 16):
           f"max {dur.max():.1f}; launch span {span:.1f} us; start skew {(r0.max() - r0.min()) / 100:.1f} us; "
           f"tail loss (span/median - 1) {span / np.median(dur) - 1:.2%}; clock GHz min {clk.min():.3f} "
           f"median {np.median(clk):.3f} max {clk.max():.3f}", flush=True)
+    ph = buf.cpu().numpy()[16384:].astype(np.float64)          # per-wave phase cycles (s_memtime)
+    ph = ph[ph[:, 3] > 0]
+    if len(ph):
+        tot = ph[:, :3].sum(axis=1)
+        fr = ph[:, :3] / tot[:, None]
+        print(f"phases over {len(ph)} waves (median fraction of loop cycles): wait {np.median(fr[:, 0]):.2%}  "
+              f"issue {np.median(fr[:, 1]):.2%}  compute {np.median(fr[:, 2]):.2%}; per iteration cycles: "
+              f"wait {np.median(ph[:, 0] / ph[:, 3]):.0f} issue {np.median(ph[:, 1] / ph[:, 3]):.0f} "
+              f"compute {np.median(ph[:, 2] / ph[:, 3]):.0f}", flush=True)
     bid = np.nonzero(buf.cpu().numpy()[:, 1] > 0)[0]
     for x in range(8):
         sel = (bid & 7) == x
