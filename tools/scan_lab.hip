@@ -327,6 +327,9 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   if (kind == 11 && stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64, 2, true>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
                                                              (uint64_t*)stamps);
+  // kind 12: the B <= 16 production shape (kind 6) phase-stamped
+  if (kind == 12 && stamps != nullptr)
+    return launch_scan16x4<4, 4, 2, 2, 2, true, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
