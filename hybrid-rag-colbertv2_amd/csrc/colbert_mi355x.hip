@@ -2269,6 +2269,12 @@ int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, flo
 // 18.26 -> 17.73 ms at 125k (fixed 64-doc tasks: 143.1 / 17.92).
 constexpr float kScanDynFrac = 0.10f;
 constexpr int kScanTaskDocs = -16;     // guided: tasks shrink to 16 docs at the end
+// B <= 16 (one query group, two 4-wave workgroups per CU): a larger dynamic
+// share.  Lab, 1M docs, B=16: tail loss 9.7 % at 0.1 (per-workgroup stamps;
+// clocks 1.57-1.70 GHz across XCDs under streaming); 12.41 -> 11.76 ms at 0.3
+// (-5.2 %), 1.479 -> 1.439 ms at 125k; 0.5 and 1.0 lose at 1M (14.2 / 16.2
+// ms).  B=64 is flat in the fraction (36.87-36.90 ms), so B > 16 keeps 0.1.
+constexpr float kScanDynFracSmallB = 0.30f;
 
 // Work split of one launch: n_chunks static chunks of chunk_docs per query
 // group over [0, static_docs), the rest as dynamic tasks on a fresh counter slot.
@@ -2365,7 +2371,7 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16x4W8:
       return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, Q, B, lq, out, ld_out, st);
     case kScan16x4W4:
-      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st);
+      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB);
     default:
       return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
   }

@@ -362,3 +362,23 @@ def test_scan_timing_events(dev):
     assert torch.equal(s1, ref)
     ix.score(Q)                                   # timing disabled by scan_times()
     assert ix.scan_times() == []
+
+
+def test_dynamic_tail_b16_bit_identical(dev):
+    """B <= 16 (4-wave shape, 30 % dynamic share): every score equals the B=1
+    direct scan's and a small index's over the same docs, bit for bit."""
+    N, B = 60000, 16
+    g = torch.Generator(device=dev).manual_seed(11)
+    docs = torch.randn(N, 128, 128, device=dev, generator=g)
+    docs = (docs / docs.norm(dim=-1, keepdim=True)).bfloat16()
+    doclens = torch.randint(0, 129, (N,), device=dev, generator=g, dtype=torch.int32)
+    Q = torch.randn(B, 32, 128, device=dev, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16()
+    ix = ColbertIndex(docs, doclens)
+    full = ix.score(Q)
+    assert torch.equal(ix.score(Q), full)                       # counters reset per launch
+    for b in (0, 7, 15):
+        assert torch.equal(ix.score(Q[b:b + 1]), full[b:b + 1]), b
+    for a, e in [(0, 900), (N - 3000, N)]:
+        part = ColbertIndex(docs[a:e].contiguous(), doclens[a:e].contiguous()).score(Q)
+        assert torch.equal(part, full[:, a:e]), (a, e)
