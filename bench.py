@@ -7,13 +7,26 @@ One STEP = one batch of B=256 queries (embeddings + BM25 term ids) through
 the whole path:
   stage 1  host BM25 top-100 (native C++, csrc/host_bm25.cpp) over the
            synthetic 1M-doc term corpus -- run while the GPU scans,
-  stage 2  HIP MaxSim scan + radix top-100 over the corpus (sharded over ranks:
-           per-rank top-100 -> RCCL all-gather -> HIP merge; the ranks' BM25
-           lists over their doc shards ride the same all-gather),
+  stage 2  HIP MaxSim scan with the top-100 fused into it (per-workgroup
+           candidate lists in LDS + one selection per query; sharded over
+           ranks: per-rank top-100 -> RCCL all-gather -> HIP merge; the ranks'
+           BM25 lists over their doc shards ride the same all-gather),
   fusion   host RRF (native C++, reference semantics) -> top-50 candidates,
   stage 3  HIP gather-by-id MaxSim rerank -> top-10 (sharded: RCCL all-reduce MAX).
 Inputs (the query batch and term ids, both indexes) are resident before the
 timed region; every stage runs in full inside every timed step.
+
+The JSON line also carries, measured in the same run:
+  faithful         the same K steps on the fp32-faithful index (the reference's
+                   fp32 arithmetic within 1e-4: bf16 scan + certified band
+                   rescoring), checked against the float64
+                   oracle of the fp32 values at 1e-4;
+  native_exchange  (N > 1, RCCL) the same K steps with the exchange inside the
+                   C ABI (cbv2_search_sharded_* / cbv2_rerank_sharded);
+  cpu_baseline     the CPU restatements timed on this host (numpy fp32 BLAS =
+                   `value`; the scalar C restatement; the literal mean-pool
+                   scorer), with the CPU model and thread count;
+  p50 / p99        single-query latency of the whole hot path.
 
 N>1: the SAME 1M-doc corpus is split into N contiguous shards, one per rank
 (strong scaling); value = B*K / max-over-ranks wall time.
@@ -57,14 +70,43 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def host_info():
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(Q: torch.Tensor, tokens: torch.Tensor, n_total: int, budget_s: float):
-    """Oracle MaxSim (fp32 numpy/BLAS, as the reference computes on CPU) + top-100 on a bounded sample."""
+    """The CPU restatements of the reference path, timed on this host on bounded
+    samples of the same corpus and queries, extrapolated to n_total docs:
+      numpy   oracle.maxsim fp32 (einsum -> max -> sum, BLAS threads) + top-100:
+              the reference's own CPU arithmetic (torch fp32 on "cpu", LRC:802-831
+              in its MaxSim form) -- this row is `value`;
+      c       oracle/cbv2_oracle.c, scalar C (double accumulation, one core);
+      literal the reference's code as written (LRC:821-829: mean-pool both sides,
+              doc means recomputed per call, cosine), numpy float64.
+    Threads: OMP_NUM_THREADS (the box's CPU share for this GPU) or the affinity
+    mask -- this host's cores available to the process."""
     from threadpoolctl import threadpool_limits
     from oracle import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    info = host_info()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or info["affinity_cpus"]
     n_s = min(20000, tokens.shape[0])
     docs = tokens[:n_s].float().cpu().numpy()
     q = Q.float().cpu().numpy()
+    rows = []
     with threadpool_limits(limits=threads):
         t0 = time.perf_counter()
         s = orc.maxsim(q[:2], docs, dtype=np.float32)
@@ -75,11 +117,83 @@ def cpu_baseline(Q: torch.Tensor, tokens: torch.Tensor, n_total: int, budget_s: 
         s = orc.maxsim(q[:b_s], docs, dtype=np.float32)
         orc.topk(s, 100)
         dt = time.perf_counter() - t0
-    qps = b_s / (dt * n_total / n_s)
+        qps = b_s / (dt * n_total / n_s)
+        rows.append({"impl": "numpy fp32 einsum->max->sum + top-100 (oracle.maxsim)", "value": round(qps, 6),
+                     "cores": threads, "sample": f"{b_s} queries x {n_s} docs, {dt:.1f}s"})
+        # literal scorer (per-call doc means, as LRC:822 recomputes them)
+        t0 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t0 < budget_s / 6 or reps == 0:
+            orc.meanpool_cosine(q[reps % q.shape[0]: reps % q.shape[0] + 1], docs)
+            reps += 1
+        dt_l = time.perf_counter() - t0
+        rows.append({"impl": "literal mean-pool cosine (LRC:821-829, doc means per call; oracle.meanpool_cosine)",
+                     "value": round(reps / (dt_l * n_total / n_s), 6), "cores": threads,
+                     "sample": f"{reps} queries x {n_s} docs, {dt_l:.1f}s"})
+    try:   # scalar C restatement on the same bf16 values (oracle/cbv2_oracle.c)
+        qb = Q[:1].contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
+        n_c = 64
+        t0 = time.perf_counter()
+        while True:
+            db = tokens[:n_c].contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
+            t1 = time.perf_counter()
+            orc.c_maxsim_bf16(qb, db, np.full(n_c, LD, np.int32))
+            dt_c = time.perf_counter() - t1
+            if dt_c > budget_s / 6 or n_c >= n_s or time.perf_counter() - t0 > budget_s / 3:
+                break
+            n_c *= 4
+        rows.append({"impl": "scalar C, double accumulation (oracle/cbv2_oracle.c)",
+                     "value": round(1.0 / (dt_c * n_total / n_c), 8), "cores": 1,
+                     "sample": f"1 query x {n_c} docs, {dt_c:.2f}s"})
+    except Exception as e:  # the C library is built by __graft_entry__.build(); report, do not fail
+        rows.append({"impl": "scalar C (oracle/cbv2_oracle.c)", "error": str(e)[:200]})
     return {"value": round(qps, 6), "unit": "queries/s", "cores": threads, "kind": "port",
             "sample": f"{b_s} queries x {n_s} docs (fp32 numpy einsum->max->sum + top-100, "
                       f"{threads} BLAS threads, {dt:.1f}s), extrapolated to {n_total} docs",
-            "cpu": platform.processor() or platform.machine()}
+            "cpu": info["cpu_model"], "nproc": info["nproc"], "affinity_cpus": info["affinity_cpus"],
+            "omp_num_threads": info["omp_num_threads"], "rows": rows}
+
+
+def timed_steps(run_steps, K, W, world):
+    """W untimed warmup steps, then EXACTLY K steps bracketed by barrier + sync on
+    both sides; returns (outputs, max-over-ranks elapsed seconds)."""
+    if W:
+        run_steps(W)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = run_steps(K)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    return outs, elapsed
+
+
+def spot_check(fs, fi_h, Qd, docs_fn, begin, end, queries, tol, world, dev):
+    """Oracle MaxSim of the final top-10 of a few queries, each id checked on the
+    rank that owns it; the mismatch count is summed over ranks."""
+    from oracle import oracle as orc
+    bad = 0
+    for b in queries:
+        pos = [j for j, x in enumerate(fi_h[b]) if begin <= x < end]
+        if not pos:
+            continue
+        sel = torch.tensor([int(fi_h[b][j]) for j in pos], device=dev) - begin
+        ref = orc.maxsim(Qd[b:b + 1], docs_fn(sel))[0]
+        got = fs[b, pos].cpu().numpy()
+        bad += int(np.abs(got - ref).max() > tol)
+    if world > 1:
+        t = torch.tensor([bad], device=dev, dtype=torch.int64)
+        dist.all_reduce(t)
+        bad = int(t.item())
+    return bad
 
 
 def main():
@@ -92,13 +206,15 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--fused", type=int, default=50)
     ap.add_argument("--final-k", type=int, default=10)
-    ap.add_argument("--p50-iters", type=int, default=30)
+    ap.add_argument("--p50-iters", type=int, default=100)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check-queries", type=int, default=4)
+    ap.add_argument("--no-faithful", action="store_true", help="skip the fp32-faithful leg")
+    ap.add_argument("--check-queries", type=int, default=8)
     ap.add_argument("--no-pipeline", action="store_true", help="time unpipelined steps")
     ap.add_argument("--native-exchange", action="store_true",
-                    help="N>1: run the all-gather / all-reduce inside the C ABI (cbv2_*_sharded) on torch's RCCL comm")
+                    help="N>1: the MAIN timing uses the exchange inside the C ABI (the native leg always runs too)")
+    ap.add_argument("--unfused-topk", action="store_true", help="stage 2 without the fused top-k (A/B)")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
                          "(bf16 hi scanned + residual-certified band, DESIGN 3.12)")
@@ -122,6 +238,7 @@ def main():
 
     B, n_total = args.batch, args.docs
     begin, end = shard_range(n_total, rank, world)
+    n_local = end - begin
     t_setup = time.time()
     Qf = synth.make_queries(B, LQ, seed=1)
     planted = synth.planted_ids(B, n_total, 10, seed=2)
@@ -141,50 +258,38 @@ def main():
         ix = ColbertIndex.faithful_f32(tokens, doclens, id_base=begin)
     elif args.dtype == "fp8":
         ix = ColbertIndex.mxfp8(tokens, doclens, id_base=begin)   # quantized on the GPU (HIP kernel)
-        tokens_ref = tokens                                          # kept only for the spot parity check
     else:
         ix = ColbertIndex(tokens, doclens, id_base=begin)
-    searcher = ShardedSearcher(ix, native=args.native_exchange and world > 1 and backend == "nccl",
-                               lexical_k=args.k)
+    if args.unfused_topk:
+        from hybrid_rag_colbertv2_amd import _lib
+        ix.set_option(_lib.OPT_FUSED_TOPK, 0)
+    nccl = world > 1 and backend == "nccl"
+    searcher = ShardedSearcher(ix, native=args.native_exchange and nccl, lexical_k=args.k)
     Q = Qf.to(dev, torch.float32 if faithful else torch.bfloat16)
     Q1 = Q[:1].contiguous()
     torch.cuda.synchronize()
     log(f"setup {time.time() - t_setup:.1f}s: rank {rank}/{world} docs [{begin},{end}) B={B}")
 
-    def step(Qb, lexical):
+    def step(srch, Qb, lexical):
         """One batch, unpipelined (used for the B=1 latency)."""
-        _, ids, bm = searcher.search_hybrid(Qb, args.k, lexical)
+        _, ids, bm = srch.search_hybrid(Qb, args.k, lexical)
         bm = bm.cpu().numpy() if isinstance(bm, torch.Tensor) else bm
         cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=args.fused)
         cand_d = torch.from_numpy(cand).to(dev, non_blocking=False)
-        return searcher.rerank(Qb, cand_d, args.final_k)
+        return srch.rerank(Qb, cand_d, args.final_k)
 
-    # Throughput: K batches through the software-pipelined path (batch j+1's
-    # scan runs on the GPU while the host runs its BM25 and fuses batch j; see
-    # PipelinedRetriever).
-    pipe = PipelinedRetriever(searcher, dev, colbert_k=args.k, fused=args.fused, final_k=args.final_k)
-    if args.no_pipeline:
-        run_steps = lambda K: [step(Q, bm_all)[:2] for _ in range(K)]  # noqa: E731
-    else:
-        run_steps = lambda K: pipe.run([(Q, bm_all)] * K)  # noqa: E731
-    if args.warmup:
-        run_steps(args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    def stepper(srch, Qb):
+        # K batches through the software-pipelined path (batch j+1's scan runs on
+        # the GPU while the host runs its BM25 and fuses batch j; PipelinedRetriever)
+        pipe = PipelinedRetriever(srch, dev, colbert_k=args.k, fused=args.fused, final_k=args.final_k)
+        if args.no_pipeline:
+            return lambda K: [step(srch, Qb, bm_all)[:2] for _ in range(K)]
+        return lambda K: pipe.run([(Qb, bm_all)] * K)
+
     ix.time_scans(True)      # HIP events around each scan launch, on its own stream (C ABI)
-    t0 = time.perf_counter()
-    outs = run_steps(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    scan_ms = ix.scan_times()                           # the K scans of the timed region
-    if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world)
+    scan_ms = ix.scan_times()                           # the warmup + K scans; keep the K of the timed region
+    scan_ms = scan_ms[-args.steps:] if len(scan_ms) >= args.steps else scan_ms
     qps = B * args.steps / elapsed
     band = None
     if faithful:                         # the band each query of the last timed batch rescored
@@ -198,18 +303,19 @@ def main():
     top10_planted = float(np.mean([set(fi_h[b]) == set(planted[b]) for b in range(B)]))
     sorted_ok = bool((torch.diff(fs, dim=1) <= 0).all().item())
 
-    # ---- p50 latency at batch 1 (whole hot path, one query)
+    # ---- p50 / p99 latency at batch 1 (whole hot path, one query)
     lat = []
     for it in range(args.p50_iters + 3):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t = time.perf_counter()
-        step(Q1, bm_one)
+        step(searcher, Q1, bm_one)
         torch.cuda.synchronize()
         if it >= 3:
             lat.append((time.perf_counter() - t) * 1e3)
     p50 = statistics.median(lat) if lat else None
+    p99 = float(np.percentile(lat, 99)) if lat else None
     bm_ms = []
     for _ in range(3):                                  # stage 1 alone (host), for the record
         t = time.perf_counter()
@@ -221,59 +327,83 @@ def main():
     # ABI (cbv2_index_time_scans); fp32-faithful: the bf16 scan of hi
     if len(scan_ms) != args.steps:
         log(f"warning: {len(scan_ms)} timed scans recorded for {args.steps} steps")
-    if not scan_ms:                      # (not expected) time 3 launches after the region instead
-        st = torch.cuda.current_stream()
-        scan_ix, Qs = (ColbertIndex(ix.tokens, ix.doclens, id_base=begin), Q.bfloat16()) if faithful else (ix, Q)
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            scan_ix.score(Qs)
-            e1.record(st)
-            e1.synchronize()
-            scan_ms.append(e0.elapsed_time(e1))
-    scan_avg = sum(scan_ms) / len(scan_ms)
-    n_local = end - begin
+    scan_avg = sum(scan_ms) / len(scan_ms) if scan_ms else float("nan")
     achieved = B * n_local * FLOP_PER_PAIR / (scan_avg * 1e-3) / 1e12
+    fused_topk = ix.fused_topk_slots(B, args.k) > 0
     # HBM bytes per launch from the committed PMC passes of the same kernel and
     # shape (tools/profile_round.sh -> tools/pmc_summary.py); null otherwise
     traffic = clock = None
     pmc = os.path.join(ROOT, "profiles", "pmc_scan.json")
+    want = "maxsim_scan_f8x4_kernel" if args.dtype == "fp8" else SCAN_KERNEL
+    variant = "fused" if fused_topk else "unfused"
     if os.path.exists(pmc):
         with open(pmc) as f:
             entries = json.load(f).get("entries", [])
-        want = "maxsim_scan_f8x4_kernel" if args.dtype == "fp8" else SCAN_KERNEL
         for d in entries:
-            if d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == want:
+            if (d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == want
+                    and d.get("variant", "unfused") == variant):
                 traffic, clock = d.get("hbm_bytes_per_launch"), d.get("clock_ghz")
 
-    # ---- spot parity: oracle MaxSim of the final candidates for a few queries
-    from oracle import oracle as orc
-    bad = 0
-    for b in range(min(args.check_queries, B)):
-        ids_b = [int(x) for x in fi_h[b] if begin <= x < end]
-        if world > 1 or not ids_b:
-            continue
-        sel = torch.tensor(ids_b, device=dev) - begin
-        if args.dtype == "fp8":          # the oracle scores the same dequantized fp8 values
-            d = orc.mxfp8_dequant(ix.tokens[sel].cpu().numpy(), ix.scales[sel].cpu().numpy())
-            qq, qs = quantize_mxfp8(Q[b:b + 1])
-            qd = orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy())
-            tol = 2e-3
-        else:                            # bf16: the stored bf16 values; fp32: the fp32 values themselves
-            d = tokens[sel].float().cpu().numpy()
-            qd = Q[b:b + 1].float().cpu().numpy()
-            tol = 1e-4 if faithful else 1e-3
-        ref = orc.maxsim(qd, d)[0]
-        got = fs[b, : len(ids_b)].cpu().numpy()
-        bad += int(np.abs(got - ref).max() > tol)
+    # ---- spot parity: oracle MaxSim of the final candidates, on the owning rank
+    check_rows = list(range(min(args.check_queries, B)))
+    if args.dtype == "fp8":              # the oracle scores the same dequantized fp8 values
+        from oracle import oracle as orc
+        qq, qs = quantize_mxfp8(Q)
+        Qd = orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy())
+        docs_fn = lambda sel: orc.mxfp8_dequant(ix.tokens[sel].cpu().numpy(), ix.scales[sel].cpu().numpy())  # noqa: E731
+        tol = 2e-3
+    else:                                # bf16: the stored bf16 values; fp32: the fp32 values themselves
+        Qd = Q.float().cpu().numpy()
+        docs_fn = lambda sel: tokens[sel].float().cpu().numpy()   # noqa: E731
+        tol = 1e-4 if faithful else 1e-3
+    bad = spot_check(fs, fi_h, Qd, docs_fn, begin, end, check_rows, tol, world, dev)
 
+    # ---- N > 1 over RCCL: the same K steps with the native (in-ABI) exchange
+    native = nsearch = None
+    if nccl and not faithful:
+        nsearch = searcher if args.native_exchange else ShardedSearcher(ix, native=True, lexical_k=args.k)
+        nouts, nel = timed_steps(stepper(nsearch, Q), args.steps, args.warmup, world)
+        nfi = nouts[-1][1].cpu().numpy()
+        native = {"value": round(B * args.steps / nel, 2), "ms_per_step": round(nel / args.steps * 1e3, 3),
+                  "top10_equals_planted": float(np.mean([set(nfi[b]) == set(planted[b]) for b in range(B)])),
+                  "equals_torch_exchange": bool(np.array_equal(nfi, fi_h)),
+                  "main_line": "native" if args.native_exchange else "torch.distributed"}
+
+    # ---- CPU baseline (rank 0; the other ranks wait at the barrier below)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(Q, tokens, n_total, args.cpu_budget)
+    if world > 1:
+        dist.barrier()
+
+    # ---- the contract-precision leg: the same K steps on the fp32-faithful index
+    fleg = None
+    if args.dtype == "bf16" and not args.no_faithful:
+        nsearch = None
+        del searcher, ix, tokens
+        torch.cuda.empty_cache()
+        f32, dl32 = synth.make_shard(begin, end, Qf, planted, dev, seed=0, dtype=torch.float32)
+        fix = ColbertIndex.faithful_f32(f32, dl32, id_base=begin)
+        fsearch = ShardedSearcher(fix, lexical_k=args.k)
+        Qf32 = Qf.to(dev)
+        fix.time_scans(True)
+        fouts, fel = timed_steps(stepper(fsearch, Qf32), args.steps, args.warmup, world)
+        fscan = fix.scan_times()[-args.steps:]
+        ffs, ffi = fouts[-1]
+        ffi_h = ffi.cpu().numpy()
+        bs = fix.last_band.float()
+        fbad = spot_check(ffs, ffi_h, Qf32.cpu().numpy(), lambda sel: f32[sel].cpu().numpy(), begin, end,
+                          check_rows, 1e-4, world, dev)
+        fleg = {"value": round(B * args.steps / fel, 2), "ms_per_step": round(fel / args.steps * 1e3, 3),
+                "scan_avg_ms": round(sum(fscan) / len(fscan), 3) if fscan else None,
+                "band": {"mean": round(float(bs.mean()), 1), "max": int(bs.max()),
+                         "overflow_rows": int((bs < 0).sum())},
+                "tolerance": 1e-4, "oracle_mismatch_queries": fbad,
+                "top10_equals_planted": float(np.mean([set(ffi_h[b]) == set(planted[b]) for b in range(B)])),
+                "note": "fp32 index (the reference stores fp32, LRC:735-746); scores vs float64 oracle of the fp32 values"}
 
     fp8 = args.dtype == "fp8"
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
-    kern = "maxsim_scan_f8x4_kernel" if fp8 else SCAN_KERNEL
     if rank == 0:
         line = {
             "metric": "queries/sec + p50 retrieval latency, 1M-chunk corpus, top-10 rerank",
@@ -288,18 +418,28 @@ def main():
                                    "ColBERT MaxSim top-100 + RRF + rerank top-10",
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
-                       "parallelism": f"corpus sharded x{world}" + (" (RCCL all-gather + all-reduce)" if world > 1 else "")},
+                       "parallelism": f"corpus sharded x{world}" + (
+                           (" (RCCL all-gather + all-reduce, " + ("native in-ABI" if args.native_exchange
+                                                                  else "torch.distributed") + " exchange)")
+                           if world > 1 else "")},
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
+            "p99_ms_b1": round(p99, 3) if p99 is not None else None,
+            "latency_samples": len(lat),
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
-            "roofline": {"bound": "mfma", "kernel": kern, "achieved": round(achieved, 2),
+            "roofline": {"bound": "mfma", "kernel": want, "variant": variant, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic, "avg_ms": round(scan_avg, 3), "launches_timed": len(scan_ms),
                          "clock_ghz_under_load": round(clock, 3) if clock else None},
             "cpu_baseline": cpu,
-            "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad},
+            "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad,
+                       "oracle_checked_queries": len(check_rows), "oracle_tolerance": tol},
         }
         if band is not None:
             line["faithful_band"] = band
+        if fleg is not None:
+            line["faithful"] = fleg
+        if native is not None:
+            line["native_exchange"] = native
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

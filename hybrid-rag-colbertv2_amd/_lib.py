@@ -22,6 +22,7 @@ SCORER_REF_MEANPOOL_COSINE = 1
 SCORERS = {"maxsim": SCORER_MAXSIM, "ref_meanpool_cosine": SCORER_REF_MEANPOOL_COSINE}
 ERR_EINVAL, ERR_EUNSUPPORTED, ERR_EHIP, ERR_ESTATE = -1, -2, -3, -4
 F32_SCORE, F32_SEARCH, F32_RERANK = 0, 1, 2
+OPT_FUSED_TOPK, OPT_DYNAMIC_TAIL = 1, 2
 
 _p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
 _SIGS = {
@@ -38,6 +39,10 @@ _SIGS = {
     "cbv2_index_build_means": (ctypes.c_int, [_p, _p, _i32, _p, _p]),
     "cbv2_score": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _p, _i64, _p]),
     "cbv2_search_workspace_bytes": (_sz, [_p, _i32]),
+    "cbv2_search_workspace_size": (_sz, [_p, _i32, _i32, _i32]),
+    "cbv2_index_set_option": (ctypes.c_int, [_p, _i32, _i64]),
+    "cbv2_search_fused_slots": (_i64, [_p, _i32, _i32, _i32]),
+    "cbv2_index_last_scan_plan": (ctypes.c_int, [_p, _p]),
     "cbv2_search": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p]),
     "cbv2_rerank": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _p, _p, _p]),
     "cbv2_select_topk": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
@@ -52,6 +57,7 @@ _SIGS = {
     "cbv2_bm25_build_shard": (ctypes.c_int, [_p, _p, _i64, _i32, ctypes.c_float, ctypes.c_float, _i64, _i64,
                                              _i64, _p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_bm25_num_docs": (_i64, [_p]),
+    "cbv2_stem_en": (ctypes.c_int, [_p, _p, _i64, _p, _i64, _p]),
     "cbv2_index_file_info": (ctypes.c_int, [ctypes.c_char_p, _p, _p, _p]),
     "cbv2_index_file_write": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _p, _p, _p, _i64, _p]),
     "cbv2_index_file_read": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _p, _p, _p, _p]),

@@ -1,14 +1,30 @@
-"""Host-side lexical stage (stage 1 of HybridRetriever.retrieve, LRC:937-950).
+r"""Host-side lexical stage (stage 1 of HybridRetriever.retrieve, LRC:937-950).
 
-The reference uses ``bm25s`` with English stopwords and a Snowball stemmer
-(LRC:851-858, 939-945).  Neither bm25s nor PyStemmer is installed in this
-image.  This module keeps bm25s' object interface (``tokenize``, ``index``,
-``retrieve(query_tokens, k) -> (ids[nq, k], scores[nq, k])``, ``save``/``load``)
-and does the scoring natively: text -> term ids here (lower-case ``\\w+``,
-scikit-learn's English stopword list, no stemming), then the Lucene BM25
-index and multi-threaded search in C++ (csrc/host_bm25.cpp, k1=1.5, b=0.75,
-bm25s' defaults).  Parity with bm25s itself is UNPINNED; the C++ scoring is
-pinned bit-for-bit by oracle/oracle.py:bm25_topk.
+The reference builds and queries bm25s (LRC:851-858, 939-945):
+
+    tokens = bm25s.tokenize(texts, stopwords="en", stemmer=Stemmer.Stemmer("english"))
+    bm25s.BM25().index(tokens);  results, scores = retriever.retrieve(query_tokens, k)
+
+Neither bm25s nor PyStemmer is installed in this image.  This module restates
+that pipeline with the same shapes:
+
+  * ``tokenize`` -- bm25s.tokenize's semantics: lower-case, the default token
+    pattern ``(?u)\b\w\w+\b`` (Python's own regex engine, so \w is Unicode
+    \w exactly), stopwords dropped BEFORE stemming (bm25s' "en" list,
+    ``STOPWORDS_EN``), then the UNIQUE tokens stemmed once and mapped to stem
+    ids; returns ``Tokenized(ids, vocab)``.
+  * ``Stemmer("english")`` -- PyStemmer-shaped (``stemWord``/``stemWords``),
+    the Snowball English ("Porter2") algorithm in C++ (csrc/text_en.cpp).
+  * ``HostBM25`` -- bm25s.BM25-shaped (``index``/``retrieve``/``save``/``load``);
+    the Lucene BM25 index and multi-threaded search are C++
+    (csrc/host_bm25.cpp, k1=1.5, b=0.75, bm25s' defaults; a query's score sums
+    the postings of every query token, repeats included, as bm25s does).
+
+No fallback exists: a stopword list or stemmer other than these raises.
+Parity with bm25s / PyStemmer themselves is UNPINNED (no reference test or
+fixture touches BM25); the stemmer is pinned by the published Snowball sample
+vocabulary (tests/test_text_en.py) and the C++ scoring bit-for-bit by
+oracle/oracle.py:bm25_topk.
 LRC = local_rag_complete.py
 """
 from __future__ import annotations
@@ -17,18 +33,105 @@ import ctypes
 import json
 import os
 import re
-from typing import List, Optional, Sequence, Tuple, Union
+from typing import Dict, List, NamedTuple, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
 from . import _lib
 
-try:  # scikit-learn ships a standard English stopword list
-    from sklearn.feature_extraction.text import ENGLISH_STOP_WORDS as _STOP
-except Exception:  # pragma: no cover
-    _STOP = frozenset("a an and are as at be by for from has he in is it its of on that the to was were will with".split())
+# bm25s.stopwords.STOPWORDS_EN (what bm25s.tokenize(stopwords="en") uses): the
+# Lucene / Elasticsearch English stop set.
+STOPWORDS_EN = ("a", "an", "and", "are", "as", "at", "be", "but", "by", "for", "if", "in", "into", "is", "it", "no",
+                "not", "of", "on", "or", "such", "that", "the", "their", "then", "there", "these", "they", "this",
+                "to", "was", "will", "with")
+TOKEN_PATTERN = r"(?u)\b\w\w+\b"     # bm25s.tokenize's default
 
-_WORD = re.compile(r"\w+")
+
+class Stemmer:
+    """PyStemmer-shaped Snowball stemmer (``Stemmer.Stemmer("english")``), native."""
+
+    def __init__(self, algorithm: str = "english"):
+        if algorithm.lower() not in ("english", "en", "porter2"):
+            raise ValueError(f"only the Snowball English stemmer is built (got {algorithm!r})")
+        self.algorithm = "english"
+
+    def stemWords(self, words: Sequence[str]) -> List[str]:  # noqa: N802  (PyStemmer's name)
+        words = list(words)
+        if not words:
+            return []
+        enc = [w.encode("utf-8") for w in words]
+        offs = np.zeros(len(enc) + 1, np.int64)
+        offs[1:] = np.cumsum([len(b) for b in enc])
+        buf = b"".join(enc)
+        out = ctypes.create_string_buffer(max(len(buf), 1))
+        out_offs = np.zeros(len(enc) + 1, np.int64)
+        src = ctypes.create_string_buffer(buf, max(len(buf), 1))
+        _lib.check(_lib.lib().cbv2_stem_en(src, offs.ctypes.data, len(enc), out, len(buf), out_offs.ctypes.data))
+        raw = out.raw
+        return [raw[out_offs[i]:out_offs[i + 1]].decode("utf-8", errors="surrogateescape") for i in range(len(enc))]
+
+    def stemWord(self, word: str) -> str:  # noqa: N802
+        return self.stemWords([word])[0]
+
+    def __call__(self, words):
+        return self.stemWords(words)
+
+
+class Tokenized(NamedTuple):
+    """bm25s.tokenization.Tokenized: per-text token ids and the vocabulary."""
+    ids: List[List[int]]
+    vocab: Dict[str, int]
+
+
+def _stopword_set(stopwords) -> frozenset:
+    if stopwords in (None, False):
+        return frozenset()
+    if stopwords in ("en", "english", True):
+        return frozenset(STOPWORDS_EN)
+    if isinstance(stopwords, str):
+        raise ValueError(f"only the English stopword list is built (got {stopwords!r})")
+    return frozenset(stopwords)
+
+
+def tokenize(texts: Union[str, Sequence[str]], lower: bool = True, token_pattern: str = TOKEN_PATTERN,
+             stopwords="en", stemmer=None, return_ids: bool = True):
+    """bm25s.tokenize (the reference's LRC:851-855 / 939-943 call): one row per
+    text (an all-stopword or empty text gives an empty row, never a missing one)."""
+    if isinstance(texts, str):
+        texts = [texts]
+    split = re.compile(token_pattern).findall
+    stop = _stopword_set(stopwords)
+    token_to_index: Dict[str, int] = {}
+    rows = []
+    for text in texts:
+        if lower:
+            text = text.lower()
+        row = []
+        for tok in split(text):
+            if tok in stop:
+                continue
+            tid = token_to_index.get(tok)
+            if tid is None:
+                tid = token_to_index[tok] = len(token_to_index)
+            row.append(tid)
+        rows.append(row)
+    unique = list(token_to_index)
+    if stemmer is not None:
+        fn = stemmer.stemWords if hasattr(stemmer, "stemWords") else stemmer
+        stems = fn(unique)
+        vocab: Dict[str, int] = {}
+        remap = []
+        for st in stems:
+            if st not in vocab:
+                vocab[st] = len(vocab)
+            remap.append(vocab[st])
+        rows = [[remap[t] for t in row] for row in rows]
+    else:
+        vocab = token_to_index
+    if return_ids:
+        return Tokenized(rows, vocab)
+    inv = {v: k for k, v in vocab.items()}
+    return [[inv[t] for t in row] for row in rows]
 
 
 def to_csr(rows: Sequence[Sequence[int]]) -> Tuple[np.ndarray, np.ndarray]:
@@ -123,20 +226,36 @@ def sharded(doc_terms: np.ndarray, doc_offsets: np.ndarray, vocab: int, id_base:
 
 
 class HostBM25:
-    """bm25s-shaped object: tokenize -> index -> retrieve, scoring in C++."""
+    """bm25s.BM25-shaped host index (LRC:857-861 index/save, 878 load, 945 retrieve):
+    ``index(tokenize(corpus, ...))``, ``retrieve(tokenize(query, ...), k)``;
+    the BM25 index and search are C++ (NativeBM25)."""
 
-    def __init__(self, k1: float = 1.5, b: float = 0.75, stopwords: bool = True):
-        self.k1, self.b, self.stopwords = k1, b, stopwords
-        self.vocab = {}
+    def __init__(self, k1: float = 1.5, b: float = 0.75, stemmer: Optional[Stemmer] = None, stopwords="en"):
+        self.k1, self.b = k1, b
+        self.stemmer = stemmer if stemmer is not None else Stemmer("english")
+        self.stopwords = stopwords
+        self.vocab: Dict[str, int] = {}
         self.n_docs = 0
         self._native: Optional[NativeBM25] = None
         self._corpus: Optional[Tuple[np.ndarray, np.ndarray]] = None
 
     # ---------------------------------------------------------------- text
-    def tokenize(self, text: Union[str, Sequence[str]]):
-        if isinstance(text, str):
-            return [w for w in _WORD.findall(text.lower()) if not (self.stopwords and w in _STOP)]
-        return [self.tokenize(t) for t in text]
+    def tokenize(self, texts: Union[str, Sequence[str]]) -> Tokenized:
+        """The reference's bm25s.tokenize call: stopwords "en", Snowball English."""
+        _stopword_set(self.stopwords)
+        return tokenize(texts, stopwords=self.stopwords, stemmer=self.stemmer)
+
+    @staticmethod
+    def _rows(tokens) -> List[List[str]]:
+        """Tokenized -> token strings per text; a list of strings is ONE text."""
+        if isinstance(tokens, Tokenized) or (isinstance(tokens, tuple) and len(tokens) == 2
+                                             and isinstance(tokens[1], dict)):
+            inv = {v: k for k, v in tokens[1].items()}
+            return [[inv[t] for t in row] for row in tokens[0]]
+        tokens = list(tokens)
+        if not tokens or isinstance(tokens[0], str):
+            return [tokens]
+        return [list(r) for r in tokens]
 
     def _ids(self, toks: Sequence[str], grow: bool) -> List[int]:
         out = []
@@ -145,21 +264,24 @@ class HostBM25:
             if v is None and grow:
                 v = self.vocab[t] = len(self.vocab)
             if v is not None:
-                out.append(v)
+                out.append(v)          # tokens unknown to the index are dropped (bm25s' get_tokens_ids)
         return out
 
     # ---------------------------------------------------------------- index
-    def index(self, corpus_tokens: List[List[str]]) -> None:
-        rows = [self._ids(toks, grow=True) for toks in corpus_tokens]
+    def index(self, corpus_tokens) -> None:
+        self.vocab = {}
+        rows = [self._ids(toks, grow=True) for toks in self._rows(corpus_tokens)]
         self._corpus = to_csr(rows)
         self.n_docs = len(rows)
         self._native = NativeBM25(*self._corpus, len(self.vocab), self.k1, self.b)
 
-    def retrieve(self, query_tokens, k: int = 10):
-        if query_tokens and isinstance(query_tokens[0], str):
-            query_tokens = [query_tokens]
-        q, off = to_csr([self._ids(t, grow=False) for t in query_tokens])
-        ids, sc = self._native.search(q, off, k)
+    def retrieve(self, query_tokens, k: int = 10, n_threads: int = 0):
+        """-> (doc ids int64 [n_queries, k], scores float32 [n_queries, k]); rows with no
+        scoring term pad with the lowest-id zero-score docs (then -1 past the corpus)."""
+        if self._native is None:
+            raise RuntimeError("BM25 index not built: call index() or load() first")
+        q, off = to_csr([self._ids(t, grow=False) for t in self._rows(query_tokens)])
+        ids, sc = self._native.search(q, off, k, n_threads)
         return ids.astype(np.int64), sc
 
     # ---------------------------------------------------------------- persistence
@@ -168,13 +290,14 @@ class HostBM25:
         np.savez(os.path.join(path, "bm25_corpus.npz"), terms=self._corpus[0], offsets=self._corpus[1])
         with open(os.path.join(path, "bm25.json"), "w") as f:
             json.dump({"vocab": self.vocab, "n_docs": self.n_docs, "k1": self.k1, "b": self.b,
-                       "stopwords": self.stopwords}, f)
+                       "stopwords": self.stopwords if isinstance(self.stopwords, (str, bool)) or self.stopwords is None
+                       else list(self.stopwords), "stemmer": "english"}, f)
 
     @classmethod
     def load(cls, path: str) -> "HostBM25":
         with open(os.path.join(path, "bm25.json")) as f:
             meta = json.load(f)
-        self = cls(meta["k1"], meta["b"], meta["stopwords"])
+        self = cls(meta["k1"], meta["b"], stopwords=meta.get("stopwords", "en"))
         self.vocab, self.n_docs = meta["vocab"], meta["n_docs"]
         z = np.load(os.path.join(path, "bm25_corpus.npz"))
         self._corpus = (z["terms"], z["offsets"])

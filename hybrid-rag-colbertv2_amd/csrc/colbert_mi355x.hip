@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 #include <stdio.h>
 #include <string.h>
@@ -537,6 +538,104 @@ __device__ __forceinline__ void iter4_ragged(const uint8_t* buf, int lane, int j
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused top-k (SURVEY §7 hard part (ii)): instead of writing the [B, n] score
+// matrix, each wave keeps, per query it owns, a buffer of up to FK ranking
+// keys (score bits << 32 | ~local doc index: unique, larger = better) in its
+// own LDS region, with a threshold key and a count beside it (LDS too: the
+// scan kernels have no SGPRs or VGPRs to spare).  A 64-doc epilogue block
+// offers its keys; those above the threshold are appended.  When a buffer
+// would overflow, the wave finds its k-th largest key by a bitwise binary
+// search over ballot counts (64 steps, scalar work: 2 keys per lane, no sort,
+// ~4 VGPRs) and keeps the k keys >= it, which becomes the threshold.  No
+// barrier is involved: a buffer belongs to one wave.  After its last doc range
+// the workgroup writes its best k keys per query to part[query][slot][k]
+// (slot = its chunk in its query group; key 0 = padding) and
+// select_keys_kernel picks each query's top-k over the slots.  Keys compare as
+// the unfused (score desc, index asc) rule does, so the ids equal the unfused
+// path's bit for bit.
+// ---------------------------------------------------------------------------
+constexpr int kFusedCap = 120;                    // keys per (wave, query) buffer (<= 128: 2 per lane)
+constexpr int kFusedMaxK = kFusedCap - 16;        // appends go in 16-lane batches after a compaction
+constexpr int kFusedStateBytes = 16;              // per (wave, query): threshold u64, count i32
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Keep the best min(cnt, k) keys of buf[0..cnt) (this wave's LDS buffer, cnt
+// <= 128) at buf[0..), unordered; thr = the k-th largest key once k are held.
+__device__ __forceinline__ void topk_compact(uint64_t* buf, int& cnt, uint64_t& thr, int k, int lane) {
+  if (cnt <= k) {
+    if (cnt == k) {  // threshold = the smallest held key
+      uint64_t m = lane < cnt ? buf[lane] : ~0ull;
+      const uint64_t m2 = lane + 64 < cnt ? buf[lane + 64] : ~0ull;
+      m = m < m2 ? m : m2;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), off) << 32) |
+                           (uint32_t)__shfl_xor((int)(uint32_t)m, off);
+        m = m < o ? m : o;
+      }
+      thr = uniform64(m);
+    }
+    return;
+  }
+  const uint64_t a = lane < cnt ? buf[lane] : 0ull;
+  const uint64_t b = lane + 64 < cnt ? buf[lane + 64] : 0ull;
+  uint64_t T = 0;  // largest T with count(key >= T) >= k: the k-th largest (keys are unique)
+#pragma unroll 1
+  for (int bit = 63; bit >= 0; --bit) {
+    const uint64_t t = T | (1ull << bit);
+    const int c = __popcll(__ballot(a >= t)) + __popcll(__ballot(b >= t));
+    if (c >= k) T = t;
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint64_t ma = __ballot(a >= T), mb = __ballot(b >= T);
+  if (a >= T) buf[__popcll(ma & below)] = a;
+  if (b >= T) buf[__popcll(ma) + __popcll(mb & below)] = b;
+  thr = T;
+  cnt = k;
+}
+
+// Offer one key per lane (0 = none) to the buffer of one (wave, query).
+template <int FK>
+__device__ __forceinline__ void topk_offer(uint64_t* buf, uint8_t* state, int k, uint64_t key, int lane) {
+  uint64_t thr = uniform64(*reinterpret_cast<const uint64_t*>(state));
+  const uint64_t mask = __ballot(key > thr);
+  const int np = __popcll(mask);
+  if (np == 0) return;
+  int cnt = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(state + 8));
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (cnt + np <= FK) {
+    if (key > thr) buf[cnt + __popcll(mask & below)] = key;
+    cnt += np;
+  } else {
+#pragma unroll 1
+    for (int h = 0; h < 4; ++h) {  // 16 lanes at a time: cnt <= k + 16 <= FK after a compaction
+      const bool mine = (lane >> 4) == h;
+      const int nh = __popcll(__ballot(mine && key > thr));
+      if (nh == 0) continue;
+      if (cnt + nh > FK) topk_compact(buf, cnt, thr, k, lane);
+      const uint64_t m3 = __ballot(mine && key > thr);
+      if (mine && key > thr) buf[cnt + __popcll(m3 & below)] = key;
+      cnt += __popcll(m3);
+    }
+    if (lane == 0) *reinterpret_cast<uint64_t*>(state) = thr;
+  }
+  if (lane == 0) *reinterpret_cast<int*>(state + 8) = cnt;
+}
+
+// End of a workgroup's work: its best k keys of one query to dst[0..k) (0-padded).
+__device__ __forceinline__ void topk_flush(uint64_t* buf, uint8_t* state, int k, uint64_t* dst, int lane) {
+  uint64_t thr = uniform64(*reinterpret_cast<const uint64_t*>(state));
+  int cnt = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(state + 8));
+  if (cnt > k) topk_compact(buf, cnt, thr, k, lane);
+  for (int e = lane; e < k; e += 64) dst[e] = e < cnt ? buf[e] : 0ull;
+}
+
 // Dynamic-tail task grab (one thread): writes (doc offset into the tail, size;
 // size 0 = done) to slot[0..1].  task_docs > 0: fixed tasks, the counter counts
 // tasks; task_docs < 0: guided, the counter counts docs and a task takes
@@ -576,13 +675,15 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
 // next iteration one per tile from inside the MFMA stream, instead of all at
 // once after the barrier, where every wave of the CU queues on the address
 // path at the same moment (lab phase stamps: ~1.2k issue cycles/iteration).
+// FK > 0: fused top-k (see topk_offer): no score matrix; each workgroup writes
+// its best topk_k keys per query to part[qi][slot][topk_k] (slot = its chunk).
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
-          bool SPREAD = false>
+          bool SPREAD = false, int FK = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
     int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr, int task_docs,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0) {
   // TPI tokens of 4 docs per iteration (32: 32 KiB, 64: 64 KiB), IPG per group
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kRowBytes;
@@ -594,12 +695,17 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
   // one LDS object only: with a second __shared__ array hipcc starts putting
   // vmcnt(0) before the ring's ds_reads (LDS-DMA alias tracking)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterBytes + 16];
+  // fused top-k: one key buffer + state per (wave, query), after the task slots
+  constexpr int kCandBytes = FK > 0 ? QPB * (FK * 8 + kFusedStateBytes) : 0;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterBytes + 16 + kCandBytes];
   int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterBytes);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
+  uint64_t* const cand = reinterpret_cast<uint64_t*>(smem + NBUF * kIterBytes + 16) + (size_t)wave * QW * (FK > 0 ? FK : 1);
+  uint8_t* const tk_state = smem + NBUF * kIterBytes + 16 + (FK > 0 ? QPB * FK * 8 : 0) + wave * QW * kFusedStateBytes;
+  if (FK > 0 && lane < 2 * QW) reinterpret_cast<uint64_t*>(tk_state)[lane] = 0ull;  // thr = 0, cnt = 0
   const int nq_groups = (B + QPB - 1) / QPB;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
@@ -736,12 +842,22 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           }
           if ((G & 15) == 15 || G == ngr - 1) {
             const int dd = 64 * (G >> 4) + 4 * c + g;
+            if constexpr (FK > 0) {
 #pragma unroll
-            for (int q = 0; q < QW; ++q) {
-              const int qi = qg * QPB + wave * QW + q;
-              if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+              for (int q = 0; q < QW; ++q) {
+                if (qg * QPB + wave * QW + q >= B) continue;   // wave-uniform
+                const uint32_t loc = (uint32_t)(d_begin + dd);
+                const uint64_t key = (c <= (G & 15) && dd < nd) ? ((uint64_t)f2u(sc[q]) << 32) | (uint32_t)~loc : 0ull;
+                topk_offer<FK>(cand + q * FK, tk_state + q * kFusedStateBytes, topk_k, key, lane);
+              }
+            } else {
+#pragma unroll
+              for (int q = 0; q < QW; ++q) {
+                const int qi = qg * QPB + wave * QW + q;
+                if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+              }
+              stored = true;
             }
-            stored = true;
           }
         }
       }
@@ -757,6 +873,15 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     d_begin = static_docs + (int64_t)o;
     if (sz <= 0 || d_begin >= n) break;
     d_end = d_begin + sz < n ? d_begin + sz : n;
+  }
+  if constexpr (FK > 0) {  // this workgroup's best topk_k per query; key 0 pads
+#pragma unroll 1
+    for (int q = 0; q < QW; ++q) {
+      const int qi = qg * QPB + wave * QW + q;
+      if (qi >= B) continue;
+      topk_flush(cand + q * FK, tk_state + q * kFusedStateBytes, topk_k,
+                 part + ((size_t)qi * nslots + (size_t)chunk) * topk_k, lane);
+    }
   }
   if constexpr (STAMPS) {
     if (ph_t) ph_comp += __builtin_amdgcn_s_memtime() - ph_t;
@@ -1153,12 +1278,13 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
   }
 }
 
-template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2>   // D = 2 spills at QW = 8
+template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
+          int FK = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
     float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr,
-    int task_docs) {
+    int task_docs, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0) {
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kDim;                 // e4m3 bytes per iteration
   constexpr int kIterStage = kIterBytes + 4 * TPI * 2;        // + 2 scale bytes per row
@@ -1169,12 +1295,18 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   static_assert(TPI == 32 || TPI == 64 || TPI == 128, "32, 64 or 128 tokens per iteration");
   static_assert(kPieces % WAVES == 0 && kScaleDma <= WAVES, "pieces must split evenly over waves");
   static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterStage + 256 + 16];
+  constexpr int kCandBytes = FK > 0 ? QPB * (FK * 8 + kFusedStateBytes) : 0;   // fused top-k buffers + state
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterStage + 256 + 16 + kCandBytes];
   int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterStage + 256);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
+  uint64_t* const cand =
+      reinterpret_cast<uint64_t*>(smem + NBUF * kIterStage + 256 + 16) + (size_t)wave * QW * (FK > 0 ? FK : 1);
+  uint8_t* const tk_state =
+      smem + NBUF * kIterStage + 256 + 16 + (FK > 0 ? QPB * FK * 8 : 0) + wave * QW * kFusedStateBytes;
+  if (FK > 0 && lane < 2 * QW) reinterpret_cast<uint64_t*>(tk_state)[lane] = 0ull;
   const int nq_groups = (B + QPB - 1) / QPB;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
@@ -1274,12 +1406,22 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       }
       if ((G & 15) == 15 || G == ngr - 1) {
         const int dd = 64 * (G >> 4) + 4 * c + g;
+        if constexpr (FK > 0) {
 #pragma unroll
-        for (int q = 0; q < QW; ++q) {
-          const int qi = qg * QPB + wave * QW + q;
-          if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+          for (int q = 0; q < QW; ++q) {
+            if (qg * QPB + wave * QW + q >= B) continue;   // wave-uniform
+            const uint32_t loc = (uint32_t)(d_begin + dd);
+            const uint64_t key = (c <= (G & 15) && dd < nd) ? ((uint64_t)f2u(sc[q]) << 32) | (uint32_t)~loc : 0ull;
+            topk_offer<FK>(cand + q * FK, tk_state + q * kFusedStateBytes, topk_k, key, lane);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < QW; ++q) {
+            const int qi = qg * QPB + wave * QW + q;
+            if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
+          }
+          stored = true;
         }
-        stored = true;
       }
     }
   }
@@ -1292,6 +1434,15 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     d_begin = static_docs + (int64_t)o;
     if (sz <= 0 || d_begin >= n) break;
     d_end = d_begin + sz < n ? d_begin + sz : n;
+  }
+  if constexpr (FK > 0) {
+#pragma unroll 1
+    for (int q = 0; q < QW; ++q) {
+      const int qi = qg * QPB + wave * QW + q;
+      if (qi >= B) continue;
+      topk_flush(cand + q * FK, tk_state + q * kFusedStateBytes, topk_k,
+                 part + ((size_t)qi * nslots + (size_t)chunk) * topk_k, lane);
+    }
   }
 }
 
@@ -1602,6 +1753,67 @@ __global__ __launch_bounds__(kTkThreads) void topk_select_kernel(const float* __
     topk_exact_row(scores + (size_t)row * ld, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
   }
   sort_and_write(sel, m, k, id_base, out_s + (size_t)row * k, out_i + (size_t)row * k);
+}
+
+// ---------------------------------------------------------------------------
+// Top-k of the fused scan's per-workgroup lists: row b holds M = slots * k
+// unique 64-bit ranking keys (0 = padding).  Exact radix select of the
+// kk = min(k, M)-th largest key (8 passes of 8-bit digits over the keys in
+// global memory / L2), then the kk keys >= it (exactly kk: keys are unique)
+// sorted in LDS; a 0 key is written as (-inf, -1).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTkThreads) void select_keys_kernel(const uint64_t* __restrict__ keys, int64_t M,
+                                                                 int64_t row_stride, int k, int64_t id_base,
+                                                                 float* __restrict__ out_s,
+                                                                 int32_t* __restrict__ out_i) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sel[kTopkMax];
+  __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const uint64_t* x = keys + (size_t)blockIdx.x * row_stride;
+  const int kk = (int)((int64_t)k < M ? k : M);
+  uint64_t prefix = 0, mask = 0;
+  uint32_t kleft = (uint32_t)kk;
+  for (int p = 0; p < 8; ++p) {
+    const int shift = 56 - 8 * p;
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < M; i += kTkThreads) {
+      const uint64_t u = x[i];
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (wave == 0) find_bin(hist, 256, kleft, &s_bin, &s_above, &s_bincount);
+    __syncthreads();
+    kleft -= s_above;
+    prefix |= (uint64_t)s_bin << shift;
+    mask |= 255ull << shift;
+    __syncthreads();
+  }
+  // the kk keys >= the kk-th largest (unique, except padding zeros: when the
+  // kk-th largest is 0 only the nonzero keys are collected, the rest pad)
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (int64_t i = tid; i < M; i += kTkThreads) {
+    const uint64_t u = x[i];
+    if (u >= prefix && u != 0ull) {
+      const uint32_t pos = atomicAdd(&s_cnt, 1u);
+      if (pos < (uint32_t)kk) sel[pos] = u;
+    }
+  }
+  __syncthreads();
+  const int got = (int)(s_cnt < (uint32_t)kk ? s_cnt : (uint32_t)kk);
+  int P = 1;
+  while (P < kk) P <<= 1;
+  for (int i = got + tid; i < P; i += kTkThreads) sel[i] = 0;
+  bitonic_desc(sel, P);
+  float* os = out_s + (size_t)blockIdx.x * k;
+  int32_t* oi = out_i + (size_t)blockIdx.x * k;
+  for (int j = tid; j < k; j += kTkThreads) {
+    const uint64_t key = j < kk ? sel[j] : 0ull;
+    os[j] = key ? u2f((uint32_t)(key >> 32)) : neg_inf();
+    oi[j] = key ? (int32_t)(id_base + (int64_t)(~(uint32_t)key)) : -1;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2141,11 +2353,22 @@ struct cbv2_index {
   const float* doc_means;
   int32_t dtype;           // CBV2_DTYPE_BF16 or CBV2_DTYPE_MXFP8
   const uint8_t* scales;   // MXFP8: E8M0 [n][128][2]
-  // Dynamic-tail task counters of the B > 16 scans: a ring of slots, one per
-  // launch (zeroed on the launch's stream), owned by the handle; nullptr =
-  // static split only.
+  // Dynamic-tail task counters.  cbv2_search (and everything built on it)
+  // takes them from the caller's workspace, so concurrent calls on distinct
+  // streams never share a counter.  cbv2_score has no workspace: it uses a
+  // ring of slots owned by the handle, one per launch, each zeroed on the
+  // launch's stream; before a slot is reused, the new launch's stream waits
+  // for the event recorded after the slot's previous launch (ring_ev), so
+  // slot reuse is ordered across streams.  nullptr = static split only.
   int* task_ring = nullptr;
   uint32_t task_seq = 0;
+  hipEvent_t ring_ev[128] = {};
+  bool ring_ev_used[128] = {};
+  // Work split of the most recent scan launch (cbv2_index_last_scan_plan).
+  int64_t last_plan[4] = {0, 0, 0, 0};
+  bool fused_topk = true;    // CBV2_OPT_FUSED_TOPK
+  bool dynamic_tail = true;  // CBV2_OPT_DYNAMIC_TAIL
+  std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
   // max ||hi||); nullptr = plain bf16 index.
@@ -2194,16 +2417,29 @@ struct DeviceGuard {
   }
 };
 
-constexpr int kRingSlots = 128;   // launches in flight before a slot is reused
+constexpr int kRingSlots = 128;   // cbv2_score launches in flight before a slot is reused
 constexpr int kRingInts = 64;     // query groups per launch with a dynamic tail (B <= 64 * 32)
+constexpr size_t kCtrBytes = 256; // counter block at the head of a search workspace (kRingInts ints)
 
-// The handle's task-counter ring (index creation; failure leaves the static split).
+// The handle's task-counter ring and its per-slot events (index creation;
+// failure leaves cbv2_score on the static split).
 void alloc_task_ring(cbv2_index* ix) {
   if (ix->n == 0) return;
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(ix->device) != hipSuccess) return;
   void* p = nullptr;
-  if (hipMalloc(&p, (size_t)kRingSlots * kRingInts * sizeof(int)) == hipSuccess) ix->task_ring = (int*)p;
+  if (hipMalloc(&p, (size_t)kRingSlots * kRingInts * sizeof(int)) == hipSuccess) {
+    bool ok = true;
+    for (int s = 0; s < kRingSlots && ok; ++s)
+      ok = hipEventCreateWithFlags(&ix->ring_ev[s], hipEventDisableTiming) == hipSuccess;
+    if (ok) {
+      ix->task_ring = (int*)p;
+    } else {
+      for (int s = 0; s < kRingSlots; ++s)
+        if (ix->ring_ev[s]) (void)hipEventDestroy(ix->ring_ev[s]), ix->ring_ev[s] = nullptr;
+      (void)hipFree(p);
+    }
+  }
   (void)hipSetDevice(prev);
 }
 
@@ -2272,31 +2508,59 @@ constexpr int kScanTaskDocs = -16;     // guided: tasks shrink to 16 docs at the
 // B <= 16 (one query group, two 4-wave workgroups per CU): a larger dynamic
 // share.  Lab, 1M docs, B=16: tail loss 9.7 % at 0.1 (per-workgroup stamps;
 // clocks 1.57-1.70 GHz across XCDs under streaming); 12.41 -> 11.76 ms at 0.3
-// (-5.2 %), 1.479 -> 1.439 ms at 125k; 0.5 and 1.0 lose at 1M (14.2 / 16.2
-// ms).  B=64 is flat in the fraction (36.87-36.90 ms), so B > 16 keeps 0.1.
+// (-5.2 %); 0.5 and 1.0 lose at 1M (14.2 / 16.2 ms).  B=64 is flat in the
+// fraction (36.87-36.90 ms), so B > 16 keeps 0.1.  (Round 1's "125k: 1.479 ->
+// 1.439 ms" was noise: the tail only switched on from 262,144 docs at B <= 16
+// then; it now switches on whenever each static chunk keeps >= 64 docs.)
 constexpr float kScanDynFracSmallB = 0.30f;
+constexpr int64_t kMinChunkDocs = 64;
+
+// Fused top-k output of one scan launch: part [B][max_slots][k] keys; the
+// launch records how many slots (chunks per query group) it wrote.
+struct FusedTopk {
+  uint64_t* part = nullptr;
+  int k = 0;
+  int64_t max_slots = 0;
+  int64_t slots = 0;
+};
 
 // Work split of one launch: n_chunks static chunks of chunk_docs per query
-// group over [0, static_docs), the rest as dynamic tasks on a fresh counter slot.
+// group over [0, static_docs), the rest as dynamic tasks on a zeroed counter
+// block (the caller's workspace, or a ring slot of the handle).
 struct ScanSplit {
   int64_t n_chunks = 1, chunk_docs = 0, static_docs = 0;
   int* ctr = nullptr;
   int task_docs = 0;
+  int ring_slot = -1;   // >= 0: the handle's ring slot, released by finish_split
 };
 
 int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, int task_docs, hipStream_t st,
-               ScanSplit* sp) {
+               ScanSplit* sp, int* ctr_ws) {
   int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
   if (n_chunks < 1) n_chunks = 1;
   if (n_chunks > ix->n) n_chunks = ix->n;
   sp->task_docs = task_docs > 0 ? std::max(64, task_docs & ~63) : -std::max(16, (-task_docs) & ~15);
   sp->ctr = nullptr;
-  if (ix->task_ring != nullptr && dyn_frac > 0.0f && nq_groups <= kRingInts &&
-      ix->n >= std::max<int64_t>(512, 4 * (int64_t)std::abs(sp->task_docs)) * n_chunks) {
-    sp->chunk_docs = ((int64_t)((double)ix->n * (1.0 - (double)dyn_frac)) / n_chunks) & ~(int64_t)63;
+  sp->ring_slot = -1;
+  const int64_t tail_chunk = ((int64_t)((double)ix->n * (1.0 - (double)dyn_frac)) / n_chunks) & ~(int64_t)63;
+  const bool have_ctr = ctr_ws != nullptr || ix->task_ring != nullptr;
+  if (have_ctr && ix->dynamic_tail && dyn_frac > 0.0f && nq_groups <= kRingInts && tail_chunk >= kMinChunkDocs) {
+    sp->chunk_docs = tail_chunk;
     sp->static_docs = sp->chunk_docs * n_chunks;
-    const uint32_t slot = __atomic_fetch_add(&ix->task_seq, 1u, __ATOMIC_RELAXED) % kRingSlots;
-    sp->ctr = ix->task_ring + (size_t)slot * kRingInts;
+    if (ctr_ws != nullptr) {
+      sp->ctr = ctr_ws;
+    } else {
+      const uint32_t slot = __atomic_fetch_add(&ix->task_seq, 1u, __ATOMIC_RELAXED) % kRingSlots;
+      bool wait = false;
+      {
+        std::lock_guard<std::mutex> lk(ix->mu);
+        wait = ix->ring_ev_used[slot];
+      }
+      // the slot's previous launch (maybe on another stream) must be done with it
+      if (wait) CBV2_HIP(hipStreamWaitEvent(st, ix->ring_ev[slot], 0));
+      sp->ctr = ix->task_ring + (size_t)slot * kRingInts;
+      sp->ring_slot = (int)slot;
+    }
     CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sizeof(int), st));
   } else {
     sp->chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
@@ -2305,21 +2569,52 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
   }
   sp->n_chunks = n_chunks;
   if ((int64_t)nq_groups * n_chunks > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  ix->last_plan[0] = (int64_t)nq_groups * n_chunks;
+  ix->last_plan[1] = sp->chunk_docs;
+  ix->last_plan[2] = sp->static_docs;
+  ix->last_plan[3] = sp->ctr != nullptr ? 1 : 0;
   return CBV2_OK;
 }
 
-template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false>
+// After the launch: a ring slot's event marks when its counters are free again.
+int finish_split(cbv2_index* ix, const ScanSplit& sp, hipStream_t st) {
+  if (sp.ring_slot < 0) return CBV2_OK;
+  CBV2_HIP(hipEventRecord(ix->ring_ev[sp.ring_slot], st));
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->ring_ev_used[sp.ring_slot] = true;
+  return CBV2_OK;
+}
+
+// Static chunks per query group of a launch (plan_split's first step): the
+// slot count a fused top-k launch writes at most.
+int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
+  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  if (n_chunks < 1) n_chunks = 1;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  return n_chunks;
+}
+
+template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
+          int FK = 0>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
-                    float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr) {
+                    float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
+                    int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   ScanSplit sp;
-  const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
+  int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp, ctr_ws);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD>), dim3((unsigned)(nq_groups * sp.n_chunks)),
-                     dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens, ix->n, Q, B, lq, out, ld_out, sp.chunk_docs,
-                     sp.static_docs, sp.ctr, sp.task_docs, stamps);
-  return launch_check("maxsim_scan16x4_kernel");
+  if (FK > 0) {
+    if (ft == nullptr || ft->k < 1 || ft->k > FK - 16 || sp.n_chunks > ft->max_slots)
+      return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
+    ft->slots = sp.n_chunks;
+  }
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK>),
+                     dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
+                     ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
+                     ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0);
+  if ((rc = launch_check("maxsim_scan16x4_kernel"))) return rc;
+  return finish_split(ix, sp, st);
 }
 
 template <int QW>
@@ -2340,8 +2635,11 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
 }
 
 int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
-                int variant = kDefaultScan) {
+                int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   if (ix->n == 0) return CBV2_OK;
+  if (ft != nullptr)   // fused top-k: the B > 16 doc-interleaved scan only (fused_eligible)
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap>(ix, Q, B, lq, nullptr, 0, st, kScanDynFrac,
+                                                                         kScanTaskDocs, nullptr, ctr_ws, ft);
   if (variant == kScanAuto)
     variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2)
                                : (B <= kSmallLdsMaxB ? kScan16x4W4 : kScan16x4W8);
@@ -2369,9 +2667,11 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16W4Q2:
       return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
     case kScan16x4W8:
-      return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, Q, B, lq, out, ld_out, st);
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs,
+                                                        nullptr, ctr_ws);
     case kScan16x4W4:
-      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB);
+      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
     default:
       return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
   }
@@ -2382,25 +2682,36 @@ constexpr int kF8Waves = 8, kF8QW = 8;
 
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
-template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves>
+template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
+          int FK = 0>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
-                hipStream_t st, float dyn_frac, int task_docs) {
+                hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   ScanSplit sp;
-  const int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp);
+  int rc = plan_split(ix, nq_groups, (int64_t)PER_CU * cu_count(ix->device), dyn_frac, task_docs, st, &sp, ctr_ws);
   if (rc != CBV2_OK) return rc;
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC>),
+  if (FK > 0) {
+    if (ft == nullptr || ft->k < 1 || ft->k > FK - 16 || sp.n_chunks > ft->max_slots)
+      return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
+    ft->slots = sp.n_chunks;
+  }
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC, FK>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
-                     sp.task_docs);
-  return launch_check("maxsim_scan_f8x4_kernel");
+                     sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0);
+  if ((rc = launch_check("maxsim_scan_f8x4_kernel"))) return rc;
+  return finish_split(ix, sp, st);
 }
 
 int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
-            float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, int shape = 0) {
+            float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, int shape = 0, int* ctr_ws = nullptr,
+            FusedTopk* ft = nullptr) {
   if (ix->n == 0) return CBV2_OK;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+  if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
+    return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st, dyn_frac,
+                                                                      task_docs, ctr_ws, ft);
   if (B <= kF8DirectMaxB) {
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
@@ -2420,21 +2731,36 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   // 1 = the same without PF, 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 /
   // 2-deep (2-4 spill at 8 queries per wave), 5 = 0, 6 = 2 with PF
   switch (shape) {
-    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    case 5: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 5: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
 #ifdef CBV2_LAB
     // lab, 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave,
     // three workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two
     // workgroups per CU (2 waves per SIMD from independent barrier domains)
-    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
-    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
 #endif
-    default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs);
+    default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
   }
+}
+
+// Fused top-k eligibility of a search, and the slot count its workspace
+// holds (0 = the unfused path: score matrix + row top-k).  The doc-interleaved
+// scans only (bf16 B > 16, MXFP8 B > 8): the small-batch scans write B*n
+// scores, a few MB, and the selection over their many per-wave lists would
+// cost more than the matrix.
+int64_t fused_slots(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) {
+  if (!ix->fused_topk || scorer != CBV2_SCORER_MAXSIM || ix->n == 0 || k > kFusedMaxK) return 0;
+  if (ix->dtype == CBV2_DTYPE_MXFP8) {
+    if (B <= kF8DirectMaxB) return 0;
+    return scan_chunks(ix, (B + kF8Waves * kF8QW - 1) / (kF8Waves * kF8QW), cu_count(ix->device));
+  }
+  if (B <= kSmallLdsMaxB) return 0;
+  return scan_chunks(ix, (B + 31) / 32, cu_count(ix->device));
 }
 
 int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
@@ -2467,9 +2793,11 @@ int check_query(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   return CBV2_OK;
 }
 
-// Start/stop events of the next timed scan (nullptr when timing is off or an
-// event cannot be created: the scan then runs untimed).
+// Start/stop events of the next timed scan, reserved under the handle's mutex
+// (false when timing is off or an event cannot be created: the scan then runs
+// untimed).
 bool scan_event_pair(cbv2_index* ix, hipEvent_t* e0, hipEvent_t* e1) {
+  std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->time_scans) return false;
   const size_t i = ix->scan_ev_used;
   while (ix->scan_ev.size() < 2 * i + 2) {
@@ -2479,27 +2807,26 @@ bool scan_event_pair(cbv2_index* ix, hipEvent_t* e0, hipEvent_t* e1) {
   }
   *e0 = ix->scan_ev[2 * i];
   *e1 = ix->scan_ev[2 * i + 1];
+  ++ix->scan_ev_used;
   return true;
 }
 
 int scan_maxsim_timed(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, float* out, int64_t ld_out,
-                      hipStream_t st) {
+                      hipStream_t st, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timed = scan_event_pair(ix, &e0, &e1);
   if (timed && hipEventRecord(e0, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
-  const int rc = ix->dtype == CBV2_DTYPE_MXFP8 ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st)
-                                               : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st);
-  if (rc) return rc;
-  if (timed) {
-    if (hipEventRecord(e1, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
-    ++ix->scan_ev_used;
-  }
-  return CBV2_OK;
+  const int rc = ix->dtype == CBV2_DTYPE_MXFP8
+                     ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs, 0, ctr_ws, ft)
+                     : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st, kDefaultScan, ctr_ws, ft);
+  // the stop event is recorded even after a failed launch, so the reserved pair stays readable
+  if (timed && hipEventRecord(e1, st) != hipSuccess && rc == CBV2_OK) return fail(CBV2_EHIP, "hipEventRecord failed");
+  return rc;
 }
 
 int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t lq, float* out,
-               int64_t ld_out, hipStream_t st) {
-  if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim_timed(ix, Q, B, lq, out, ld_out, st);
+               int64_t ld_out, hipStream_t st, int* ctr_ws = nullptr) {
+  if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim_timed(ix, Q, B, lq, out, ld_out, st, ctr_ws);
   return scan_meanpool(ix, (const float*)Q, B, lq, out, ld_out, st);
 }
 
@@ -2550,6 +2877,7 @@ int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
 // fp32-faithful path: workspace layout and the three operations.
 // ---------------------------------------------------------------------------
 struct F32Ws {
+  int* ctr = nullptr;
   uint16_t* qhi = nullptr;
   uint16_t* qlo = nullptr;
   float* beta = nullptr;
@@ -2570,6 +2898,7 @@ size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8
     return p;
   };
   const size_t qbytes = (size_t)B * lq * kDim * sizeof(uint16_t);
+  if (op == CBV2_F32_SEARCH) w->ctr = (int*)take(kCtrBytes);
   w->qhi = (uint16_t*)take(qbytes);
   w->qlo = (uint16_t*)take(qbytes);
   w->beta = (float*)take((size_t)B * sizeof(float));
@@ -2698,6 +3027,8 @@ int cbv2_index_destroy(cbv2_index* index) {
     int prev = 0;
     if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(index->device) == hipSuccess) {
       if (index->task_ring != nullptr) (void)hipFree(index->task_ring);
+      for (hipEvent_t e : index->ring_ev)
+        if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : index->scan_ev) (void)hipEventDestroy(e);
       (void)hipSetDevice(prev);
     }
@@ -2708,6 +3039,7 @@ int cbv2_index_destroy(cbv2_index* index) {
 
 int cbv2_index_time_scans(cbv2_index* ix, int32_t enable) {
   CBV2_REQUIRE(ix != nullptr, "null index");
+  std::lock_guard<std::mutex> lk(ix->mu);
   if (enable) ix->scan_ev_used = 0;
   ix->time_scans = enable != 0;
   return CBV2_OK;
@@ -2716,6 +3048,7 @@ int cbv2_index_time_scans(cbv2_index* ix, int32_t enable) {
 int cbv2_index_scan_times(cbv2_index* ix, float* ms, int32_t max, int32_t* count) {
   CBV2_REQUIRE(ix != nullptr && count != nullptr, "null index or count");
   CBV2_REQUIRE(max >= 0 && (max == 0 || ms != nullptr), "bad output buffer");
+  std::lock_guard<std::mutex> lk(ix->mu);
   CBV2_REQUIRE(!ix->time_scans, "disable timing (cbv2_index_time_scans(ix, 0)) before reading the times");
   *count = (int32_t)ix->scan_ev_used;
   DeviceGuard dg(ix->device);
@@ -2758,9 +3091,16 @@ int cbv2_score(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, i
   return score_impl(ix, scorer, Q, B, lq, out, ld_out, (hipStream_t)stream);
 }
 
+size_t cbv2_search_workspace_size(const cbv2_index* ix, int32_t B, int32_t k, int32_t scorer) {
+  if (!ix || B < 1 || k < 1) return 0;
+  const int64_t slots = fused_slots(ix, scorer, B, k);
+  if (slots > 0) return kCtrBytes + (size_t)B * slots * k * sizeof(uint64_t);
+  return kCtrBytes + topk_ws_bytes(B, ix->n) + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
+}
+
 size_t cbv2_search_workspace_bytes(const cbv2_index* ix, int32_t B) {
-  if (!ix || B < 1) return 0;
-  return topk_ws_bytes(B, ix->n) + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
+  if (!ix || B < 1) return 0;   // enough for any k and scorer (the unfused layout is the larger)
+  return kCtrBytes + topk_ws_bytes(B, ix->n) + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
 }
 
 int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
@@ -2770,18 +3110,53 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   if (rc) return rc;
   CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
   CBV2_REQUIRE(out_scores && out_ids, "null outputs");
-  const size_t need = cbv2_search_workspace_bytes(ix, B);
-  CBV2_REQUIRE(workspace != nullptr && workspace_bytes >= need, "workspace too small (%zu < %zu)",
-               workspace_bytes, need);
+  const size_t need = cbv2_search_workspace_size(ix, B, k, scorer);
+  CBV2_REQUIRE(workspace != nullptr && workspace_bytes >= need && aligned16(workspace),
+               "workspace too small or misaligned (%zu < %zu)", workspace_bytes, need);
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
   hipStream_t st = (hipStream_t)stream;
   if (ix->n == 0) return topk_impl_empty(B, k, out_scores, out_ids, st);
+  int* ctr = (int*)workspace;
+  uint8_t* rest = (uint8_t*)workspace + kCtrBytes;
+  const int64_t slots = fused_slots(ix, scorer, B, k);
+  if (slots > 0) {  // fused scan + top-k: per-workgroup lists, then one select per query
+    FusedTopk ft{(uint64_t*)rest, k, slots, 0};
+    if ((rc = scan_maxsim_timed(ix, Q, B, lq, nullptr, 0, st, ctr, &ft))) return rc;
+    hipLaunchKernelGGL(select_keys_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, ft.part, ft.slots * k,
+                       slots * k, k, ix->id_base, out_scores, out_ids);
+    return launch_check("select_keys_kernel");
+  }
   const size_t tk = topk_ws_bytes(B, ix->n);
-  float* sc = (float*)((uint8_t*)workspace + tk);
-  rc = score_impl(ix, scorer, Q, B, lq, sc, ix->n, st);
+  float* sc = (float*)(rest + tk);
+  rc = score_impl(ix, scorer, Q, B, lq, sc, ix->n, st, ctr);
   if (rc) return rc;
-  return topk_impl(sc, B, ix->n, ix->n, k, ix->id_base, workspace, tk, out_scores, out_ids, st, ix->device);
+  return topk_impl(sc, B, ix->n, ix->n, k, ix->id_base, rest, tk, out_scores, out_ids, st, ix->device);
+}
+
+int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  switch (option) {
+    case CBV2_OPT_FUSED_TOPK:
+      ix->fused_topk = value != 0;
+      return CBV2_OK;
+    case CBV2_OPT_DYNAMIC_TAIL:
+      ix->dynamic_tail = value != 0;
+      return CBV2_OK;
+    default:
+      return fail(CBV2_EINVAL, "unknown option %d", option);
+  }
+}
+
+int64_t cbv2_search_fused_slots(const cbv2_index* ix, int32_t B, int32_t k, int32_t scorer) {
+  if (!ix || B < 1 || k < 1) return 0;
+  return fused_slots(ix, scorer, B, k);
+}
+
+int cbv2_index_last_scan_plan(const cbv2_index* ix, int64_t* out4) {
+  CBV2_REQUIRE(ix != nullptr && out4 != nullptr, "null index or output");
+  for (int i = 0; i < 4; ++i) out4[i] = ix->last_plan[i];
+  return CBV2_OK;
 }
 
 int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
@@ -2886,7 +3261,7 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   }
   if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
-  if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st))) return rc;
+  if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr))) return rc;
   if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
     return rc;
   // 2. band T >= T_k - 2 beta, 3. faithful rescoring, 4. exact top-k of the band

@@ -6,7 +6,10 @@
 // is restated over TERM IDS (tokenisation/stopwords stay in Python, bm25.py):
 //   idf(t)   = ln(1 + (N - df + 0.5) / (df + 0.5))
 //   w(t, d)  = idf * tf * (k1 + 1) / (tf + k1 * (1 - b + b * |d| / avgdl))
-//   score(q, d) = sum over the DISTINCT query terms, ascending term id, of w(t, d)
+//   score(q, d) = sum over the query's terms IN QUERY ORDER, repeats included,
+//                 of w(t, d)   (bm25s sums the postings of every query token id:
+//                 its get_scores_from_ids -> _compute_relevance_from_scores;
+//                 round 1 summed distinct terms, which differs on repeated words)
 // Weights are computed in double and stored as float; scores accumulate in
 // float in posting order, so oracle/oracle.py:bm25_topk reproduces every bit.
 // Ranking: score descending, then doc id ascending; rows are padded with the
@@ -131,8 +134,6 @@ static void search_range(const cbv2_bm25* ix, const int32_t* q_terms, const int6
   std::vector<int32_t> touched, terms, order;
   for (int32_t b = b0; b < b1; ++b) {
     terms.assign(q_terms + q_offsets[b], q_terms + q_offsets[b + 1]);
-    std::sort(terms.begin(), terms.end());
-    terms.erase(std::unique(terms.begin(), terms.end()), terms.end());
     touched.clear();
     for (int32_t t : terms) {
       if (t < 0 || t >= ix->vocab) continue;

@@ -123,7 +123,9 @@ size_t cbv2_sharded_workspace_bytes(const cbv2_index* ix, const cbv2_comm* c, in
   const size_t gather = align256(blk * 4) + align256(blk * 4 * c->nranks);
   const size_t lex_out = align256((size_t)B * (kb > 0 ? kb : 1) * 4);
   const size_t raw = align256((size_t)B * (C > 0 ? C : 1) * 4);
-  return cbv2_search_workspace_bytes(ix, B) + gather + lex_out + raw;
+  // the local search's part is sized for MaxSim (the sharded exchange's scorer;
+  // cbv2_search rejects another scorer's larger need with CBV2_EINVAL)
+  return align256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM)) + gather + lex_out + raw;
 }
 
 namespace {
@@ -134,7 +136,7 @@ struct Layout {
 };
 Layout layout(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, int32_t kb, void* ws) {
   Layout L;
-  L.search_ws = cbv2_search_workspace_bytes(ix, B);
+  L.search_ws = align256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM));
   L.blk = (size_t)2 * B * (k + kb);
   uint8_t* p = (uint8_t*)ws + L.search_ws;
   L.send = (int32_t*)p;

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .bm25 import HostBM25
+from .bm25 import HostBM25, Stemmer, tokenize
 from .config import RAGConfig
 from .retriever import JinaColBERTRetriever
 
@@ -95,10 +95,12 @@ class DualIndexer:
         self.colbert_retriever = JinaColBERTRetriever(config, encoder=encoder)
 
     def build_bm25_index(self, corpus: List[str]) -> None:
+        """LRC:846-864: bm25s.tokenize(corpus, stopwords="en", stemmer=Stemmer("english")) -> index -> save."""
         print("\n[BM25s] Building lexical search index...", end=" ")
         start = time.time()
+        corpus_tokens = tokenize(corpus, stopwords="en", stemmer=Stemmer("english"))
         self.bm25_retriever = HostBM25()
-        self.bm25_retriever.index(self.bm25_retriever.tokenize(corpus))
+        self.bm25_retriever.index(corpus_tokens)
         self.bm25_retriever.save(self.config.bm25_index_path)
         print(f"✓ {time.time() - start:.2f}s")
 
@@ -169,7 +171,12 @@ class HybridRetriever:
         bm = self.indexer.bm25_retriever
         if bm is None:
             return []
-        results, scores = bm.retrieve(bm.tokenize(query), k=k)
+        # the reference's bm25s.tokenize(query, stopwords="en", stemmer=english) (LRC:939-943):
+        # one Tokenized row per query, even when every word is a stopword; a
+        # retriever with its own tokenize() (HostBM25, test stand-ins) supplies it
+        tok = getattr(bm, "tokenize", None)
+        query_tokens = tok(query) if callable(tok) else tokenize(query, stopwords="en", stemmer=Stemmer("english"))
+        results, scores = bm.retrieve(query_tokens, k=k)
         return [{"chunk_id": int(results[0][i]), "score": float(scores[0][i]), "source": "bm25"}
                 for i in range(len(results[0])) if results[0][i] >= 0]
 

@@ -246,7 +246,23 @@ class ColbertIndex:
             _lib.lib().cbv2_index_destroy(self._h)
             self._h = ctypes.c_void_p()
 
-    # ------------------------------------------------------------ measurement
+    # ------------------------------------------------------------ options / measurement
+    def set_option(self, option: int, value: int) -> None:
+        """cbv2_index_set_option: _lib.OPT_FUSED_TOPK / OPT_DYNAMIC_TAIL (A/B and tests)."""
+        _lib.check(_lib.lib().cbv2_index_set_option(self._h, int(option), int(value)))
+
+    def fused_topk_slots(self, B: int, k: int, scorer: str = "maxsim") -> int:
+        """Per-query workgroup lists a search of (B, k) keeps when the top-k is fused
+        into the scan (0: the unfused path; cbv2_search_fused_slots)."""
+        return int(_lib.lib().cbv2_search_fused_slots(self._h, int(B), int(k), self._scorer(scorer)))
+
+    def last_scan_plan(self) -> dict:
+        """Work split of this handle's latest scan launch (cbv2_index_last_scan_plan)."""
+        buf = (ctypes.c_int64 * 4)()
+        _lib.check(_lib.lib().cbv2_index_last_scan_plan(self._h, buf))
+        return {"workgroups": int(buf[0]), "chunk_docs": int(buf[1]), "static_docs": int(buf[2]),
+                "dynamic_tail": bool(buf[3])}
+
     def time_scans(self, enable: bool) -> None:
         """Bracket every following MaxSim scan launch of this index with HIP
         events on its own stream (cbv2_index_time_scans); enable clears the
@@ -341,7 +357,7 @@ class ColbertIndex:
         if self.faithful and scorer == "maxsim":
             return self._search_f32(_keep, B, lq, k)
         L = _lib.lib()
-        need = int(L.cbv2_search_workspace_bytes(self._h, B))
+        need = int(L.cbv2_search_workspace_size(self._h, B, int(k), sid))
         if self._ws is None or self._ws.numel() * 4 < need:
             self._ws = torch.empty(((need + 3) // 4,), dtype=torch.float32, device=self.device)
         out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)

@@ -50,6 +50,32 @@ def bm25_lists(B: int, n_total: int, planted: np.ndarray, k: int = 100, hits: in
     return out
 
 
+def iter_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, device, seed: int = 0,
+               sigma: float = 0.1, dtype: torch.dtype = torch.bfloat16):
+    """Docs [begin, end) of the synthetic corpus, one generator chunk at a time:
+    yields (lo, hi, tokens ``dtype`` [hi - lo, 128, 128] on ``device``) with the
+    planted positives already in place, so a corpus larger than HBM in fp32 /
+    bf16 (10M docs = 328 GB of bf16) can be quantised or indexed chunk by chunk
+    with bounded memory.  Concatenating the chunks gives ``make_shard``'s tokens."""
+    lq = Q.shape[1]
+    flat = planted.reshape(-1)
+    owner = np.repeat(np.arange(planted.shape[0]), planted.shape[1])
+    gen = torch.Generator().manual_seed(seed + 17)
+    noise_all = torch.randn(len(flat), lq, DIM, generator=gen)          # same draws whatever the shard
+    c0, c1 = begin // CHUNK, (end + CHUNK - 1) // CHUNK
+    for c in range(c0, c1):
+        g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + c)
+        x = _unit(torch.randn((CHUNK, LD, DIM), generator=g, device=device, dtype=torch.float32))
+        lo, hi = max(begin, c * CHUNK), min(end, (c + 1) * CHUNK)
+        t = x[lo - c * CHUNK: hi - c * CHUNK].to(dtype)
+        del x
+        mine = (flat >= lo) & (flat < hi)
+        if mine.any():
+            docs = _unit(Q[torch.from_numpy(owner[mine])] + sigma * _unit(noise_all[torch.from_numpy(mine)]))
+            t[torch.from_numpy(flat[mine] - lo).to(device), :lq] = docs.to(device=device, dtype=dtype)
+        yield lo, hi, t
+
+
 def make_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, device, seed: int = 0,
                sigma: float = 0.1, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
     """Docs [begin, end) of the synthetic corpus: (``dtype`` [n, 128, 128], int32 doclens [n]) on ``device``
@@ -57,25 +83,28 @@ def make_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, devic
     n = end - begin
     tokens = torch.empty((n, LD, DIM), dtype=dtype, device=device)
     doclens = torch.full((n,), LD, dtype=torch.int32, device=device)
-    c0, c1 = begin // CHUNK, (end + CHUNK - 1) // CHUNK
-    for c in range(c0, c1):
-        g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + c)
-        x = _unit(torch.randn((CHUNK, LD, DIM), generator=g, device=device, dtype=torch.float32))
-        lo, hi = max(begin, c * CHUNK), min(end, (c + 1) * CHUNK)
-        tokens[lo - begin: hi - begin] = x[lo - c * CHUNK: hi - c * CHUNK].to(dtype)
-        del x
-    lq = Q.shape[1]
-    flat = planted.reshape(-1)
-    owner = np.repeat(np.arange(planted.shape[0]), planted.shape[1])
-    mine = (flat >= begin) & (flat < end)
-    if mine.any():
-        ids = flat[mine]
-        qb = owner[mine]
-        gen = torch.Generator().manual_seed(seed + 17)
-        noise = torch.randn(len(flat), lq, DIM, generator=gen)[torch.from_numpy(mine)]
-        docs = _unit(Q[torch.from_numpy(qb)] + sigma * _unit(noise))
-        tokens[torch.from_numpy(ids - begin).to(device), :lq] = docs.to(device=device, dtype=dtype)
+    for lo, hi, t in iter_shard(begin, end, Q, planted, device, seed, sigma, dtype):
+        tokens[lo - begin: hi - begin] = t
     return tokens, doclens
+
+
+def make_shard_mxfp8(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, device, seed: int = 0,
+                     sigma: float = 0.1):
+    """Docs [begin, end) quantised to MXFP8 chunk by chunk (HIP quantizer on the
+    bf16 tokens, exactly as ``ColbertIndex.mxfp8(make_shard(...))`` would):
+    (e4m3 uint8 [n, 128, 128], E8M0 uint8 [n, 128, 2], int32 doclens [n]).
+    Peak extra memory is one generator chunk, so 10M docs (167 GB) fit one HBM."""
+    from .index import quantize_mxfp8
+    n = end - begin
+    q = torch.empty((n, LD, DIM), dtype=torch.uint8, device=device)
+    sc = torch.empty((n, LD, 2), dtype=torch.uint8, device=device)
+    doclens = torch.full((n,), LD, dtype=torch.int32, device=device)
+    for lo, hi, t in iter_shard(begin, end, Q, planted, device, seed, sigma, torch.bfloat16):
+        qq, ss = quantize_mxfp8(t)
+        q[lo - begin: hi - begin] = qq
+        sc[lo - begin: hi - begin] = ss
+        del t, qq, ss
+    return q, sc, doclens
 
 
 BM25_VOCAB = 30000

@@ -85,6 +85,23 @@ int cbv2_index_destroy(cbv2_index* index);
 int cbv2_index_time_scans(cbv2_index* index, int32_t enable);
 int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
 
+/* Handle options (A/B and tests; defaults = production):
+ *  CBV2_OPT_FUSED_TOPK   1: cbv2_search fuses the top-k into eligible scans.
+ *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
+ *                        as dynamic tasks (0: static chunks only).
+ * cbv2_index_last_scan_plan: the work split of this handle's latest scan
+ * launch: {workgroups, static chunk docs, static docs, dynamic tail 0/1}.
+ * Thread safety: one handle may be used from several host threads and
+ * streams; the options and the last plan are plain fields (set options
+ * before sharing the handle).                                               */
+#define CBV2_OPT_FUSED_TOPK 1
+#define CBV2_OPT_DYNAMIC_TAIL 2
+int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
+int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
+/* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the
+ * top-k fused into the scan; 0 = that search runs unfused.                  */
+int64_t cbv2_search_fused_slots(const cbv2_index* index, int32_t B, int32_t k, int32_t scorer);
+
 /* MXFP8 index (config 5: half the HBM bytes of bf16, scored on the
  * block-scaled fp8 MFMA): tokens e4m3 [n][128][128] (16-B aligned), scales
  * E8M0 [n][128][2] (byte h scales dims 64h .. 64h+63 by 2^(byte-127)).
@@ -120,7 +137,16 @@ int cbv2_score(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype
  * score every doc, then top-k (torch.topk at :767) with the deterministic tie
  * rule.  Writes out_scores f32 [B][k] and out_ids int32 [B][k] (GLOBAL ids =
  * id_base + local index), best first; slots past min(k, n) hold -inf / -1.
- * `workspace` must hold cbv2_search_workspace_bytes(index, B) bytes.        */
+ * `workspace` (16-B aligned, caller-owned, also holds the scan's work-split
+ * counters, so concurrent calls on distinct streams need distinct workspaces)
+ * must hold cbv2_search_workspace_size(index, B, k, scorer) bytes;
+ * cbv2_search_workspace_bytes(index, B) is enough for any k and scorer.
+ * MaxSim with k <= 104 on the doc-interleaved scans (bf16 B > 16, MXFP8 B > 8)
+ * fuses the top-k into the scan (no [B][n] score matrix: each workgroup keeps
+ * its best k per query in LDS, then one selection per query); results are
+ * those of the unfused path bit for bit (CBV2_OPT_FUSED_TOPK turns it off).
+ * Extends §8(b)'s prototype with scorer / q_dtype / workspace.  */
+size_t cbv2_search_workspace_size(const cbv2_index* index, int32_t B, int32_t k, int32_t scorer);
 size_t cbv2_search_workspace_bytes(const cbv2_index* index, int32_t B);
 int cbv2_search(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B,
                 int32_t lq, int32_t k, void* workspace, size_t workspace_bytes,
@@ -225,7 +251,8 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
  * and stopwords stay in the caller).  Lucene BM25:
  *   idf = ln(1 + (N - df + 0.5) / (df + 0.5)),
  *   w   = idf * tf * (k1 + 1) / (tf + k1 * (1 - b + b * |d| / avgdl)),
- * summed over the distinct query terms.  Corpus as CSR: doc i's term ids are
+ * summed over the query's term ids in query order, repeats included (bm25s
+ * sums the postings of every query token).  Corpus as CSR: doc i's term ids are
  * doc_terms[doc_offsets[i] .. doc_offsets[i+1]).  Search: queries as CSR,
  * out_ids [B][k] (score desc, then doc id asc; padded with the lowest-id
  * zero-score docs, then -1), out_scores [B][k] (nullable).  n_threads <= 0:
@@ -248,6 +275,15 @@ int cbv2_bm25_build_shard(const int32_t* doc_terms, const int64_t* doc_offsets, 
                           const int64_t* df_global, cbv2_bm25** out);
 int64_t cbv2_bm25_num_docs(const cbv2_bm25* index);
 int cbv2_bm25_destroy(cbv2_bm25* index);
+
+/* English stemmer (HOST pointers, no GPU): the Snowball English ("Porter2")
+ * algorithm PyStemmer's Stemmer("english") implements, which the reference
+ * passes to bm25s.tokenize (local_rag_complete.py:851-855, 939-943).  Words
+ * are UTF-8, lower-cased by the caller; word i = words[offsets[i] ..
+ * offsets[i+1]).  Stems go to out (out_cap >= offsets[n] - offsets[0]
+ * suffices: no stem is longer than its word), out_offsets [n + 1].        */
+int cbv2_stem_en(const char* words, const int64_t* offsets, int64_t n, char* out, int64_t out_cap,
+                 int64_t* out_offsets);
 
 /* Native index file (replaces the torch.save/torch.load of
  * indexes/colbert/index.pt at local_rag_complete.py:743-746, 751 for large

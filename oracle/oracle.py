@@ -248,8 +248,9 @@ def merge_topk(scores: np.ndarray, ids: np.ndarray, k: int):
 def bm25_topk(doc_terms, doc_offsets, q_terms, q_offsets, vocab: int, k: int, k1: float = 1.5, b: float = 0.75):
     """Lucene BM25 as bm25s scores it (LRC:851-858, 939-945; bm25s absent here, so
     its published formula), restated with the C++ index's exact operation order
-    so every float matches: weights in float64 -> float32, query terms distinct and
-    ascending, float32 accumulation in doc order, ties -> lower doc id, all docs ranked."""
+    so every float matches: weights in float64 -> float32, the query's term ids in
+    query order with repeats (bm25s sums the postings of every query token),
+    float32 accumulation in doc order, ties -> lower doc id, all docs ranked."""
     import math
     k1, b = float(np.float32(k1)), float(np.float32(b))      # the C ABI takes them as float
     doc_terms = np.asarray(doc_terms, np.int64)
@@ -273,7 +274,7 @@ def bm25_topk(doc_terms, doc_offsets, q_terms, q_offsets, vocab: int, k: int, k1
     out_s = np.zeros((B, k), np.float32)
     for qb in range(B):
         acc = np.zeros(N, np.float32)
-        for t in sorted(set(int(x) for x in q_terms[q_offsets[qb]:q_offsets[qb + 1]])):
+        for t in (int(x) for x in q_terms[q_offsets[qb]:q_offsets[qb + 1]]):
             if 0 <= t < vocab:
                 for d, w in post[t]:
                     acc[d] = np.float32(acc[d] + w)

@@ -115,16 +115,41 @@ def test_synth_bm25_shards_compose_and_plant():
 
 
 def test_hostbm25_text_roundtrip(tmp_path):
-    from hybrid_rag_colbertv2_amd.bm25 import HostBM25
+    from hybrid_rag_colbertv2_amd.bm25 import HostBM25, to_csr
     corpus = ["The quick brown fox", "jumps over the lazy dog", "quick quick dog", "", "fox and dog"]
     bm = HostBM25()
     bm.index(bm.tokenize(corpus))
     ids, sc = bm.retrieve(bm.tokenize("quick dog"), k=5)
     # oracle over the same term ids
-    rows = [bm._ids(t, grow=False) for t in bm.tokenize(corpus)]
-    from hybrid_rag_colbertv2_amd.bm25 import to_csr
+    rows = [bm._ids(t, grow=False) for t in bm._rows(bm.tokenize(corpus))]
     terms, off = to_csr(rows)
-    q, qo = to_csr([bm._ids(bm.tokenize("quick dog"), grow=False)])
+    q, qo = to_csr([bm._ids(t, grow=False) for t in bm._rows(bm.tokenize("quick dog"))])
     oi, os_ = orc.bm25_topk(terms, off, q, qo, len(bm.vocab), 5)
     _same(ids, sc, oi, os_)
     assert ids[0][0] == 2
+    bm.save(str(tmp_path))
+    bm2 = HostBM25.load(str(tmp_path))
+    ids2, sc2 = bm2.retrieve(bm2.tokenize("quick dog"), k=5)
+    assert np.array_equal(ids, ids2) and np.array_equal(sc, sc2)
+
+
+def test_native_bm25_repeated_query_terms():
+    """A repeated query term counts once per occurrence (bm25s sums the
+    postings of every query token), in query order."""
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    rng = np.random.default_rng(7)
+    terms, off = _corpus(rng, 300, 40)
+    ix = NativeBM25(terms, off, 40)
+    rep = np.array([3, 5, 3, 3, 9], np.int32)
+    ids, sc = ix.search(rep, np.array([0, 5], np.int64), 20)
+    oi, os_ = orc.bm25_topk(terms, off, rep, np.array([0, 5], np.int64), 40, 20)
+    _same(ids, sc, oi, os_)
+    # a doc holding term 3 but not 5 or 9 scores exactly 3 x its term-3 weight
+    holds3 = [d for d in range(300) if set(terms[off[d]:off[d + 1]].tolist()) & {3, 5, 9} == {3}]
+    assert holds3
+    i3, s3 = ix.search(np.array([3], np.int32), np.array([0, 1], np.int64), 300)
+    ir, sr = ix.search(rep, np.array([0, 5], np.int64), 300)
+    w3 = dict(zip(i3[0].tolist(), s3[0].tolist()))
+    wr = dict(zip(ir[0].tolist(), sr[0].tolist()))
+    for d in holds3:
+        assert wr[d] == np.float32(np.float32(w3[d] + w3[d]) + w3[d])

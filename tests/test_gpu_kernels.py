@@ -4,12 +4,17 @@ Tolerances: MaxSim scores within 1e-3 absolute (fp32 accumulation of exact
 bf16 products vs the oracle's float64); ids/ranks bit-exact.  On random data
 the top-k ids are compared only where the oracle's neighbouring scores are
 separated by more than 1e-3 (a gap the fp32 reordering cannot cross); the k/16
-exact-grid fixtures are compared bit-exactly, ties included.
+exact-grid fixtures are compared bit-exactly, ties included.  Searches are
+also checked with tests/_parity.py: the returned top-k must be exactly the
+oracle's selection of the GPU's own score matrix (bit for bit, ties included),
+and the ranking must agree with the oracle's float64 scores within 1e-3.
 """
 import numpy as np
 import pytest
 import torch
 
+from _parity import assert_ids_match_separated, assert_ranking_consistent, assert_selection_exact
+from hybrid_rag_colbertv2_amd import _lib
 from hybrid_rag_colbertv2_amd.index import ColbertIndex, merge_topk, select_topk, topk_rows
 from oracle import oracle as orc
 
@@ -31,18 +36,6 @@ def make_case(seed, N, B, lq, ragged=True, min_len=1):
         doclens = torch.full((N,), 128, dtype=torch.int32)
     Q = rand_unit(g, B, lq, 128).bfloat16()
     return docs, doclens, Q
-
-
-def assert_ids_match_separated(ids, ref_ids, ref_scores, gap=ATOL):
-    """ids equal wherever the oracle ranking is unambiguous at fp32 precision."""
-    ids = np.asarray(ids)
-    for b in range(ids.shape[0]):
-        s = ref_scores[b]
-        for j in range(ids.shape[1]):
-            lo = s[j - 1] - s[j] if j > 0 else np.inf
-            hi = s[j] - s[j + 1] if j + 1 < len(s) else np.inf
-            if min(lo, hi) > gap:
-                assert ids[b, j] == ref_ids[b, j], (b, j, ids[b, j], ref_ids[b, j])
 
 
 @pytest.mark.parametrize("N,B,lq,ragged", [
@@ -108,7 +101,9 @@ def test_search_matches_oracle(dev, N, B, k):
     rs, ri = orc.topk(ref, k)
     s, i = s.cpu().numpy(), i.cpu().numpy()
     np.testing.assert_allclose(s, rs, atol=ATOL, rtol=0)
-    assert_ids_match_separated(i, ri, rs)
+    assert_selection_exact(i, s, ix.score(Q.to(dev)).cpu().numpy(), k)
+    assert_ranking_consistent(i, ref, ATOL)
+    assert_ids_match_separated(i, ri, rs, ATOL)
     kk = min(k, N)
     assert (i[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
     assert (np.diff(s[:, :kk], axis=1) <= 0).all()
@@ -157,10 +152,14 @@ def test_rerank_matches_oracle(dev, C, k, B):
     s, i, p = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), k=k)
     es, ei, ep = orc.rerank(Q.float().numpy(), docs.float().numpy(), doclens.numpy(), cand, k)
     np.testing.assert_allclose(s.cpu().numpy(), es, atol=ATOL, rtol=0)
-    assert_ids_match_separated(p.cpu().numpy(), ep, es)
-    assert_ids_match_separated(i.cpu().numpy(), ei, es)
+    assert_ids_match_separated(p.cpu().numpy(), ep, es, ATOL)
+    assert_ids_match_separated(i.cpu().numpy(), ei, es, ATOL)
     raw = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), k=0).cpu().numpy()
     assert raw.shape == (B, C)
+    # the selection of the GPU's own raw candidate scores, exactly (position tie rule)
+    for b in range(B):
+        exp = orc.rerank_select(raw[b], k)
+        assert [int(x) for x in p[b].cpu()[:len(exp)]] == [e[0] for e in exp], b
     if C > 3:
         assert np.isneginf(raw[:, 1]).all() and np.isneginf(raw[:, 2]).all()
         assert np.array_equal(raw[:, 3], raw[:, 0])
@@ -376,6 +375,12 @@ def test_dynamic_tail_b16_bit_identical(dev):
     Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16()
     ix = ColbertIndex(docs, doclens)
     full = ix.score(Q)
+    plan = ix.last_scan_plan()
+    assert plan["dynamic_tail"] and 0 < plan["static_docs"] < N, plan   # the counter path ran
+    ix.set_option(_lib.OPT_DYNAMIC_TAIL, 0)
+    assert torch.equal(ix.score(Q), full)                       # static split only: same bits
+    assert not ix.last_scan_plan()["dynamic_tail"]
+    ix.set_option(_lib.OPT_DYNAMIC_TAIL, 1)
     assert torch.equal(ix.score(Q), full)                       # counters reset per launch
     for b in (0, 7, 15):
         assert torch.equal(ix.score(Q[b:b + 1]), full[b:b + 1]), b
