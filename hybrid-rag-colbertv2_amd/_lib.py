@@ -63,6 +63,10 @@ _SIGS = {
     "cbv2_index_file_read": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _p, _p, _p, _p]),
     "cbv2_index_file_write_host": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _p, _p, _p, _i64]),
     "cbv2_index_file_read_host": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _p, _p, _p]),
+    "cbv2_index_writer_open": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_index_writer_append": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i32, _p]),
+    "cbv2_index_writer_count": (_i64, [_p]),
+    "cbv2_index_writer_close": (ctypes.c_int, [_p]),
     "cbv2_comm_init": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_comm_size": (ctypes.c_int, [_p]),
     "cbv2_comm_rank": (ctypes.c_int, [_p]),

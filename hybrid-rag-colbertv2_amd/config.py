@@ -17,6 +17,8 @@ Added fields (no reference counterpart):
   * ``index_dtype``    — "bf16" (default), "fp8" (MXFP8, config 5) or "fp32"
                           (fp32-faithful: the reference's fp32 scores within
                           ~1e-5 and their exact top-k).
+  * ``ingest_batch`` / ``index_pt_max_docs`` — batched, bounded-memory
+                          indexing (JinaColBERTRetriever.index).
 """
 from dataclasses import dataclass
 
@@ -60,3 +62,5 @@ class RAGConfig:
     query_maxlen: int = 32
     dim: int = 128
     index_dtype: str = "bf16"
+    ingest_batch: int = 256            # docs encoded and indexed per batch (bounded host memory)
+    index_pt_max_docs: int = 50_000    # larger corpora persist as index.cbv2, not the fp32 index.pt

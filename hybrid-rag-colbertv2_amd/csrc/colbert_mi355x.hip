@@ -677,8 +677,12 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
 // path at the same moment (lab phase stamps: ~1.2k issue cycles/iteration).
 // FK > 0: fused top-k (see topk_offer): no score matrix; each workgroup writes
 // its best topk_k keys per query to part[qi][slot][topk_k] (slot = its chunk).
+// SPLITLOAD: only waves 0 .. WAVES/2-1 (one per SIMD) issue the ring's LDS-DMA
+// pieces (twice as many each), so after each barrier the partner wave on the
+// SIMD (waves WAVES/2 ..) starts its MFMAs at once instead of both waves
+// spending the issue phase with the MFMA pipe idle.
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
-          bool SPREAD = false, int FK = 0>
+          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -689,10 +693,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   constexpr int kIterBytes = 4 * TPI * kRowBytes;
   constexpr int IPG = kLd / TPI, NT = TPI / 4;
   constexpr int kPieces = kIterBytes / 1024;
-  constexpr int kPiecesPerWave = kPieces / WAVES;
+  constexpr int kLoadWaves = SPLITLOAD ? WAVES / 2 : WAVES;
+  constexpr int kPiecesPerWave = kPieces / kLoadWaves;   // per loading wave
   static_assert(TPI == 32 || TPI == 64, "32 or 64 tokens per iteration");
-  static_assert(kPieces % WAVES == 0, "pieces must split evenly over waves");
+  static_assert(kPieces % kLoadWaves == 0, "pieces must split evenly over the loading waves");
   static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
+  static_assert(!(SPREAD && SPLITLOAD), "SPREAD spreads every wave's pieces; SPLITLOAD moves them");
   // one LDS object only: with a second __shared__ array hipcc starts putting
   // vmcnt(0) before the ring's ds_reads (LDS-DMA alias tracking)
   // fused top-k: one key buffer + state per (wave, query), after the task slots
@@ -724,15 +730,32 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
 
   // LDS-DMA piece p = rows 4p..4p+3 of the image [4 docs][TPI tokens] = doc
   // 4p / TPI, tokens TPI*j + 4p % TPI + 0..3; slot XOR (doc << 2 | R & 3)
-  uint32_t src_off[kPiecesPerWave];
-  int src_doc[kPiecesPerWave];
+  const bool loader = !SPLITLOAD || wave < kLoadWaves;   // wave-uniform
+  const int lwave = loader ? wave : 0;
+  // SPLITLOAD (16 pieces per loading wave): offsets on the fly instead of held
+  // in VGPRs.  With R0 = 4 * piece (uniform) and L = lane >> 4: doc = R0 / TPI,
+  // offset = (R0 % TPI + L) * 256 + 16 * (((lane & 15) ^ L) ^ (doc << 2)).
+  constexpr int kHeld = SPLITLOAD ? 1 : kPiecesPerWave;
+  uint32_t src_off[kHeld];
+  int src_doc[kHeld];
+  const uint32_t lb1 = (uint32_t)(lane >> 4) * kRowBytes, lb2 = 16u * (uint32_t)((lane & 15) ^ (lane >> 4));
 #pragma unroll
-  for (int jj = 0; jj < kPiecesPerWave; ++jj) {
-    const int R = 4 * (wave * kPiecesPerWave + jj) + (lane >> 4);
+  for (int jj = 0; jj < kHeld; ++jj) {
+    const int R = 4 * (lwave * kPiecesPerWave + jj) + (lane >> 4);
     const int doc = R / TPI;
     src_off[jj] = (R % TPI) * kRowBytes + 16 * ((lane & 15) ^ ((doc << 2) | (R & 3)));
     src_doc[jj] = doc;
   }
+  auto piece_src = [&](int jj, int& doc) -> uint32_t {
+    if constexpr (SPLITLOAD) {
+      const int R0 = 4 * (lwave * kPiecesPerWave + jj);
+      doc = R0 / TPI;
+      return (uint32_t)(R0 % TPI) * kRowBytes + lb1 + (lb2 ^ (uint32_t)(doc << 6));
+    } else {
+      doc = src_doc[jj];
+      return src_off[jj];
+    }
+  };
 
   // STAMPS (lab only): per-wave s_memtime cycles in three phases of the ring
   // loop -- wait (vmcnt + barrier), issue (next DMA + doc lengths), compute
@@ -748,14 +771,17 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       const int ngr = (nd + 3) >> 2;
       auto issue_piece = [&](int it, int buf, int jj) {
         const int G = it / IPG, j = it % IPG;
-        const int piece = wave * kPiecesPerWave + jj;
-        int d = 4 * G + src_doc[jj];
+        const int piece = lwave * kPiecesPerWave + jj;
+        int pdoc;
+        const uint32_t poff = piece_src(jj, pdoc);
+        int d = 4 * G + pdoc;
         d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * TPI * kRowBytes + src_off[jj];
+        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * TPI * kRowBytes + poff;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
                                          0, 0);
       };
       auto issue = [&](int it, int buf) {
+        if (!loader) return;
 #pragma unroll
         for (int jj = 0; jj < kPiecesPerWave; ++jj) issue_piece(it, buf, jj);
       };
@@ -2366,7 +2392,8 @@ struct cbv2_index {
   bool ring_ev_used[128] = {};
   // Work split of the most recent scan launch (cbv2_index_last_scan_plan).
   int64_t last_plan[4] = {0, 0, 0, 0};
-  bool fused_topk = true;    // CBV2_OPT_FUSED_TOPK
+  bool fused_topk = true;    // CBV2_OPT_FUSED_TOPK != 0
+  int fused_topk_mode = 1;   // its value (2: also the MXFP8 scan, A/B only)
   bool dynamic_tail = true;  // CBV2_OPT_DYNAMIC_TAIL
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
@@ -2595,7 +2622,7 @@ int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
 }
 
 template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
-          int FK = 0>
+          int FK = 0, bool SPLITLOAD = false>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
                     int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
@@ -2609,7 +2636,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK>),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
                      ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0);
@@ -2638,8 +2665,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
                 int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   if (ix->n == 0) return CBV2_OK;
   if (ft != nullptr)   // fused top-k: the B > 16 doc-interleaved scan only (fused_eligible)
-    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap>(ix, Q, B, lq, nullptr, 0, st, kScanDynFrac,
-                                                                         kScanTaskDocs, nullptr, ctr_ws, ft);
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, true>(ix, Q, B, lq, nullptr, 0, st,
+                                                                               kScanDynFrac, kScanTaskDocs, nullptr,
+                                                                               ctr_ws, ft);
   if (variant == kScanAuto)
     variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2)
                                : (B <= kSmallLdsMaxB ? kScan16x4W4 : kScan16x4W8);
@@ -2666,9 +2694,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan<8, 3, 1>(maxsim_scan16_kernel<8, 3>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
     case kScan16W4Q2:
       return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
-    case kScan16x4W8:
-      return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs,
-                                                        nullptr, ctr_ws);
+    case kScan16x4W8:   // SPLITLOAD: lab, same box, 1M / 125k / B=64: 145.25 -> 144.10, 18.14 -> 17.97, 37.98 -> 37.53 ms
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac,
+                                                                          kScanTaskDocs, nullptr, ctr_ws);
     case kScan16x4W4:
       return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
                                                    nullptr, ctr_ws);
@@ -2755,8 +2783,11 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
 // cost more than the matrix.
 int64_t fused_slots(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) {
   if (!ix->fused_topk || scorer != CBV2_SCORER_MAXSIM || ix->n == 0 || k > kFusedMaxK) return 0;
+  // MXFP8: the fused build of the f8 scan spills (its query fragments fill the
+  // VGPR file): 78.1 vs 74.1 ms at 1M, B=256 (profiles/r02b_fused_ab.jsonl),
+  // so MXFP8 searches stay unfused; CBV2_OPT_FUSED_TOPK = 2 forces it (A/B).
   if (ix->dtype == CBV2_DTYPE_MXFP8) {
-    if (B <= kF8DirectMaxB) return 0;
+    if (B <= kF8DirectMaxB || ix->fused_topk_mode < 2) return 0;
     return scan_chunks(ix, (B + kF8Waves * kF8QW - 1) / (kF8Waves * kF8QW), cu_count(ix->device));
   }
   if (B <= kSmallLdsMaxB) return 0;
@@ -3139,6 +3170,7 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
   switch (option) {
     case CBV2_OPT_FUSED_TOPK:
       ix->fused_topk = value != 0;
+      ix->fused_topk_mode = (int)value;
       return CBV2_OK;
     case CBV2_OPT_DYNAMIC_TAIL:
       ix->dynamic_tail = value != 0;

@@ -342,4 +342,98 @@ int cbv2_index_file_read(const char* path, int64_t begin, int64_t end, void* tok
   return CBV2_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Streaming writer (bounded-memory ingest): the header is written last, by
+// close(), once every doc of the declared count has been appended, so a file
+// whose ingest stopped early never reads as valid.
+// ---------------------------------------------------------------------------
+struct cbv2_index_writer {
+  cbv2_file_header h;
+  int fd = -1;
+  int64_t written = 0;
+  Pinned pin;
+  bool pinned = false;
+  char path[1024];
+};
+
+int cbv2_index_writer_open(const char* path, int32_t dtype, int64_t n, int64_t id_base, cbv2_index_writer** out) {
+  if (!out) return err(CBV2_EINVAL, "null output handle pointer");
+  *out = nullptr;
+  if (!path || strlen(path) >= 1024) return err(CBV2_EINVAL, "bad path");
+  auto* w = new cbv2_index_writer;
+  if (int rc = layout(dtype, n, id_base, w->h)) {
+    delete w;
+    return rc;
+  }
+  snprintf(w->path, sizeof(w->path), "%s", path);
+  w->fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (w->fd < 0) {
+    const int e = errno;
+    delete w;
+    return err(CBV2_EINVAL, "%s: cannot create (%s)", path, strerror(e));
+  }
+  cbv2_file_header blank;
+  memset(&blank, 0, sizeof(blank));  // not a valid header until close()
+  if (pwrite_full(w->fd, &blank, sizeof(blank), 0) || ftruncate(w->fd, (off_t)w->h.file_bytes) != 0) {
+    close(w->fd);
+    delete w;
+    return err(CBV2_EINVAL, "%s: cannot size the file", path);
+  }
+  *out = w;
+  return CBV2_OK;
+}
+
+int cbv2_index_writer_append(cbv2_index_writer* w, int64_t count, const void* tokens, const void* scales,
+                             const int32_t* doclens, int32_t on_device, void* stream) {
+  if (!w || w->fd < 0) return err(CBV2_EINVAL, "null or closed writer");
+  if (count < 0 || w->written + count > w->h.n)
+    return err(CBV2_EINVAL, "append of %lld docs past the declared %lld (written %lld)", (long long)count,
+               (long long)w->h.n, (long long)w->written);
+  if (count == 0) return CBV2_OK;
+  const bool fp8 = w->h.scales_off != 0;
+  if (!tokens || !doclens || (fp8 && !scales)) return err(CBV2_EINVAL, "null pointer");
+  const size_t per = 128 * 128 * tok_bytes(w->h.dtype);
+  const uint64_t d0 = (uint64_t)w->written;
+  if (on_device) {
+    if (!w->pinned) {
+      if (int rc = w->pin.alloc()) return rc;
+      w->pinned = true;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = range_from_device(w->path, w->fd, w->h.doclens_off + 4 * d0, 4ull * count, (const uint8_t*)doclens,
+                                   w->pin.p, st))
+      return rc;
+    if (int rc = range_from_device(w->path, w->fd, w->h.tokens_off + per * d0, per * count, (const uint8_t*)tokens,
+                                   w->pin.p, st))
+      return rc;
+    if (fp8)
+      if (int rc = range_from_device(w->path, w->fd, w->h.scales_off + 256 * d0, 256ull * count,
+                                     (const uint8_t*)scales, w->pin.p, st))
+        return rc;
+  } else if (pwrite_full(w->fd, doclens, 4ull * count, w->h.doclens_off + 4 * d0) ||
+             pwrite_full(w->fd, tokens, per * count, w->h.tokens_off + per * d0) ||
+             (fp8 && pwrite_full(w->fd, scales, 256ull * count, w->h.scales_off + 256 * d0))) {
+    return err(CBV2_EINVAL, "%s: write failed (%s)", w->path, strerror(errno));
+  }
+  w->written += count;
+  return CBV2_OK;
+}
+
+int64_t cbv2_index_writer_count(const cbv2_index_writer* w) { return w ? w->written : -1; }
+
+int cbv2_index_writer_close(cbv2_index_writer* w) {
+  if (!w) return CBV2_OK;
+  int rc = CBV2_OK;
+  if (w->fd >= 0) {
+    if (w->written != w->h.n)
+      rc = err(CBV2_EINVAL, "%s: closed after %lld of %lld docs (left without a header)", w->path,
+               (long long)w->written, (long long)w->h.n);
+    else if (pwrite_full(w->fd, &w->h, sizeof(w->h), 0) || fsync(w->fd) != 0)
+      rc = err(CBV2_EINVAL, "%s: header write failed", w->path);
+    close(w->fd);
+  }
+  delete w;
+  return rc;
+}
+
 }  // extern "C"

@@ -418,6 +418,124 @@ class ColbertIndex:
         return out_s, out_i, out_p
 
 
+# --------------------------------------------------------------------- bounded-memory ingest
+def _as_batch(embs, device, dtype):
+    """Encoder output of one batch -> (tokens ``dtype`` [m, 128, 128], int32 doclens [m]) on ``device``."""
+    return pack_tokens(embs, device, dtype=dtype)
+
+
+class IndexBuilder:
+    """Builds an HBM-resident index batch by batch, so ingest never holds the
+    corpus's embeddings on the host (the reference encodes the whole corpus in
+    one ``model.encode`` call and keeps it, fp32, LRC:735-739).  Each batch of
+    encoder output is packed on the GPU and written into preallocated shard
+    tensors: cast to bf16, quantised to MXFP8 by the HIP quantizer, or split
+    into bf16 hi/lo by cbv2_split_f32 (fp32-faithful; the residual bounds
+    accumulate over the batches).  ``finish()`` returns the ColbertIndex."""
+
+    def __init__(self, n: int, device="cuda", dtype: str = "bf16", id_base: int = 0):
+        if dtype not in ("bf16", "fp8", "fp32"):
+            raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
+        self.n, self.dtype, self.id_base = int(n), dtype, int(id_base)
+        self.device = torch.device(device)
+        self.pos = 0
+        self.doclens = torch.zeros((self.n,), dtype=torch.int32, device=self.device)
+        if dtype == "fp8":
+            self.tokens = torch.empty((self.n, LD, DIM), dtype=torch.uint8, device=self.device)
+            self.scales = torch.empty((self.n, LD, 2), dtype=torch.uint8, device=self.device)
+        else:
+            self.tokens = torch.empty((self.n, LD, DIM), dtype=torch.bfloat16, device=self.device)
+            self.scales = None
+        if dtype == "fp32":
+            self.residual = torch.empty((self.n, LD, DIM), dtype=torch.bfloat16, device=self.device)
+            self.bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
+
+    def append(self, embs) -> int:
+        """Add the next batch of encoder output (dense [m, L, D], pooled [m, D] or a list
+        of [L_i, D]); returns the number of docs added."""
+        t, dl = _as_batch(embs, self.device, torch.float32 if self.dtype == "fp32" else torch.bfloat16)
+        m = int(t.shape[0])
+        if self.pos + m > self.n:
+            raise ValueError(f"batch of {m} docs past the declared {self.n} (have {self.pos})")
+        a, b = self.pos, self.pos + m
+        self.doclens[a:b] = dl
+        if self.dtype == "fp8":
+            q, sc = quantize_mxfp8(t)
+            self.tokens[a:b] = q
+            self.scales[a:b] = sc
+        elif self.dtype == "fp32":
+            t = t.contiguous()
+            hi, lo = self.tokens[a:b], self.residual[a:b]
+            _lib.check(_lib.lib().cbv2_split_f32(t.data_ptr(), m * LD, LD, self.doclens[a:b].data_ptr(),
+                                                 hi.data_ptr(), lo.data_ptr(), self.bounds.data_ptr(),
+                                                 _stream_ptr(self.device)))
+        else:
+            self.tokens[a:b] = t
+        del t
+        self.pos = b
+        return m
+
+    def finish(self) -> "ColbertIndex":
+        if self.pos != self.n:
+            raise ValueError(f"{self.pos} of {self.n} declared docs were appended")
+        if self.dtype == "fp32":
+            b = self.bounds.tolist()        # synchronises
+            return ColbertIndex(self.tokens, self.doclens, id_base=self.id_base, residual=self.residual,
+                                bounds=(b[0], b[1]))
+        return ColbertIndex(self.tokens, self.doclens, id_base=self.id_base, scales=self.scales)
+
+
+class IndexWriter:
+    """Streams batches straight into the native index file (cbv2_index_writer_*)
+    for corpora larger than HBM: each batch is cast (bf16) or quantised
+    (MXFP8, HIP) on the GPU and written through two 64 MiB pinned buffers, so
+    host memory does not grow with the corpus.  The file is valid only after
+    ``close()`` with every declared doc written."""
+
+    def __init__(self, path: str, n: int, dtype: str = "bf16", id_base: int = 0, device="cuda"):
+        if dtype not in ("bf16", "fp8"):
+            raise ValueError("the native file holds bf16 or MXFP8 tokens")
+        self.path, self.n, self.dtype = path, int(n), dtype
+        self.device = torch.device(device)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().cbv2_index_writer_open(os.fsencode(path), _lib.DTYPE_MXFP8 if dtype == "fp8"
+                                                     else _lib.DTYPE_BF16, self.n, int(id_base), ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def written(self) -> int:
+        return int(_lib.lib().cbv2_index_writer_count(self._h))
+
+    def append(self, embs) -> int:
+        t, dl = _as_batch(embs, self.device, torch.bfloat16)
+        m = int(t.shape[0])
+        sc = None
+        if self.dtype == "fp8":
+            t, sc = quantize_mxfp8(t)
+        t, dl = t.contiguous(), dl.contiguous()
+        _lib.check(_lib.lib().cbv2_index_writer_append(self._h, m, t.data_ptr(), sc.data_ptr() if sc is not None
+                                                       else None, dl.data_ptr(), 1, _stream_ptr(self.device)))
+        return m
+
+    def close(self) -> None:
+        if self._h is not None and self._h.value:
+            h, self._h = self._h, None
+            _lib.check(_lib.lib().cbv2_index_writer_close(h))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if et is None:
+            self.close()
+        else:                      # keep the original error; the file stays without a header
+            try:
+                self.close()
+            except Exception:
+                pass
+        return False
+
+
 # --------------------------------------------------------------------- free functions
 def index_file_info(path: str):
     """(ABI dtype, doc count, id_base) of a native index file."""

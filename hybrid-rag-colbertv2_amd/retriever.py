@@ -27,7 +27,7 @@ import torch
 
 from .config import RAGConfig
 from .encoder import load_local_encoder
-from .index import ColbertIndex, select_topk
+from .index import ColbertIndex, IndexBuilder, select_topk
 
 
 class JinaColBERTRetriever:
@@ -52,16 +52,56 @@ class JinaColBERTRetriever:
                                             build_means=(self.scorer == "ref_meanpool_cosine"),
                                             dtype=getattr(self.config, "index_dtype", "bf16"))
 
-    def index(self, corpus: List[str]) -> None:
-        """LRC:728-746: encode the corpus, keep it in HBM, save index.pt."""
+    def _encode_docs(self, texts: List[str]):
+        try:
+            return self.model.encode(texts, show_progress_bar=False, convert_to_tensor=True, is_query=False)
+        except TypeError:                         # encoders without the is_query keyword
+            return self.model.encode(texts, show_progress_bar=False, convert_to_tensor=True)
+
+    def index(self, corpus: List[str], batch_size: Optional[int] = None) -> None:
+        """LRC:728-746: encode the corpus, keep it in HBM, persist it.
+
+        The reference encodes the whole corpus in one call and torch.saves the
+        fp32 embeddings (host memory grows with the corpus: 65 GB at 1M docs x
+        128 tokens).  Here the corpus is encoded ``config.ingest_batch`` docs at a
+        time and each batch goes straight into the HBM index (cast / quantised
+        / split on the GPU: ``IndexBuilder``), so host memory stays bounded.
+        Persistence: a corpus of at most ``config.index_pt_max_docs`` docs is
+        also saved as the reference's ``index.pt`` (its fp32 embeddings, kept
+        per batch on the host); a larger one as the native ``index.cbv2``
+        (streamed from HBM through pinned buffers) + ``index.corpus.json``."""
         self.corpus = corpus
-        print(f"  Encoding {len(corpus)} documents...")
-        embeddings = self.model.encode(corpus, show_progress_bar=True, convert_to_tensor=True, is_query=False)
-        self.corpus_embeddings = self._build(embeddings)
+        n = len(corpus)
+        bs = int(batch_size or getattr(self.config, "ingest_batch", 256))
+        keep_pt = n <= int(getattr(self.config, "index_pt_max_docs", 50_000))
+        dtype = getattr(self.config, "index_dtype", "bf16")
+        print(f"  Encoding {n} documents...")
+        if self.scorer == "ref_meanpool_cosine" or n == 0:
+            # the literal scorer needs every doc's fp32 means: one pass as the reference does
+            embeddings = self._encode_docs(corpus) if n else torch.zeros((0, 1, 128))
+            self.corpus_embeddings = self._build(embeddings)
+            host = [embeddings.cpu()] if isinstance(embeddings, torch.Tensor) else [[e.cpu() for e in embeddings]]
+        else:
+            builder = IndexBuilder(n, device=self.device, dtype=dtype)
+            host = []
+            for a in range(0, n, bs):
+                emb = self._encode_docs(corpus[a:a + bs])
+                builder.append(emb)
+                if keep_pt:
+                    host.append(emb.cpu() if isinstance(emb, torch.Tensor) else [e.cpu() for e in emb])
+                del emb
+            self.corpus_embeddings = builder.finish()
         os.makedirs(self.config.colbert_index_path, exist_ok=True)
-        saved = embeddings.cpu() if isinstance(embeddings, torch.Tensor) else [e.cpu() for e in embeddings]
-        torch.save({"embeddings": saved, "corpus": corpus},
-                   os.path.join(self.config.colbert_index_path, "index.pt"))
+        if keep_pt:
+            if host and all(isinstance(h, torch.Tensor) for h in host) and \
+                    len({tuple(h.shape[1:]) for h in host}) == 1:
+                saved = torch.cat(host, 0)
+            else:
+                saved = [e for h in host for e in (h if isinstance(h, list) else list(h.unbind(0)))]
+            torch.save({"embeddings": saved, "corpus": corpus},
+                       os.path.join(self.config.colbert_index_path, "index.pt"))
+        elif not self.corpus_embeddings.faithful:
+            self.save_native()
 
     def load(self) -> None:
         """LRC:748-753 (reads the reference's own index.pt format; never unpickles code).

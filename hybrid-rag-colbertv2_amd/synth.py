@@ -159,3 +159,29 @@ def bm25_shard(begin: int, end: int, planted: np.ndarray, q_len: int = 6, vocab:
     offsets[1:] = np.cumsum(lens)
     terms = np.concatenate(rows_t).astype(np.int32) if rows_t else np.zeros(0, np.int32)
     return terms, offsets, vocab
+
+
+class SyntheticDocEncoder:
+    """Encoder stand-in for ingest at scale: ``encode(texts)`` for texts
+    ``"synthetic doc <id>"`` returns the synthetic corpus's tokens of those
+    global ids (bf16 [m, 128, 128] on ``device``, generated by ``make_shard``),
+    so a 1M-doc ingest needs no real model and no host-side embeddings.  The
+    ids of one call must be consecutive (ingest batches are)."""
+
+    def __init__(self, Q: torch.Tensor, planted: np.ndarray, device, seed: int = 0):
+        self.Q, self.planted, self.device, self.seed = Q, planted, torch.device(device), seed
+
+    @staticmethod
+    def texts(begin: int, end: int):
+        return [f"synthetic doc {i}" for i in range(begin, end)]
+
+    def encode(self, texts, convert_to_tensor: bool = True, **_unused):
+        texts = [texts] if isinstance(texts, str) else list(texts)
+        ids = [int(t.rsplit(" ", 1)[1]) for t in texts]
+        if not ids:
+            return torch.zeros((0, LD, DIM), dtype=torch.bfloat16, device=self.device)
+        a, b = ids[0], ids[-1] + 1
+        if ids != list(range(a, b)):
+            raise ValueError("SyntheticDocEncoder encodes consecutive doc ids only")
+        tokens, _ = make_shard(a, b, self.Q, self.planted, self.device, seed=self.seed)
+        return tokens

@@ -86,7 +86,9 @@ int cbv2_index_time_scans(cbv2_index* index, int32_t enable);
 int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
 
 /* Handle options (A/B and tests; defaults = production):
- *  CBV2_OPT_FUSED_TOPK   1: cbv2_search fuses the top-k into eligible scans.
+ *  CBV2_OPT_FUSED_TOPK   1: cbv2_search fuses the top-k into eligible scans
+ *                        (the bf16 doc-interleaved scan; 2 also fuses the
+ *                        MXFP8 scan, which is slower fused: A/B only).
  *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
  *                        as dynamic tasks (0: static chunks only).
  * cbv2_index_last_scan_plan: the work split of this handle's latest scan
@@ -141,8 +143,8 @@ int cbv2_score(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype
  * counters, so concurrent calls on distinct streams need distinct workspaces)
  * must hold cbv2_search_workspace_size(index, B, k, scorer) bytes;
  * cbv2_search_workspace_bytes(index, B) is enough for any k and scorer.
- * MaxSim with k <= 104 on the doc-interleaved scans (bf16 B > 16, MXFP8 B > 8)
- * fuses the top-k into the scan (no [B][n] score matrix: each workgroup keeps
+ * MaxSim with k <= 104 on the bf16 doc-interleaved scan (B > 16) fuses the
+ * top-k into the scan (no [B][n] score matrix: each workgroup keeps
  * its best k per query in LDS, then one selection per query); results are
  * those of the unfused path bit for bit (CBV2_OPT_FUSED_TOPK turns it off).
  * Extends §8(b)'s prototype with scorer / q_dtype / workspace.  */
@@ -308,6 +310,19 @@ int cbv2_index_file_write_host(const char* path, int32_t dtype, int64_t n, const
                                const int32_t* doclens, int64_t id_base);
 int cbv2_index_file_read_host(const char* path, int64_t begin, int64_t end, void* tokens, void* scales,
                               int32_t* doclens);
+
+/* Streaming index writer (bounded-memory ingest): declare the
+ * doc count, append contiguous batches (DEVICE pointers with on_device = 1 --
+ * D2H through 64 MiB pinned buffers on `stream` -- or HOST pointers), close.
+ * The header is written by close() only when every declared doc was
+ * appended, so an interrupted ingest never leaves a file that reads as valid.
+ * Host memory is two staging buffers whatever the corpus size.             */
+typedef struct cbv2_index_writer cbv2_index_writer;
+int cbv2_index_writer_open(const char* path, int32_t dtype, int64_t n, int64_t id_base, cbv2_index_writer** out);
+int cbv2_index_writer_append(cbv2_index_writer* w, int64_t count, const void* tokens, const void* scales,
+                             const int32_t* doclens, int32_t on_device, void* stream);
+int64_t cbv2_index_writer_count(const cbv2_index_writer* w);
+int cbv2_index_writer_close(cbv2_index_writer* w);
 
 /* Multi-GPU exchange (SURVEY.md §8(b) "cbv2_comm_init(ncclComm_t) +
  * cbv2_search_sharded", §8(e)).  No reference counterpart: the reference is

@@ -81,3 +81,48 @@ def test_validation(tmp_path):
         f.truncate(4096 + 4096 + 100)
     with pytest.raises(ValueError):
         index_file_info(path)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_streaming_writer_host_batches(tmp_path, fp8):
+    """cbv2_index_writer_*: contiguous batches appended (host pointers) give the
+    same file as one whole write; the header appears only at a complete close."""
+    import ctypes
+    L = _lib()
+    rng = np.random.default_rng(5)
+    n = 29
+    elem = np.uint8 if fp8 else np.uint16
+    tokens = rng.integers(0, 255 if fp8 else 65535, size=(n, 128, 128)).astype(elem)
+    scales = rng.integers(0, 255, size=(n, 128, 2)).astype(np.uint8) if fp8 else None
+    doclens = rng.integers(0, 129, size=n).astype(np.int32)
+    dt = L.DTYPE_MXFP8 if fp8 else L.DTYPE_BF16
+    whole, streamed = str(tmp_path / "whole.cbv2"), str(tmp_path / "streamed.cbv2")
+    _write(whole, dt, tokens, scales, doclens, id_base=77)
+    h = ctypes.c_void_p()
+    L.check(L.lib().cbv2_index_writer_open(os.fsencode(streamed), dt, n, 77, ctypes.byref(h)))
+    for a, b in [(0, 10), (10, 11), (11, 11), (11, 29)]:
+        t, d = np.ascontiguousarray(tokens[a:b]), np.ascontiguousarray(doclens[a:b])
+        sc = np.ascontiguousarray(scales[a:b]) if fp8 else None
+        L.check(L.lib().cbv2_index_writer_append(h, b - a, t.ctypes.data, sc.ctypes.data if fp8 else None,
+                                                 d.ctypes.data, 0, None))
+    assert L.lib().cbv2_index_writer_count(h) == n
+    with pytest.raises(ValueError):                         # past the declared count
+        L.check(L.lib().cbv2_index_writer_append(h, 1, tokens.ctypes.data, None, doclens.ctypes.data, 0, None))
+    L.check(L.lib().cbv2_index_writer_close(h))
+    assert open(whole, "rb").read() == open(streamed, "rb").read()
+
+
+def test_streaming_writer_incomplete_file_is_invalid(tmp_path):
+    import ctypes
+    L = _lib()
+    path = str(tmp_path / "partial.cbv2")
+    tokens = np.zeros((3, 128, 128), np.uint16)
+    doclens = np.full(3, 128, np.int32)
+    h = ctypes.c_void_p()
+    L.check(L.lib().cbv2_index_writer_open(os.fsencode(path), L.DTYPE_BF16, 10, 0, ctypes.byref(h)))
+    L.check(L.lib().cbv2_index_writer_append(h, 3, tokens.ctypes.data, None, doclens.ctypes.data, 0, None))
+    with pytest.raises(ValueError):
+        L.check(L.lib().cbv2_index_writer_close(h))
+    from hybrid_rag_colbertv2_amd.index import index_file_info
+    with pytest.raises(ValueError):
+        index_file_info(path)

@@ -330,6 +330,29 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   // kind 12: the B <= 16 production shape (kind 6) phase-stamped
   if (kind == 12 && stamps != nullptr)
     return launch_scan16x4<4, 4, 2, 2, 2, true, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps);
+  // kind 13: production shape (round 2: SPLITLOAD, waves 0-3 issue all LDS-DMA
+  // pieces; kind 0 is the round-1 shape, every wave issuing its own); kind 14:
+  // its phase-stamped build; kind 15 / 16: the fused top-k build (k = 100,
+  // keys into `out`) without / with SPLITLOAD (16 = what cbv2_search runs).
+  // Round 2, one box, 1M docs B=256: k0 145.25, k13 144.10, k15 146.33, k16
+  // 145.58 ms; phase stamps per iteration (cycles, waves 0-3 | 4-7): k0 wait
+  // 4288 | 111, issue 762 | 1599, compute 13211 | 16548; k14 wait 3919 | 116,
+  // issue 1405 | 398, compute 12642 | 17459 (r02c)
+  if (kind == 13)
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                        task_docs);
+  if (kind == 14 && stamps != nullptr)
+    return launch_scan16x4<8, 4, 1, 2, 2, true, 64, 2, false, 0, true>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                       task_docs, (uint64_t*)stamps);
+  if (kind == 15 || kind == 16) {
+    FusedTopk ft{(uint64_t*)out, 100, scan_chunks(ix, (B + 31) / 32, cu_count(ix->device)), 0};
+    if ((int64_t)B * ft.max_slots * 100 * 8 > ld * (int64_t)B * 4) return -1;   // keys must fit the buffer
+    if (kind == 15)
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, false>(
+          ix, q, B, lq, nullptr, 0, st, dyn_frac, task_docs, nullptr, nullptr, &ft);
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, true>(
+        ix, q, B, lq, nullptr, 0, st, dyn_frac, task_docs, nullptr, nullptr, &ft);
+  }
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,

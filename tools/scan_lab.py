@@ -153,7 +153,16 @@ def stamps_report(run_stamped, n_wg_max=1 << 16):
           f"tail loss (span/median - 1) {span / np.median(dur) - 1:.2%}; clock GHz min {clk.min():.3f} "
           f"median {np.median(clk):.3f} max {clk.max():.3f}", flush=True)
     ph = buf.cpu().numpy()[16384:].astype(np.float64)          # per-wave phase cycles (s_memtime)
-    ph = ph[ph[:, 3] > 0]
+    wv = np.arange(len(ph)) % 8                                 # row 16384 + 8 * bid + wave
+    keep = ph[:, 3] > 0
+    ph, wv = ph[keep], wv[keep]
+    for lo, hi in ((0, 4), (4, 8)):                            # SPLITLOAD: loader waves 0-3 vs 4-7
+        sel = (wv >= lo) & (wv < hi)
+        if sel.any():
+            p2 = ph[sel]
+            print(f"  waves {lo}-{hi - 1}: per iteration cycles wait {np.median(p2[:, 0] / p2[:, 3]):.0f} "
+                  f"issue {np.median(p2[:, 1] / p2[:, 3]):.0f} compute {np.median(p2[:, 2] / p2[:, 3]):.0f}",
+                  flush=True)
     if len(ph):
         tot = ph[:, :3].sum(axis=1)
         fr = ph[:, :3] / tot[:, None]
