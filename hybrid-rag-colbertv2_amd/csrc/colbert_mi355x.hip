@@ -3378,51 +3378,4 @@ int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32
   return launch_check("merge_topk_kernel");
 }
 
-// Host-side reciprocal rank fusion (HOST pointers).  Restates
-// HybridRetriever._reciprocal_rank_fusion (local_rag_complete.py:960-978):
-// score[id] += 1.0 / (rrf_k + rank) over the BM25 list, then the ColBERT list
-// (rank 1-based, float64, same operation order as the Python), then a STABLE
-// sort by score descending, so ties keep first-insertion order.  ids < 0 are
-// padding and skipped.  Writes the first C fused ids/scores per query (-1 / 0
-// padded); out_count (nullable) receives the number of distinct ids.
-int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_ids, int32_t kc, int32_t B,
-                  int32_t rrf_k, int32_t C, int32_t* out_ids, double* out_scores, int32_t* out_count) {
-  CBV2_REQUIRE(B >= 1 && C >= 1 && kb >= 0 && kc >= 0, "bad sizes");
-  CBV2_REQUIRE((kb == 0 || bm25_ids) && (kc == 0 || colbert_ids) && out_ids, "null pointer");
-  std::vector<int32_t> ids;
-  std::vector<double> sc;
-  std::vector<int> order;
-  ids.reserve(kb + kc);
-  sc.reserve(kb + kc);
-  for (int32_t b = 0; b < B; ++b) {
-    ids.clear();
-    sc.clear();
-    auto add = [&](int32_t id, int32_t rank) {
-      const double inc = 1.0 / (double)(rrf_k + rank);
-      for (size_t j = 0; j < ids.size(); ++j)
-        if (ids[j] == id) { sc[j] = sc[j] + inc; return; }
-      ids.push_back(id);
-      sc.push_back(0.0 + inc);
-    };
-    for (int32_t r = 0; r < kb; ++r) {
-      const int32_t id = bm25_ids[(size_t)b * kb + r];
-      if (id >= 0) add(id, r + 1);
-    }
-    for (int32_t r = 0; r < kc; ++r) {
-      const int32_t id = colbert_ids[(size_t)b * kc + r];
-      if (id >= 0) add(id, r + 1);
-    }
-    order.resize(ids.size());
-    for (size_t j = 0; j < ids.size(); ++j) order[j] = (int)j;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return sc[a] > sc[c]; });
-    for (int32_t j = 0; j < C; ++j) {
-      const bool ok = j < (int32_t)order.size();
-      out_ids[(size_t)b * C + j] = ok ? ids[order[j]] : -1;
-      if (out_scores) out_scores[(size_t)b * C + j] = ok ? sc[order[j]] : 0.0;
-    }
-    if (out_count) out_count[b] = (int32_t)ids.size();
-  }
-  return CBV2_OK;
-}
-
 }  // extern "C"

@@ -241,27 +241,29 @@ postlude:
   return w;
 }
 
-// UTF-8 <-> code points (invalid bytes pass through as single code points).
+// UTF-8 <-> code points.  A byte that does not start a valid sequence (or
+// starts one encoding a surrogate) becomes U+DC00 + byte, a non-vowel, and is
+// written back as that single byte (Python's "surrogateescape"), so no stem
+// is ever longer in bytes than its word.
 W decode(const char* s, size_t n) {
   W w;
   w.reserve(n);
   for (size_t i = 0; i < n;) {
     const unsigned char c = (unsigned char)s[i];
     int len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
-    if (len == 0 || i + len > n) {
-      w.push_back(c);
-      ++i;
-      continue;
-    }
-    char32_t cp = len == 1 ? c : len == 2 ? (c & 0x1f) : len == 3 ? (c & 0x0f) : (c & 0x07);
-    bool ok = true;
-    for (int k = 1; k < len; ++k) {
-      const unsigned char d = (unsigned char)s[i + k];
-      if ((d >> 6) != 2) { ok = false; break; }
-      cp = (cp << 6) | (d & 0x3f);
+    char32_t cp = 0;
+    bool ok = len > 0 && i + len <= n;
+    if (ok) {
+      cp = len == 1 ? c : len == 2 ? (c & 0x1f) : len == 3 ? (c & 0x0f) : (c & 0x07);
+      for (int k = 1; k < len && ok; ++k) {
+        const unsigned char d = (unsigned char)s[i + k];
+        ok = (d >> 6) == 2;
+        cp = (cp << 6) | (d & 0x3f);
+      }
+      ok = ok && !(cp >= 0xD800 && cp <= 0xDFFF) && cp <= 0x10FFFF;
     }
     if (!ok) {
-      w.push_back(c);
+      w.push_back(0xDC00 + c);
       ++i;
       continue;
     }
@@ -272,7 +274,9 @@ W decode(const char* s, size_t n) {
 }
 void encode(const W& w, std::string& out) {
   for (char32_t cp : w) {
-    if (cp < 0x80) {
+    if (cp >= 0xDC80 && cp <= 0xDCFF) {   // an escaped raw byte
+      out.push_back((char)(cp - 0xDC00));
+    } else if (cp < 0x80) {
       out.push_back((char)cp);
     } else if (cp < 0x800) {
       out.push_back((char)(0xc0 | (cp >> 6)));

@@ -77,8 +77,8 @@ def encode_queries_sharded(encoder, queries, device=None, dtype=torch.bfloat16,
     dist.all_reduce(shape, op=dist.ReduceOp.MAX, group=group)
     lq, d = int(shape[0]), int(shape[1])
     send = torch.zeros((per, lq, d), dtype=dtype, device=dev)
-    if mine is not None:
-        send[: b1 - b0].copy_(mine)
+    if mine is not None:   # an encoder that does not pad to Lq: zero rows add 0 to every MaxSim sum
+        send[: b1 - b0, : mine.shape[1], : mine.shape[2]].copy_(mine)
     out = torch.empty((G, per, lq, d), dtype=dtype, device=dev)
     if nccl:
         dist.all_gather_into_tensor(out, send, group=group)
@@ -110,11 +110,13 @@ class _PinnedStage:
     that stalls the host until batch j+1's scan ends before it can fuse batch j
     and leaves the GPU idle for the host steps.  Here the array is copied into
     a pinned buffer and uploaded with ``non_blocking=True``; buffers rotate
-    over ``slots`` calls (the pipeline keeps at most two batches in flight, and
-    a slot is reused only after the host has waited for a later batch)."""
+    over ``slots`` calls, and each slot's upload is followed by an event that
+    the host waits on before it overwrites that slot again (a caller that loops
+    faster than the stream drains never corrupts a pending upload)."""
 
     def __init__(self, slots: int = 2):
         self._bufs = [None] * slots
+        self._events = [None] * slots
         self._next = 0
 
     def upload(self, arr: np.ndarray, device) -> torch.Tensor:
@@ -124,13 +126,19 @@ class _PinnedStage:
             return src.clone()
         k = self._next
         self._next = (k + 1) % len(self._bufs)
+        if self._events[k] is not None:
+            self._events[k].synchronize()          # the slot's previous upload has been consumed
         buf = self._bufs[k]
         if buf is None or buf.numel() < src.numel() * src.element_size():
             buf = torch.empty((src.numel() * src.element_size(),), dtype=torch.uint8, pin_memory=True)
             self._bufs[k] = buf
         h = buf[: src.numel() * src.element_size()].view(src.dtype).view(src.shape)
         h.copy_(src)
-        return h.to(device, non_blocking=True)
+        out = h.to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self._events[k] = ev
+        return out
 
 
 class NativeExchange:

@@ -200,3 +200,49 @@ def test_sharded_query_encoding_equals_single_process():
         for _, outs in res:
             assert np.array_equal(outs[0], want[0]) and np.array_equal(outs[1], want[1])
             assert outs[2].shape[0] == 0
+
+
+class _UnpaddedEncoder:
+    """Query encoder that does NOT pad to a fixed Lq: a batch comes out
+    [b, max words in the batch, 128], shorter queries zero-padded."""
+
+    def encode(self, texts, convert_to_tensor=True, **_):
+        from hybrid_rag_colbertv2_amd.encoder import FakeEncoder
+        fe = FakeEncoder(maxlen=64)
+        rows = [[w for w in fe.tokenize(t) if not w.startswith("[PAD]")] for t in texts]
+        L = max([len(r) for r in rows] + [1])
+        out = torch.zeros((len(texts), L, 128))
+        for i, r in enumerate(rows):
+            for j, w in enumerate(r):
+                out[i, j] = torch.from_numpy(fe._vec(w))
+        return out
+
+
+def _ragged_encode_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hybrid_rag_colbertv2_amd.distributed import encode_queries_sharded
+        q.put((rank, encode_queries_sharded(_UnpaddedEncoder(), _QUERIES).float().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_query_encoding_unpadded_encoder():
+    """Ranks whose slices encode to different Lq: the gathered batch is
+    the single-process encode, zero rows added where a rank's Lq was shorter."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_encode_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _UnpaddedEncoder().encode(_QUERIES).to(torch.bfloat16).float().numpy()
+    for _, got in res:
+        assert np.array_equal(got, want)
