@@ -1593,11 +1593,16 @@ __device__ void bitonic_desc(uint64_t* keys, int P) {
 // Exact selection of the kk largest keys of row x into sel[0..kk) (unordered).
 // Radix select on the 32-bit score key (11/11/10-bit digits); if the kk-th
 // score is tied, a second radix select over ~index keeps the lowest indices.
+// BOUNDED: only entries whose ranking key is < bound take part (the next
+// pass of a multi-pass selection: bound = the previous pass's smallest key).
+template <bool BOUNDED = false>
 __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, uint64_t* sel, uint32_t* hist,
-                               uint32_t* s_bin, uint32_t* s_above, uint32_t* s_bincount, uint32_t* s_cnt) {
+                               uint32_t* s_bin, uint32_t* s_above, uint32_t* s_bincount, uint32_t* s_cnt,
+                               uint64_t bound = ~0ull) {
   const int tid = threadIdx.x, nth = blockDim.x;
   const int wave = tid >> 6;
-  if (kk == n) {
+  auto live = [&](float v, int64_t i) { return !BOUNDED || rank_key(v, (uint32_t)i) < bound; };
+  if (!BOUNDED && kk == n) {
     for (int i = tid; i < kk; i += nth) sel[i] = rank_key(x[i], (uint32_t)i);
     __syncthreads();
     return;
@@ -1610,8 +1615,9 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
     for (int b = tid; b < nb; b += nth) hist[b] = 0;
     __syncthreads();
     for (int64_t i = tid; i < n; i += nth) {
-      const uint32_t u = f2u(x[i]);
-      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shifts[p]) & (nb - 1)], 1u);
+      const float v = x[i];
+      const uint32_t u = f2u(v);
+      if ((u & mask) == prefix && live(v, i)) atomicAdd(&hist[(u >> shifts[p]) & (nb - 1)], 1u);
     }
     __syncthreads();
     if (wave == 0) find_bin(hist, nb, kleft, s_bin, s_above, s_bincount);
@@ -1632,7 +1638,9 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
       __syncthreads();
       for (int64_t i = tid; i < n; i += nth) {
         const uint32_t key2 = ~(uint32_t)i;
-        if (f2u(x[i]) == ustar && (key2 & imask) == iprefix) atomicAdd(&hist[(key2 >> shifts[p]) & (nb - 1)], 1u);
+        const float v = x[i];
+        if (f2u(v) == ustar && (key2 & imask) == iprefix && live(v, i))
+          atomicAdd(&hist[(key2 >> shifts[p]) & (nb - 1)], 1u);
       }
       __syncthreads();
       if (wave == 0) find_bin(hist, nb, kl2, s_bin, s_above, s_bincount);
@@ -1647,8 +1655,9 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
   if (tid == 0) *s_cnt = 0;
   __syncthreads();
   for (int64_t i = tid; i < n; i += nth) {
-    const uint32_t u = f2u(x[i]);
-    if (u > ustar || (u == ustar && (uint32_t)i <= id_thr)) {
+    const float v = x[i];
+    const uint32_t u = f2u(v);
+    if ((u > ustar || (u == ustar && (uint32_t)i <= id_thr)) && live(v, i)) {
       const uint32_t pos = atomicAdd(s_cnt, 1u);
       if (pos < (uint32_t)kk) sel[pos] = ((uint64_t)u << 32) | (uint32_t)(~(uint32_t)i);
     }
@@ -1688,6 +1697,61 @@ __global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __re
   const int kk = (int)((int64_t)k < n ? k : n);
   topk_exact_row(x, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
   sort_and_write(sel, kk, k, id_base, out_s + (size_t)blockIdx.x * k, out_i + (size_t)blockIdx.x * k);
+}
+
+// ---------------------------------------------------------------------------
+// Multi-pass selection for k beyond one LDS sort (torch.topk takes any k,
+// local_rag_complete.py:767; argsort any C, :789): passes of up to PASS keys,
+// each an exact selection restricted to keys below the previous pass's
+// smallest (topk_exact_row<true>), sorted in LDS and written at its offset.
+// Same keys and tie rule (score desc, lower index first) as every other path.
+// ids_row (nullable) maps index -> id (else id_base + index); out_i / out_p
+// (nullable) receive ids / indices.  Slots past min(k, n): -inf / -1 / -1.
+// ---------------------------------------------------------------------------
+template <int PASS>
+__device__ void topk_multi_row(const float* x, int64_t n, int k, const int32_t* ids_row, int64_t id_base,
+                               float* out_s, int32_t* out_i, int32_t* out_p, uint64_t* sel, uint32_t* hist,
+                               uint32_t* misc) {
+  const int kk_total = (int)((int64_t)k < n ? k : n);
+  uint64_t bound = ~0ull;
+  for (int off = 0; off < kk_total; off += PASS) {
+    const int kk = kk_total - off < PASS ? kk_total - off : PASS;
+    topk_exact_row<true>(x, n, kk, sel, hist, misc, misc + 1, misc + 2, misc + 3, bound);
+    int P = 1;
+    while (P < kk) P <<= 1;
+    for (int i = kk + threadIdx.x; i < P; i += blockDim.x) sel[i] = 0;
+    bitonic_desc(sel, P);
+    for (int j = threadIdx.x; j < kk; j += blockDim.x) {
+      const uint64_t key = sel[j];
+      const uint32_t idx = ~(uint32_t)key;
+      out_s[off + j] = u2f((uint32_t)(key >> 32));
+      if (out_i) out_i[off + j] = ids_row ? ids_row[idx] : (int32_t)(id_base + (int64_t)idx);
+      if (out_p) out_p[off + j] = (int32_t)idx;
+    }
+    bound = sel[kk - 1];
+    __syncthreads();  // every thread has read sel before the next pass refills it
+  }
+  for (int j = kk_total + threadIdx.x; j < k; j += blockDim.x) {
+    out_s[j] = neg_inf();
+    if (out_i) out_i[j] = -1;
+    if (out_p) out_p[j] = -1;
+  }
+}
+
+constexpr int kMultiPass = 4096;  // keys sorted per pass (32 KiB of LDS)
+__global__ __launch_bounds__(kTkThreads) void topk_multi_kernel(const float* __restrict__ scores, int64_t n,
+                                                                int64_t ld, int k, int64_t id_base,
+                                                                const int32_t* __restrict__ ids, int64_t ids_ld,
+                                                                float* __restrict__ out_s, int32_t* __restrict__ out_i,
+                                                                int32_t* __restrict__ out_p,
+                                                                const int32_t* __restrict__ only_neg = nullptr) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint64_t sel[kMultiPass];
+  __shared__ uint32_t misc[4];
+  if (only_neg != nullptr && only_neg[blockIdx.x] >= 0) return;  // block-uniform: rows flagged < 0 only
+  const size_t b = blockIdx.x;
+  topk_multi_row<kMultiPass>(scores + b * ld, n, k, ids ? ids + b * ids_ld : nullptr, id_base, out_s + b * k,
+                             out_i ? out_i + b * k : nullptr, out_p ? out_p + b * k : nullptr, sel, hist, misc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1884,66 +1948,96 @@ __global__ __launch_bounds__(256) void select_small_kernel(const float* __restri
 // ---------------------------------------------------------------------------
 // Rerank: one workgroup per query; each wave gathers whole candidate docs
 // (32 KiB, contiguous) straight into VGPRs and scores them with the same MFMA
-// tiling as the scan; then rank-select top-k in LDS.
+// tiling as the scan; then rank-select top-k in LDS.  BIG (C > kSmallMax): the
+// C raw scores live in dynamic LDS (C <= kRerankMaxC) and the selection is the
+// multi-pass one (any k).
 // ---------------------------------------------------------------------------
 constexpr int kRrWaves = 8;
-__global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
-    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
-    const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, int k,
-    float* __restrict__ out_s, int32_t* __restrict__ out_i, int32_t* __restrict__ out_p) {
-  __shared__ float sc[kSmallMax];
-  __shared__ uint64_t keys[kSmallMax];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b = blockIdx.x;
-  bf16x8 qf[1][2][4];
-  load_qfrag16(Q, b, b + 1, lq, lane, qf[0]);
+constexpr int kRerankMaxC = 32768;   // BIG: 128 KiB of scores + 16 KiB of selection state
+
+__device__ __forceinline__ float rerank_one_bf16(const uint8_t* __restrict__ tokens,
+                                                 const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
+                                                 const bf16x8 (&qf)[1][2][4], int lq, int32_t id, int lane) {
+  const int64_t loc = (int64_t)id - id_base;
+  if (id < 0 || loc < 0 || loc >= n) return neg_inf();
   const int g = lane >> 4;
-  const int32_t* crow = cand + (size_t)b * C;
-  for (int c = wave; c < C; c += kRrWaves) {
-    const int32_t id = crow[c];
-    const int64_t loc = (int64_t)id - id_base;
-    float v = neg_inf();
-    if (id >= 0 && loc >= 0 && loc < n) {
-      int dl = doclens[loc];
-      dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-      const uint8_t* dbase = tokens + (size_t)loc * kDocBytes;
-      // the whole doc in flight at once (32 KiB per wave), then the scan's math
-      bf16x8 af[kLd / 16][4];
+  int dl = doclens[loc];
+  dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+  const uint8_t* dbase = tokens + (size_t)loc * kDocBytes;
+  // the whole doc in flight at once (32 KiB per wave), then the scan's math
+  bf16x8 af[kLd / 16][4];
 #pragma unroll
-      for (int rt = 0; rt < kLd / 16; ++rt)
-        if (16 * rt < dl) gbl_afrag16(dbase, rt, lane, af[rt]);
-      float m[1][2] = {{neg_inf(), neg_inf()}};
+  for (int rt = 0; rt < kLd / 16; ++rt)
+    if (16 * rt < dl) gbl_afrag16(dbase, rt, lane, af[rt]);
+  float m[1][2] = {{neg_inf(), neg_inf()}};
 #pragma unroll
-      for (int rt = 0; rt < kLd / 16; ++rt) {
-        if (16 * rt < dl) {
-          const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-          tile16<1>(af[rt], qf, init, m);
-        }
-      }
-      v = reduce16(m[0][0], m[0][1], lane, lq);
+  for (int rt = 0; rt < kLd / 16; ++rt) {
+    if (16 * rt < dl) {
+      const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+      tile16<1>(af[rt], qf, init, m);
     }
-    if (lane == 0) sc[c] = v;
   }
+  return reduce16(m[0][0], m[0][1], lane, lq);
+}
+
+// The selection tail shared by the bf16 and MXFP8 rerank kernels: sc[0..C) raw
+// candidate scores (LDS) -> raw output (k == 0) or the top-k by position rule.
+template <bool BIG>
+__device__ __forceinline__ void rerank_finish(float* sc, uint64_t* keys, uint32_t* hist, uint32_t* misc, int b,
+                                              const int32_t* crow, int C, int k, float* __restrict__ out_s,
+                                              int32_t* __restrict__ out_i, int32_t* __restrict__ out_p) {
   __syncthreads();
   if (k == 0) {
     for (int t = threadIdx.x; t < C; t += blockDim.x) out_s[(size_t)b * C + t] = sc[t];
     return;
   }
-  for (int t = threadIdx.x; t < C; t += blockDim.x) keys[t] = rank_key(sc[t], (uint32_t)t);
-  __syncthreads();
-  select_from_lds(sc, keys, C, k, crow, out_s + (size_t)b * k, out_i + (size_t)b * k,
-                  out_p ? out_p + (size_t)b * k : nullptr);
+  if constexpr (BIG) {
+    topk_multi_row<kTopkMax>(sc, C, k, crow, 0, out_s + (size_t)b * k, out_i + (size_t)b * k,
+                             out_p ? out_p + (size_t)b * k : nullptr, keys, hist, misc);
+  } else {
+    for (int t = threadIdx.x; t < C; t += blockDim.x) keys[t] = rank_key(sc[t], (uint32_t)t);
+    __syncthreads();
+    select_from_lds(sc, keys, C, k, crow, out_s + (size_t)b * k, out_i + (size_t)b * k,
+                    out_p ? out_p + (size_t)b * k : nullptr);
+  }
 }
 
+template <bool BIG = false>
+__global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
+    const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, int k,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i, int32_t* __restrict__ out_p) {
+  extern __shared__ float sc_dyn[];
+  __shared__ float sc_fix[BIG ? 1 : kSmallMax];
+  __shared__ uint64_t keys[BIG ? kTopkMax : kSmallMax];
+  __shared__ uint32_t hist[BIG ? 2048 : 1];
+  __shared__ uint32_t misc[4];
+  float* sc = BIG ? sc_dyn : sc_fix;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x;
+  bf16x8 qf[1][2][4];
+  load_qfrag16(Q, b, b + 1, lq, lane, qf[0]);
+  const int32_t* crow = cand + (size_t)b * C;
+  for (int c = wave; c < C; c += kRrWaves) {
+    const float v = rerank_one_bf16(tokens, doclens, n, id_base, qf, lq, crow[c], lane);
+    if (lane == 0) sc[c] = v;
+  }
+  rerank_finish<BIG>(sc, keys, hist, misc, b, crow, C, k, out_s, out_i, out_p);
+}
 
+template <bool BIG = false>
 __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, int64_t id_base, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int lq,
     const int32_t* __restrict__ cand, int C, int k, float* __restrict__ out_s, int32_t* __restrict__ out_i,
     int32_t* __restrict__ out_p) {
-  __shared__ float sc[kSmallMax];
-  __shared__ uint64_t keys[kSmallMax];
+  extern __shared__ float sc_dyn[];
+  __shared__ float sc_fix[BIG ? 1 : kSmallMax];
+  __shared__ uint64_t keys[BIG ? kTopkMax : kSmallMax];
+  __shared__ uint32_t hist[BIG ? 2048 : 1];
+  __shared__ uint32_t misc[4];
+  float* sc = BIG ? sc_dyn : sc_fix;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
@@ -1978,15 +2072,7 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
     }
     if (lane == 0) sc[c] = v;
   }
-  __syncthreads();
-  if (k == 0) {
-    for (int t = threadIdx.x; t < C; t += blockDim.x) out_s[(size_t)b * C + t] = sc[t];
-    return;
-  }
-  for (int t = threadIdx.x; t < C; t += blockDim.x) keys[t] = rank_key(sc[t], (uint32_t)t);
-  __syncthreads();
-  select_from_lds(sc, keys, C, k, crow, out_s + (size_t)b * k, out_i + (size_t)b * k,
-                  out_p ? out_p + (size_t)b * k : nullptr);
+  rerank_finish<BIG>(sc, keys, hist, misc, b, crow, C, k, out_s, out_i, out_p);
 }
 
 // ---------------------------------------------------------------------------
@@ -2251,40 +2337,56 @@ __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __
 // Merge G sorted per-shard lists: rank = own position + #greater keys in every
 // other list (binary search); ids are unique across shards so ranks are too.
 // ---------------------------------------------------------------------------
+// LDS_KEYS: the G*k keys are staged in LDS (G*k <= kMergeMax); otherwise the
+// binary searches read the lists in place (any k).
+template <bool LDS_KEYS = true>
 __global__ __launch_bounds__(256) void merge_topk_kernel(const float* __restrict__ in_s,
                                                          const int32_t* __restrict__ in_i, int G, int B,
                                                          int k, size_t g_stride, float* __restrict__ out_s,
                                                          int32_t* __restrict__ out_i) {
-  __shared__ uint64_t keys[kMergeMax];
+  __shared__ uint64_t keys[LDS_KEYS ? kMergeMax : 1];
   __shared__ int nvalid[64];
   const int b = blockIdx.x;
-  for (int t = threadIdx.x; t < G * k; t += blockDim.x) {
-    const int g = t / k, j = t % k;
-    const size_t src = (size_t)g * g_stride + (size_t)b * k + j;
-    const int32_t id = in_i[src];
-    keys[t] = id >= 0 ? rank_key(in_s[src], (uint32_t)id) : 0ull;
+  auto key_at = [&](int g, int j) -> uint64_t {
+    if constexpr (LDS_KEYS) {
+      return keys[g * k + j];
+    } else {
+      const size_t src = (size_t)g * g_stride + (size_t)b * k + j;
+      const int32_t id = in_i[src];
+      return id >= 0 ? rank_key(in_s[src], (uint32_t)id) : 0ull;
+    }
+  };
+  if constexpr (LDS_KEYS) {
+    for (int t = threadIdx.x; t < G * k; t += blockDim.x) {
+      const int g = t / k, j = t % k;
+      const size_t src = (size_t)g * g_stride + (size_t)b * k + j;
+      const int32_t id = in_i[src];
+      keys[t] = id >= 0 ? rank_key(in_s[src], (uint32_t)id) : 0ull;
+    }
   }
-  if (threadIdx.x < G) {
-    int cnt = 0;
+  if (threadIdx.x < G) {  // valid entries form a prefix of each sorted list
     const size_t base = (size_t)threadIdx.x * g_stride + (size_t)b * k;
-    while (cnt < k && in_i[base + cnt] >= 0) ++cnt;
-    nvalid[threadIdx.x] = cnt;
+    int lo = 0, hi = k;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (in_i[base + mid] >= 0) lo = mid + 1; else hi = mid;
+    }
+    nvalid[threadIdx.x] = lo;
   }
   __syncthreads();
   int total = 0;
   for (int g = 0; g < G; ++g) total += nvalid[g];
-  for (int t = threadIdx.x; t < G * k; t += blockDim.x) {
-    const int g = t / k, j = t % k;
+  for (int64_t t = threadIdx.x; t < (int64_t)G * k; t += blockDim.x) {
+    const int g = (int)(t / k), j = (int)(t % k);
     if (j >= nvalid[g]) continue;
-    const uint64_t key = keys[t];
+    const uint64_t key = key_at(g, j);
     int rank = j;
     for (int g2 = 0; g2 < G; ++g2) {
       if (g2 == g) continue;
-      const uint64_t* L = keys + g2 * k;
       int lo = 0, hi = nvalid[g2];  // count of entries > key (list sorted descending)
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (L[mid] > key) lo = mid + 1; else hi = mid;
+        if (key_at(g2, mid) > key) lo = mid + 1; else hi = mid;
       }
       rank += lo;
     }
@@ -2880,8 +2982,17 @@ size_t topk_ws_bytes(int32_t B, int64_t n) {
   return (size_t)B * kCandCap * sizeof(uint64_t) + (((size_t)B * sizeof(uint32_t) + 255) & ~(size_t)255);
 }
 
+int topk_multi(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base,
+               const int32_t* ids, int64_t ids_ld, float* out_s, int32_t* out_i, int32_t* out_p, hipStream_t st,
+               const int32_t* only_neg = nullptr) {
+  hipLaunchKernelGGL(topk_multi_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base, ids,
+                     ids_ld, out_s, out_i, out_p, only_neg);
+  return launch_check("topk_multi_kernel");
+}
+
 int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, void* ws,
               size_t ws_bytes, float* out_s, int32_t* out_i, hipStream_t st, int dev) {
+  if (k > kTopkMax) return topk_multi(scores, B, n, ld, k, id_base, nullptr, 0, out_s, out_i, nullptr, st);
   const size_t need = topk_ws_bytes(B, n);
   if (need == 0 || ws == nullptr || ws_bytes < need || B > 65535) {  // grid.y of the filter launch
     hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
@@ -3139,7 +3250,7 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
                 void* stream) {
   int rc = check_query(ix, scorer, Q, q_dtype, B, lq);
   if (rc) return rc;
-  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
   CBV2_REQUIRE(out_scores && out_ids, "null outputs");
   const size_t need = cbv2_search_workspace_size(ix, B, k, scorer);
   CBV2_REQUIRE(workspace != nullptr && workspace_bytes >= need && aligned16(workspace),
@@ -3197,22 +3308,40 @@ int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int3
   int rc = check_query(ix, CBV2_SCORER_MAXSIM, Q, qdt, B, lq);
   if (rc) return rc;
   CBV2_REQUIRE(cand != nullptr, "null candidates");
-  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
-  CBV2_REQUIRE(k >= 0 && k <= kTopkMax, "k must be in [0, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(C >= 1 && C <= kRerankMaxC, "C must be in [1, %d] (got %d)", kRerankMaxC, C);
+  CBV2_REQUIRE(k >= 0, "k must be >= 0 (got %d)", k);
   CBV2_REQUIRE(out_scores != nullptr, "null out_scores");
   CBV2_REQUIRE(k == 0 || out_ids != nullptr, "null out_ids");
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  const hipStream_t st = (hipStream_t)stream;
+  const bool big = C > kSmallMax;                 // raw scores in dynamic LDS, multi-pass selection
+  const unsigned dyn = big ? (unsigned)C * sizeof(float) : 0u;
   if (ix->dtype == CBV2_DTYPE_MXFP8) {
     const uint8_t* Qb = (const uint8_t*)Q;
-    hipLaunchKernelGGL(rerank_f8_kernel, dim3((unsigned)B), dim3(kRrWaves * 64), 0, (hipStream_t)stream, ix->tokens,
-                       ix->scales, ix->doclens, ix->n, ix->id_base, Qb, Qb + (size_t)B * lq * kDim, lq, cand, C, k,
-                       out_scores, out_ids, out_pos);
+    const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+    if (big) {
+      CBV2_HIP(hipFuncSetAttribute((const void*)rerank_f8_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)dyn));
+      hipLaunchKernelGGL(rerank_f8_kernel<true>, dim3((unsigned)B), dim3(kRrWaves * 64), dyn, st, ix->tokens,
+                         ix->scales, ix->doclens, ix->n, ix->id_base, Qb, Qs, lq, cand, C, k, out_scores, out_ids,
+                         out_pos);
+    } else {
+      hipLaunchKernelGGL(rerank_f8_kernel<false>, dim3((unsigned)B), dim3(kRrWaves * 64), 0, st, ix->tokens,
+                         ix->scales, ix->doclens, ix->n, ix->id_base, Qb, Qs, lq, cand, C, k, out_scores, out_ids,
+                         out_pos);
+    }
     return launch_check("rerank_f8_kernel");
   }
-  hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)B), dim3(kRrWaves * 64), 0, (hipStream_t)stream, ix->tokens,
-                     ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids,
-                     out_pos);
+  if (big) {
+    CBV2_HIP(hipFuncSetAttribute((const void*)rerank_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)dyn));
+    hipLaunchKernelGGL(rerank_kernel<true>, dim3((unsigned)B), dim3(kRrWaves * 64), dyn, st, ix->tokens, ix->doclens,
+                       ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids, out_pos);
+  } else {
+    hipLaunchKernelGGL(rerank_kernel<false>, dim3((unsigned)B), dim3(kRrWaves * 64), 0, st, ix->tokens, ix->doclens,
+                       ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids, out_pos);
+  }
   return launch_check("rerank_kernel");
 }
 
@@ -3220,8 +3349,10 @@ int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t
                      int32_t* out_ids, int32_t* out_pos, void* stream) {
   CBV2_REQUIRE(scores && out_scores, "null scores/out_scores");
   CBV2_REQUIRE(B >= 1, "B must be >= 1");
-  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
-  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(C >= 1, "C must be >= 1 (got %d)", C);
+  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
+  if (C > kSmallMax)  // long rows: the multi-pass selection (same tie rule)
+    return topk_multi(scores, B, C, C, k, 0, ids, C, out_scores, out_ids, out_pos, (hipStream_t)stream);
   hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, scores, ids, C, k,
                      out_scores, out_ids, out_pos);
   return launch_check("select_small_kernel");
@@ -3278,8 +3409,10 @@ int cbv2_score_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, void* 
 
 int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
                     size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_status, void* stream) {
-  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
-  CBV2_REQUIRE(cap >= k && cap <= kBandCapMax, "cap must be in [k, %d] (got %d)", kBandCapMax, cap);
+  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
+  // k beyond any band: every row takes the full faithful scan (status -1)
+  const bool full = k > kBandCapMax;
+  CBV2_REQUIRE(full || (cap >= k && cap <= kBandCapMax), "cap must be in [k, %d] (got %d)", kBandCapMax, cap);
   F32Ws w;
   int rc = check_f32(ix, CBV2_F32_SEARCH, Q, B, lq, cap, ws, wsb, &w);
   if (rc) return rc;
@@ -3292,6 +3425,11 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
     return topk_impl_empty(B, k, out_scores, out_ids, st);
   }
   if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
+  if (full) {
+    CBV2_HIP(hipMemsetAsync(out_status, 0xff, (size_t)B * sizeof(int32_t), st));
+    if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st))) return rc;
+    return topk_multi(w.T, B, ix->n, ix->n, k, ix->id_base, nullptr, 0, out_scores, out_ids, nullptr, st);
+  }
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
   if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr))) return rc;
   if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
@@ -3312,6 +3450,8 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   // 5. rows whose band overflowed cap (status -1): the full faithful scan over
   //    every doc and an exact top-k, on the device (other rows exit at once)
   if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st, out_status))) return rc;
+  if (k > kTopkMax)
+    return topk_multi(w.T, B, ix->n, ix->n, k, ix->id_base, nullptr, 0, out_scores, out_ids, nullptr, st, out_status);
   hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.T, ix->n, ix->n, k, ix->id_base,
                      out_scores, out_ids, out_status);
   return launch_check("topk_rows_kernel");
@@ -3321,8 +3461,8 @@ int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const
                     int32_t k, void* ws, size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
                     void* stream) {
   CBV2_REQUIRE(cand != nullptr, "null candidates");
-  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "C must be in [1, %d] (got %d)", kSmallMax, C);
-  CBV2_REQUIRE(k >= 0 && k <= kTopkMax, "k must be in [0, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(C >= 1, "C must be >= 1 (got %d)", C);
+  CBV2_REQUIRE(k >= 0, "k must be >= 0 (got %d)", k);
   CBV2_REQUIRE(out_scores != nullptr, "null out_scores");
   CBV2_REQUIRE(k == 0 || out_ids != nullptr, "null out_ids");
   F32Ws w;
@@ -3335,6 +3475,7 @@ int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const
   float* raw = k == 0 ? out_scores : w.F;
   if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
   if (k == 0) return CBV2_OK;
+  if (C > kSmallMax) return topk_multi(raw, B, C, C, k, 0, cand, C, out_scores, out_ids, out_pos, st);
   hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
                      out_pos);
   return launch_check("select_small_kernel");
@@ -3348,7 +3489,7 @@ int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_
   CBV2_REQUIRE(B >= 1, "B must be >= 1");
   CBV2_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "n out of range");
   CBV2_REQUIRE(ld >= n, "ld < n");
-  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d] (got %d)", kTopkMax, k);
+  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
   CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "ids must fit int32");
   int dev = 0;
   CBV2_HIP(hipGetDevice(&dev));
@@ -3356,25 +3497,27 @@ int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_
                    (hipStream_t)stream, dev);
 }
 
+int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
+                            size_t g_stride, float* out_scores, int32_t* out_ids, void* stream);
+
 int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
                     float* out_scores, int32_t* out_ids, void* stream) {
-  CBV2_REQUIRE(in_scores && in_ids && out_scores && out_ids, "null pointer");
-  CBV2_REQUIRE(G >= 1 && G <= 64, "G must be in [1, 64]");
-  CBV2_REQUIRE(B >= 1, "B must be >= 1");
-  CBV2_REQUIRE(k >= 1 && k <= kTopkMax, "k must be in [1, %d]", kTopkMax);
-  CBV2_REQUIRE((int64_t)G * k <= kMergeMax, "G*k must be <= %d", kMergeMax);
-  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores, in_ids, G,
-                     B, k, (size_t)B * k, out_scores, out_ids);
-  return launch_check("merge_topk_kernel");
+  return cbv2_merge_topk_strided(in_scores, in_ids, G, B, k, (size_t)B * k, out_scores, out_ids, stream);
 }
 
 // Internal (sharded.cpp): the same merge with shard g's lists at g * g_stride.
 int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
                             size_t g_stride, float* out_scores, int32_t* out_ids, void* stream) {
-  CBV2_REQUIRE(G >= 1 && G <= 64 && B >= 1 && k >= 1 && k <= kTopkMax && (int64_t)G * k <= kMergeMax,
-               "bad merge sizes");
-  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores, in_ids, G,
-                     B, k, g_stride, out_scores, out_ids);
+  CBV2_REQUIRE(in_scores && in_ids && out_scores && out_ids, "null pointer");
+  CBV2_REQUIRE(G >= 1 && G <= 64, "G must be in [1, 64]");
+  CBV2_REQUIRE(B >= 1, "B must be >= 1");
+  CBV2_REQUIRE(k >= 1, "k must be >= 1");
+  if ((int64_t)G * k <= kMergeMax)
+    hipLaunchKernelGGL(merge_topk_kernel<true>, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores,
+                       in_ids, G, B, k, g_stride, out_scores, out_ids);
+  else
+    hipLaunchKernelGGL(merge_topk_kernel<false>, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, in_scores,
+                       in_ids, G, B, k, g_stride, out_scores, out_ids);
   return launch_check("merge_topk_kernel");
 }
 

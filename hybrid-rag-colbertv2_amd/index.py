@@ -546,7 +546,7 @@ def index_file_info(path: str):
 
 
 def select_topk(scores: torch.Tensor, k: int, ids: Optional[torch.Tensor] = None):
-    """Top-k of each row of a short [B, C] matrix (C <= 1024); ties -> lower position."""
+    """Top-k of each row of a [B, C] score matrix (any C, any k); ties -> lower position."""
     _require_cuda(scores, "scores")
     scores = scores.to(torch.float32).contiguous()
     if scores.dim() == 1:

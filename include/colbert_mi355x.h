@@ -147,6 +147,8 @@ int cbv2_score(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype
  * top-k into the scan (no [B][n] score matrix: each workgroup keeps
  * its best k per query in LDS, then one selection per query); results are
  * those of the unfused path bit for bit (CBV2_OPT_FUSED_TOPK turns it off).
+ * Any k >= 1 (torch.topk takes any k): k > 1024 selects in passes of 4096
+ * keys, each bounded below the previous pass's last key (same tie rule).
  * Extends §8(b)'s prototype with scorer / q_dtype / workspace.  */
 size_t cbv2_search_workspace_size(const cbv2_index* index, int32_t B, int32_t k, int32_t scorer);
 size_t cbv2_search_workspace_bytes(const cbv2_index* index, int32_t B);
@@ -159,7 +161,10 @@ int cbv2_search(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtyp
  * the HBM index by global id (cand int32 [B][C]; ids outside this shard or < 0
  * score -inf) and MaxSim-scored against Q (bf16 [B][lq][128]).
  *  k > 0:  out_scores [B][k], out_ids [B][k] (global ids), out_pos [B][k]
- *          (candidate position = the reference's `result_index`), best first.
+ *          (candidate position = the reference's `result_index`), best first;
+ *          slots past C hold -inf / -1 / -1.
+ *  1 <= C <= 32768 (the reference's argsort takes any C, :789): C > 1024
+ *  keeps the raw scores in dynamic LDS and selects in multiple passes.
  *  k == 0: out_scores [B][C] receives the raw candidate scores (for the
  *          sharded path: all-reduce(max) across shards, then cbv2_select_topk). */
 int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const int32_t* cand,
@@ -192,6 +197,7 @@ int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const i
  *    out_status int32 [B]: the band size, or -1 when the band exceeded `cap`
  *    (k <= cap <= 16384): that row was then recomputed on the device by the
  *    full faithful scan (cbv2_score_f32's arithmetic) and an exact top-k.
+ *    k > 16384 (no band can hold it): every row takes the full scan (-1).
  *    Either way the result is the faithful top-k of the whole corpus; the
  *    call stays asynchronous (no host round trip).
  *  - cbv2_rerank_f32: cbv2_rerank with faithful scores.                      */
@@ -212,10 +218,11 @@ int cbv2_rerank_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, co
                     int32_t* out_ids, int32_t* out_pos, void* stream);
 
 /* Selection -----------------------------------------------------------------
- * cbv2_select_topk — top-k of each row of a small score matrix (rows of
- * C <= 1024 entries: rerank after the cross-shard all-reduce).  ids (nullable)
- * [B][C] maps positions to doc ids (NULL: id = position).  Ties: lower
- * position first.  out_pos (nullable) receives positions.                   */
+ * cbv2_select_topk — top-k of each row of a score matrix [B][C] (rerank after
+ * the cross-shard all-reduce): rank counting in LDS for C <= 1024, the
+ * multi-pass selection beyond (any C, any k).  ids (nullable) [B][C] maps
+ * positions to doc ids (NULL: id = position).  Ties: lower position first.
+ * out_pos (nullable) receives positions.                                    */
 int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t C, int32_t k,
                      float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
 
@@ -223,8 +230,9 @@ int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t
  * i < n; ids written = id_base + i.  With a workspace of
  * cbv2_topk_workspace_bytes(B, n) bytes (0 for short rows) long rows use the
  * sampled-threshold filter + candidate sort; with workspace NULL, or on a
- * candidate overflow, the exact single-pass-per-digit radix select.  The
- * result is identical either way.                                          */
+ * candidate overflow, the exact single-pass-per-digit radix select; k > 1024
+ * selects in bounded passes (no workspace needed).  The result is identical
+ * either way.                                                               */
 size_t cbv2_topk_workspace_bytes(int32_t B, int64_t n);
 int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k,
                    int64_t id_base, void* workspace, size_t workspace_bytes,
@@ -232,7 +240,8 @@ int cbv2_topk_rows(const float* scores, int32_t B, int64_t n, int64_t ld, int32_
 
 /* cbv2_merge_topk — merge G per-shard sorted top-k lists ([G][B][k] scores and
  * global ids, e.g. after an RCCL all-gather) into the global top-k [B][k].
- * Entries with id < 0 are padding.                                          */
+ * Entries with id < 0 are padding (a suffix of each list).  Any k: lists of
+ * G*k <= 8192 keys are staged in LDS, longer ones searched in place.        */
 int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B,
                     int32_t k, float* out_scores, int32_t* out_ids, void* stream);
 

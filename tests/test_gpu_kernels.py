@@ -246,7 +246,7 @@ def test_errors_raise_without_launch(dev):
     with pytest.raises(ValueError):
         ix.search(Q.to(dev), k=0)
     with pytest.raises(ValueError):
-        ix.search(Q.to(dev), k=2000)
+        ix.rerank(Q.to(dev), torch.zeros((2, 40000), dtype=torch.int32, device=dev), k=5)   # C > 32768
     with pytest.raises(ValueError):
         ix.score(torch.zeros(1, 33, 128, device=dev))
     with pytest.raises(ValueError):
