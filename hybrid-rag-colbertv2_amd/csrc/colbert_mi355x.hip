@@ -480,7 +480,10 @@ struct NoTileHook {
 
 // hook(t) runs right after tile t's first MFMA chain has issued (SPREAD: the
 // next iteration's DMA pieces; NoTileHook = nothing).
-template <int QW, int D, int NT = 8, typename Hook = NoTileHook>
+// PROBE (lab energy probe, INVALID scores): 1 = odd tiles reuse the even
+// tile's A fragments (half the LDS read bytes, same MFMAs); 2 (kernel) = no
+// doc streaming after the ring's first fill (no L2 -> LDS traffic).
+template <int QW, int D, int NT = 8, typename Hook = NoTileHook, int PROBE = 0>
 __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
                                            float (&m)[QW][2], Hook hook = Hook{}) {
   constexpr int NC = 2 * QW;
@@ -499,11 +502,15 @@ __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const b
   for (int k = 0; k < NK + D; ++k) {
     if (k < NK) {
       const int t = k / NC, cc = k % NC;
-      if (cc == 0 && t + 1 < NT) frag(t + 1, a[(t + 1) & 1]);
+      if (cc == 0 && t + 1 < NT && (PROBE != 1 || ((t + 1) & 1) == 0)) frag(t + 1, a[((t + 1) & 1) * (PROBE != 1)]);
+      if (PROBE == 1 && cc == 0) {   // opaque: the reused fragments must not fold the MFMAs
+#pragma unroll
+        for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(a[0][s]));
+      }
       f32x4 x = f32x4{};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t & 1][s], qf[cc >> 1][cc & 1][s], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[(t & 1) * (PROBE != 1)][s], qf[cc >> 1][cc & 1][s], x, 0, 0, 0);
       acc[k % (D + 1)] = x;
       if (cc == 0) hook(t);
     }
@@ -536,6 +543,16 @@ __device__ __forceinline__ void iter4_ragged(const uint8_t* buf, int lane, int j
     for (int r = 0; r < 4; ++r) init[r] = (tok0 + r < dl_g) ? 0.0f : neg_inf();
     tile16<QW>(a, qf, init, m);
   }
+}
+
+// Wait until flags[0 .. n) >= target (LDS counters of the ARRIVE ring; n <= 64).
+__device__ __forceinline__ void lds_wait_all_ge(int* flags, int n, int target, int lane) {
+  for (;;) {
+    const int v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : target;
+    if (__ballot(v < target) == 0) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -681,8 +698,15 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
 // pieces (twice as many each), so after each barrier the partner wave on the
 // SIMD (waves WAVES/2 ..) starts its MFMAs at once instead of both waves
 // spending the issue phase with the MFMA pipe idle.
+// ARRIVE (with SPLITLOAD): no workgroup barrier per iteration.  Each loading
+// wave publishes "iteration g landed" in LDS after its own vmcnt wait, every
+// wave publishes "done with iteration g" after its last read of the slot, and
+// a loader refills the slot of iteration g-1 once every wave is done with it.
+// A wave waits only for what it reads or overwrites, so the partner waves
+// cross iteration boundaries without draining the MFMA pipe at a barrier, and
+// an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
-          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false>
+          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -697,21 +721,32 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   constexpr int kPiecesPerWave = kPieces / kLoadWaves;   // per loading wave
   static_assert(TPI == 32 || TPI == 64, "32 or 64 tokens per iteration");
   static_assert(kPieces % kLoadWaves == 0, "pieces must split evenly over the loading waves");
-  static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
+  static_assert(NBUF == 2 || NBUF == 3 || (ARRIVE && NBUF == 4), "2- or 3-deep ring (4 with ARRIVE)");
   static_assert(!(SPREAD && SPLITLOAD), "SPREAD spreads every wave's pieces; SPLITLOAD moves them");
+  static_assert(!ARRIVE || (SPLITLOAD && !SPREAD && kLoadWaves + WAVES <= 16), "ARRIVE needs SPLITLOAD");
   // one LDS object only: with a second __shared__ array hipcc starts putting
   // vmcnt(0) before the ring's ds_reads (LDS-DMA alias tracking)
   // fused top-k: one key buffer + state per (wave, query), after the task slots
+  // (and, with ARRIVE, the landed / done counters)
   constexpr int kCandBytes = FK > 0 ? QPB * (FK * 8 + kFusedStateBytes) : 0;
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterBytes + 16 + kCandBytes];
+  constexpr int kSyncBytes = ARRIVE ? 64 : 0;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterBytes + 16 + kSyncBytes + kCandBytes];
   int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterBytes);
+  int* const sync_landed = reinterpret_cast<int*>(smem + NBUF * kIterBytes + 16);  // [loading waves]
+  int* const sync_done = sync_landed + kLoadWaves;                                // [WAVES]
+  uint8_t* const after_sync = smem + NBUF * kIterBytes + 16 + kSyncBytes;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
-  uint64_t* const cand = reinterpret_cast<uint64_t*>(smem + NBUF * kIterBytes + 16) + (size_t)wave * QW * (FK > 0 ? FK : 1);
-  uint8_t* const tk_state = smem + NBUF * kIterBytes + 16 + (FK > 0 ? QPB * FK * 8 : 0) + wave * QW * kFusedStateBytes;
+  uint64_t* const cand = reinterpret_cast<uint64_t*>(after_sync) + (size_t)wave * QW * (FK > 0 ? FK : 1);
+  uint8_t* const tk_state = after_sync + (FK > 0 ? QPB * FK * 8 : 0) + wave * QW * kFusedStateBytes;
   if (FK > 0 && lane < 2 * QW) reinterpret_cast<uint64_t*>(tk_state)[lane] = 0ull;  // thr = 0, cnt = 0
+  if constexpr (ARRIVE) {
+    if (threadIdx.x < kLoadWaves + WAVES) sync_landed[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  uint32_t gbase = 0;   // ARRIVE: iterations of the earlier doc ranges (ring slot of iteration it = (gbase+it) % NBUF)
   const int nq_groups = (B + QPB - 1) / QPB;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
@@ -781,7 +816,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
                                          0, 0);
       };
       auto issue = [&](int it, int buf) {
-        if (!loader) return;
+        if (!loader || (PROBE == 2 && it >= NBUF)) return;   // PROBE 2 (INVALID): no streaming after the first fill
 #pragma unroll
         for (int jj = 0; jj < kPiecesPerWave; ++jj) issue_piece(it, buf, jj);
       };
@@ -793,8 +828,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       int dl_g = 0, dl_min = 0, dl_max = 0;
 
       const int nit = IPG * ngr;
-      issue(0, 0);
-      if (NBUF == 3 && nit > 1) issue(1, 1);
+      if constexpr (ARRIVE) {   // the first NBUF-1 iterations (every earlier iteration is done: range barrier)
+        for (int j0 = 0; j0 < NBUF - 1 && j0 < nit; ++j0) issue(j0, (int)((gbase + (uint32_t)j0) % NBUF));
+      } else {
+        issue(0, 0);
+        if (NBUF == 3 && nit > 1) issue(1, 1);
+      }
       int cur = 0;           // ring slot of iteration it
       bool stored = false;   // global stores issued last iteration (they count in vmcnt)
       for (int it = 0; it < nit; ++it) {
@@ -803,23 +842,48 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           ph_a = __builtin_amdgcn_s_memtime();
           if (ph_t) ph_comp += ph_a - ph_t;
         }
-        if (NBUF == 3 && it + 1 < nit && !stored)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+        const uint32_t gi = gbase + (uint32_t)it;   // ARRIVE: global iteration number
+        int nslot = 0;
+        const uint8_t* buf;
+        if constexpr (ARRIVE) {
+          if (loader) {   // this iteration's pieces of this wave landed -> publish
+            const int ahead = min(NBUF - 2, nit - 1 - it);   // younger iterations already issued
+            if (stored || ahead <= 0)
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (ahead == 1)
+              asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPiecesPerWave) : "memory");
+            if (lane == 0)
+              __hip_atomic_store(sync_landed + lwave, (int)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          lds_wait_all_ge(sync_landed, kLoadWaves, (int)(gi + 1), lane);   // every loader's pieces
+          if (loader && it + NBUF - 1 < nit) {   // refill iteration gi-1's slot once every wave is done with it
+            lds_wait_all_ge(sync_done, WAVES, (int)gi, lane);
+            issue(it + NBUF - 1, (int)((gi + NBUF - 1) % NBUF));
+          }
+          buf = smem + (gi % NBUF) * kIterBytes;
+        } else {
+          if (NBUF == 3 && it + 1 < nit && !stored)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
         uint64_t ph_b = 0;
         if constexpr (STAMPS) {
           ph_b = __builtin_amdgcn_s_memtime();
           ph_wait += ph_b - ph_a;
         }
         stored = false;
-        const int nslot = cur ^ 1;  // 2-deep ring: iteration it+1's slot
-        if (NBUF == 2 && !SPREAD && it + 1 < nit) issue(it + 1, nslot);
-        if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
-        const uint8_t* buf = smem + cur * kIterBytes;
-        cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+        if constexpr (!ARRIVE) {
+          nslot = cur ^ 1;  // 2-deep ring: iteration it+1's slot
+          if (NBUF == 2 && !SPREAD && it + 1 < nit) issue(it + 1, nslot);
+          if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+          buf = smem + cur * kIterBytes;
+          cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+        }
 
         const int G = it / IPG, j = it % IPG;
         if (j == 0) {
@@ -854,7 +918,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
             else
               iter4_full<QW, D, NT>(buf, lane, qf, m);
           } else {
-            iter4_full<QW, D, NT>(buf, lane, qf, m);
+            iter4_full<QW, D, NT, NoTileHook, PROBE>(buf, lane, qf, m);
           }
         } else if (TPI * j < dl_max)
           iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
@@ -886,7 +950,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
             }
           }
         }
+        if constexpr (ARRIVE) {   // this wave's reads of the slot are issued (LDS serves a wave in order)
+          asm volatile("" ::: "memory");
+          if (lane == 0) __hip_atomic_store(sync_done + wave, (int)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
+      if constexpr (ARRIVE) gbase += (uint32_t)nit;
     }
     if (task_ctr == nullptr) break;
     // next dynamic task; the barrier also retires every wave's reads of the
@@ -2724,7 +2793,7 @@ int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
 }
 
 template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
-          int FK = 0, bool SPLITLOAD = false>
+          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
                     int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
@@ -2738,7 +2807,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD>),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
                      ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0);

@@ -353,6 +353,40 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
     return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, true>(
         ix, q, B, lq, nullptr, 0, st, dyn_frac, task_docs, nullptr, nullptr, &ft);
   }
+  // kinds 17-22 (round 2): ARRIVE -- LDS landed/done counters instead of the
+  // per-iteration barrier.  17: 32-token iterations, 4-deep ring; 18: 64-token,
+  // 2-deep; 19: 32-token, 3-deep; 20: kind 17 phase-stamped; 21 / 22: the fused
+  // top-k builds of 17 / 18 (k = 100, keys into `out`).
+  if (kind == 17)
+    return launch_scan16x4<8, 4, 1, 2, 4, false, 32, 2, false, 0, true, true>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                             task_docs);
+  if (kind == 18)
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, true>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                             task_docs);
+  if (kind == 19)
+    return launch_scan16x4<8, 4, 1, 2, 3, false, 32, 2, false, 0, true, true>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                             task_docs);
+  if (kind == 20 && stamps != nullptr)
+    return launch_scan16x4<8, 4, 1, 2, 4, true, 32, 2, false, 0, true, true>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                            task_docs, (uint64_t*)stamps);
+  if (kind == 21 || kind == 22) {
+    FusedTopk ft{(uint64_t*)out, 100, scan_chunks(ix, (B + 31) / 32, cu_count(ix->device)), 0};
+    if ((int64_t)B * ft.max_slots * 100 * 8 > ld * (int64_t)B * 4) return -1;
+    if (kind == 21)
+      return launch_scan16x4<8, 4, 1, 2, 4, false, 32, 2, false, kFusedCap, true, true>(
+          ix, q, B, lq, nullptr, 0, st, dyn_frac, task_docs, nullptr, nullptr, &ft);
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, true, true>(
+        ix, q, B, lq, nullptr, 0, st, dyn_frac, task_docs, nullptr, nullptr, &ft);
+  }
+  // kind 23: energy probe (INVALID scores) -- kind 13 with half the LDS read
+  // bytes (odd tiles reuse the even tile's fragments), same MFMA stream
+  if (kind == 23)
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 1>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                                 task_docs);
+  // kind 24: energy probe (INVALID) -- kind 13 without doc streaming after the first fill
+  if (kind == 24)
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 2>(ix, q, B, lq, out, ld, st, dyn_frac,
+                                                                                 task_docs);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
