@@ -2325,6 +2325,190 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Doc-major band rescoring.  The bands of a batch overlap (at B=256, 1M docs,
+// ~6.1k band docs per query: 1.56M (query, doc) pairs over ~0.8M distinct
+// docs), so rescoring pair by pair gathers most band docs' hi+lo (64 KiB)
+// twice.  Instead the pairs are grouped by doc (counting sort: per-doc counts,
+// wave-aggregated segment offsets, scatter) and one wave rescored every pair
+// of a doc with the doc's tiles loaded once per half, the queries' fragments
+// (16 KiB each, L2-resident) streamed per pair.  Same arithmetic and max
+// order per pair as rescore_x3_kernel: identical bits.  Rows whose band
+// overflowed cap are skipped (the search recomputes them in full).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void band_count_kernel(const int32_t* __restrict__ cand,
+                                                         const int32_t* __restrict__ count, int cap,
+                                                         int64_t id_base, int64_t n, int32_t* __restrict__ dcnt) {
+  const int b = blockIdx.y;
+  const int tot = count[b];
+  if (tot > cap) return;   // overflow row: full scan later
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < tot; c += gridDim.x * blockDim.x) {
+    const int64_t d = (int64_t)cand[(size_t)b * cap + c] - id_base;
+    if (d >= 0 && d < n) atomicAdd(dcnt + d, 1);
+  }
+}
+
+// Per doc with pairs: a segment [doff, doff + cnt) of the pair list and an
+// entry in the active list; one atomic per wave for each.  ctr[0] = pairs,
+// ctr[1] = active docs.
+__global__ __launch_bounds__(256) void band_offsets_kernel(const int32_t* __restrict__ dcnt, int64_t n,
+                                                           int32_t* __restrict__ doff, int32_t* __restrict__ act,
+                                                           int32_t* __restrict__ act_off,
+                                                           int32_t* __restrict__ act_cnt, int32_t* __restrict__ ctr) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t d0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63LL; d0 < n;
+       d0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = d0 + lane;
+    const int c = d < n ? dcnt[d] : 0;
+    int incl = c;   // inclusive prefix sum over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(incl, off);
+      if (lane >= off) incl += t;
+    }
+    const int total = __shfl(incl, 63);
+    const uint64_t am = __ballot(c > 0);
+    if (am == 0) continue;   // wave-uniform
+    int pbase = 0, abase = 0;
+    if (lane == 0) {
+      pbase = atomicAdd(ctr, total);
+      abase = atomicAdd(ctr + 1, __popcll(am));
+    }
+    pbase = __shfl(pbase, 0);
+    abase = __shfl(abase, 0);
+    if (c > 0) {
+      const int o = pbase + incl - c;
+      const int a = abase + __popcll(am & ((1ull << lane) - 1ull));
+      doff[d] = o;
+      act[a] = (int32_t)d;
+      act_off[a] = o;
+      act_cnt[a] = c;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void band_scatter_kernel(const int32_t* __restrict__ cand,
+                                                           const int32_t* __restrict__ count, int cap,
+                                                           int64_t id_base, int64_t n, int32_t* __restrict__ dcnt,
+                                                           const int32_t* __restrict__ doff,
+                                                           int32_t* __restrict__ pair_b, int32_t* __restrict__ pair_c) {
+  const int b = blockIdx.y;
+  const int tot = count[b];
+  if (tot > cap) return;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < tot; c += gridDim.x * blockDim.x) {
+    const int64_t d = (int64_t)cand[(size_t)b * cap + c] - id_base;
+    if (d < 0 || d >= n) continue;
+    const int pos = doff[d] + atomicSub(dcnt + d, 1) - 1;   // leaves dcnt at 0
+    pair_b[pos] = b;
+    pair_c[pos] = c;
+  }
+}
+
+constexpr int kDocPairs = 4;   // pairs of one doc held per pass (their running maxima in VGPRs)
+// PAIR_OUTER: a wave takes the doc's pairs one at a time, each with its query
+// fragments loaded once and the doc's tiles re-read per pair (cache-served
+// after the first); otherwise the doc's tiles are loaded once per half and
+// the query fragments re-read per pair and half.
+template <bool PAIR_OUTER = false>
+__global__ __launch_bounds__(256) void rescore_docs_kernel(
+    const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens,
+    const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int B, int lq,
+    const int32_t* __restrict__ act, const int32_t* __restrict__ act_off, const int32_t* __restrict__ act_cnt,
+    const int32_t* __restrict__ ctr, const int32_t* __restrict__ pair_b, const int32_t* __restrict__ pair_c,
+    float* __restrict__ F, int cap) {
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n_act = ctr[1];
+  for (int a = blockIdx.x * 4 + wave; a < n_act; a += gridDim.x * 4) {   // one doc per wave
+    const int64_t d = act[a];
+    const int o = act_off[a], cnt = act_cnt[a];
+    int dl = doclens[d];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    const uint8_t* dh = hi + (size_t)d * kDocBytes;
+    const uint8_t* dlo = lo + (size_t)d * kDocBytes;
+    if constexpr (PAIR_OUTER) {
+#pragma unroll 1
+      for (int p = 0; p < cnt; ++p) {
+        const int b = pair_b[o + p];
+        bf16x8 qh[2][4], ql[2][4];
+        load_qfrag16(qhi, b, B, lq, lane, qh);
+        load_qfrag16(qlo, b, B, lq, lane, ql);
+        float m[2] = {neg_inf(), neg_inf()};
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          bf16x8 ah[4][4], al[4][4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int rt = 4 * half + t;
+            if (16 * rt < dl) {
+              gbl_afrag16(dh, rt, lane, ah[t]);
+              gbl_afrag16(dlo, rt, lane, al[t]);
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int rt = 4 * half + t;
+            if (16 * rt < dl) {
+              const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+              tile16_x3(ah[t], al[t], qh, ql, init, m);
+            }
+          }
+        }
+        const float v = reduce16(m[0], m[1], lane, lq);
+        if (lane == 0) F[(size_t)b * cap + pair_c[o + p]] = v;
+      }
+      continue;
+    }
+    for (int p0 = 0; p0 < cnt; p0 += kDocPairs) {
+      const int np = cnt - p0 < kDocPairs ? cnt - p0 : kDocPairs;
+      float m[kDocPairs][2];
+#pragma unroll
+      for (int q = 0; q < kDocPairs; ++q) m[q][0] = m[q][1] = neg_inf();
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        bf16x8 ah[4][4], al[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int rt = 4 * half + t;
+          if (16 * rt < dl) {
+            gbl_afrag16(dh, rt, lane, ah[t]);
+            gbl_afrag16(dlo, rt, lane, al[t]);
+          }
+        }
+#pragma unroll 1
+        for (int p = 0; p < np; ++p) {
+          const int b = pair_b[o + p0 + p];
+          bf16x8 qh[2][4], ql[2][4];
+          load_qfrag16(qhi, b, B, lq, lane, qh);
+          load_qfrag16(qlo, b, B, lq, lane, ql);
+          float mm[2] = {neg_inf(), neg_inf()};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int rt = 4 * half + t;
+            if (16 * rt < dl) {
+              const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+              tile16_x3(ah[t], al[t], qh, ql, init, mm);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < kDocPairs; ++q)
+            if (q == p) {
+              m[q][0] = fmaxf(m[q][0], mm[0]);
+              m[q][1] = fmaxf(m[q][1], mm[1]);
+            }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kDocPairs; ++q) {
+        if (q < np) {
+          const float v = reduce16(m[q][0], m[q][1], lane, lq);
+          if (lane == 0) F[(size_t)pair_b[o + p0 + q] * cap + pair_c[o + p0 + q]] = v;
+        }
+      }
+    }
+  }
+}
+
 // Band collect: row b of the bf16 scan's scores T; every doc with T >= T_k -
 // 2 beta(b) is appended (global id) to cand[b][0..cap); count[b] = the band
 // size (may exceed cap: the search then recomputes that row in full).  Hits
@@ -2566,6 +2750,7 @@ struct cbv2_index {
   bool fused_topk = true;    // CBV2_OPT_FUSED_TOPK != 0
   int fused_topk_mode = 1;   // its value (2: also the MXFP8 scan, A/B only)
   bool dynamic_tail = true;  // CBV2_OPT_DYNAMIC_TAIL
+  int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -3098,6 +3283,15 @@ struct F32Ws {
   void* tk = nullptr;
   size_t tk_bytes = 0;
   float* T = nullptr;
+  // doc-major band rescoring (SEARCH)
+  int32_t* dcnt = nullptr;
+  int32_t* doff = nullptr;
+  int32_t* act = nullptr;
+  int32_t* act_off = nullptr;
+  int32_t* act_cnt = nullptr;
+  int32_t* dctr = nullptr;
+  int32_t* pair_b = nullptr;
+  int32_t* pair_c = nullptr;
 };
 
 // op SCORE: split queries; RERANK: + F [B][C]; SEARCH: + band [B][cap] + scan.
@@ -3121,6 +3315,15 @@ size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8
     w->tk_bytes = topk_ws_bytes(B, ix->n);
     w->tk = take(w->tk_bytes);
     w->T = (float*)take((size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float));
+    const size_t nd = (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(int32_t);
+    w->dcnt = (int32_t*)take(nd);
+    w->doff = (int32_t*)take(nd);
+    w->act = (int32_t*)take(nd);
+    w->act_off = (int32_t*)take(nd);
+    w->act_cnt = (int32_t*)take(nd);
+    w->dctr = (int32_t*)take(2 * sizeof(int32_t));
+    w->pair_b = (int32_t*)take((size_t)B * cap * sizeof(int32_t));
+    w->pair_c = (int32_t*)take((size_t)B * cap * sizeof(int32_t));
   }
   return off;
 }
@@ -3355,6 +3558,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
     case CBV2_OPT_DYNAMIC_TAIL:
       ix->dynamic_tail = value != 0;
       return CBV2_OK;
+    case CBV2_OPT_BAND_DOC_MAJOR:
+      ix->band_doc_major = (int)value;
+      return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);
   }
@@ -3512,7 +3718,31 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
                      out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count);
   if ((rc = launch_check("band_collect_kernel"))) return rc;
-  if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) return rc;
+  if (ix->band_doc_major) {   // pairs grouped by doc: each band doc's tiles read once per batch
+    CBV2_HIP(hipMemsetAsync(w.dcnt, 0, (size_t)ix->n * sizeof(int32_t), st));
+    CBV2_HIP(hipMemsetAsync(w.dctr, 0, 2 * sizeof(int32_t), st));
+    const unsigned gc = (unsigned)std::min<int64_t>((cap + 255) / 256, 16);
+    hipLaunchKernelGGL(band_count_kernel, dim3(gc, (unsigned)B), dim3(256), 0, st, w.cand, w.count, cap, ix->id_base,
+                       ix->n, w.dcnt);
+    if ((rc = launch_check("band_count_kernel"))) return rc;
+    const unsigned go = (unsigned)std::min<int64_t>((ix->n + 255) / 256, 4096);
+    hipLaunchKernelGGL(band_offsets_kernel, dim3(go), dim3(256), 0, st, w.dcnt, ix->n, w.doff, w.act, w.act_off,
+                       w.act_cnt, w.dctr);
+    if ((rc = launch_check("band_offsets_kernel"))) return rc;
+    hipLaunchKernelGGL(band_scatter_kernel, dim3(gc, (unsigned)B), dim3(256), 0, st, w.cand, w.count, cap,
+                       ix->id_base, ix->n, w.dcnt, w.doff, w.pair_b, w.pair_c);
+    if ((rc = launch_check("band_scatter_kernel"))) return rc;
+    const unsigned gr = (unsigned)(2 * cu_count(ix->device) * 4);   // 4 waves each; grid-stride over docs
+    if (ix->band_doc_major == 2)
+      hipLaunchKernelGGL(rescore_docs_kernel<true>, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
+                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
+    else
+      hipLaunchKernelGGL(rescore_docs_kernel<false>, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
+                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
+    if ((rc = launch_check("rescore_docs_kernel"))) return rc;
+  } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) {
+    return rc;
+  }
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
                      ix->id_base, out_scores, out_ids, out_status);
   if ((rc = launch_check("band_select_kernel"))) return rc;

@@ -248,7 +248,7 @@ class ColbertIndex:
 
     # ------------------------------------------------------------ options / measurement
     def set_option(self, option: int, value: int) -> None:
-        """cbv2_index_set_option: _lib.OPT_FUSED_TOPK / OPT_DYNAMIC_TAIL (A/B and tests)."""
+        """cbv2_index_set_option: _lib.OPT_FUSED_TOPK / OPT_DYNAMIC_TAIL / OPT_BAND_DOC_MAJOR (A/B and tests)."""
         _lib.check(_lib.lib().cbv2_index_set_option(self._h, int(option), int(value)))
 
     def fused_topk_slots(self, B: int, k: int, scorer: str = "maxsim") -> int:

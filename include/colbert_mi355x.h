@@ -91,6 +91,9 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        MXFP8 scan, which is slower fused: A/B only).
  *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
  *                        as dynamic tasks (0: static chunks only).
+ *  CBV2_OPT_BAND_DOC_MAJOR 1: cbv2_search_f32 rescores its band grouped by
+ *                        doc (each band doc read once per batch; 0: pair by
+ *                        pair).  Identical results either way.
  * cbv2_index_last_scan_plan: the work split of this handle's latest scan
  * launch: {workgroups, static chunk docs, static docs, dynamic tail 0/1}.
  * Thread safety: one handle may be used from several host threads and
@@ -98,6 +101,7 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  * before sharing the handle).                                               */
 #define CBV2_OPT_FUSED_TOPK 1
 #define CBV2_OPT_DYNAMIC_TAIL 2
+#define CBV2_OPT_BAND_DOC_MAJOR 3
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

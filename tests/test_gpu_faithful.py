@@ -142,3 +142,25 @@ def test_faithful_shards_merge_equal_unsharded(dev):
              for a, b in ((0, 1800), (1800, 5000))]
     ms, mi = merge_topk(torch.stack([p[0] for p in parts]), torch.stack([p[1] for p in parts]), 50)
     assert torch.equal(mi, fi) and torch.equal(ms, fs)
+
+
+@pytest.mark.parametrize("N,dups", [(6000, 1), (3000, 9)])
+def test_band_doc_major_equals_pair_major(dev, N, dups):
+    """Doc-major band rescoring (pairs grouped by doc, each band doc's tiles
+    read once per batch) returns the pair-by-pair rescoring's results bit for
+    bit.  dups > 1 repeats queries, so every band doc has > 4 pairs (several
+    passes of one wave over the doc)."""
+    docs, doclens, Q = make_case(N + dups, N, 6, 32)
+    if dups > 1:
+        Q = torch.cat([Q[:1].expand(dups, -1, -1), Q[1:]]).contiguous()
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=5)
+    s1, i1 = ix.search(Q.to(dev), 100)
+    b1 = ix.last_band.clone()
+    ix.set_option(_lib.OPT_BAND_DOC_MAJOR, 0)
+    s0, i0 = ix.search(Q.to(dev), 100)
+    assert torch.equal(ix.last_band, b1) and (b1 >= 100).all()
+    assert torch.equal(i1, i0) and torch.equal(s1, s0)
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    rs, _ = orc.topk(exact, 100, id_base=5)
+    fin = np.isfinite(rs)
+    np.testing.assert_allclose(s1.cpu().numpy()[fin], rs[fin], atol=ATOL, rtol=0)
