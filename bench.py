@@ -7,8 +7,8 @@ One STEP = one batch of B=256 queries (embeddings + BM25 term ids) through
 the whole path:
   stage 1  host BM25 top-100 (native C++, csrc/host_bm25.cpp) over the
            synthetic 1M-doc term corpus -- run while the GPU scans,
-  stage 2  HIP MaxSim scan with the top-100 fused into it (per-workgroup
-           candidate lists in LDS + one selection per query; sharded over
+  stage 2  HIP MaxSim scan + radix top-100 (the top-k fused into the scan,
+           --fused-topk, is ~1 % slower on MI355X: profiles/r02k; sharded over
            ranks: per-rank top-100 -> RCCL all-gather -> HIP merge; the ranks'
            BM25 lists over their doc shards ride the same all-gather),
   fusion   host RRF (native C++, reference semantics) -> top-50 candidates,
@@ -214,7 +214,7 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="time unpipelined steps")
     ap.add_argument("--native-exchange", action="store_true",
                     help="N>1: the MAIN timing uses the exchange inside the C ABI (the native leg always runs too)")
-    ap.add_argument("--unfused-topk", action="store_true", help="stage 2 without the fused top-k (A/B)")
+    ap.add_argument("--fused-topk", action="store_true", help="stage 2 with the top-k fused into the scan (A/B)")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
                          "(bf16 hi scanned + residual-certified band, DESIGN 3.12)")
@@ -260,9 +260,9 @@ def main():
         ix = ColbertIndex.mxfp8(tokens, doclens, id_base=begin)   # quantized on the GPU (HIP kernel)
     else:
         ix = ColbertIndex(tokens, doclens, id_base=begin)
-    if args.unfused_topk:
+    if args.fused_topk:
         from hybrid_rag_colbertv2_amd import _lib
-        ix.set_option(_lib.OPT_FUSED_TOPK, 0)
+        ix.set_option(_lib.OPT_FUSED_TOPK, 1)
     nccl = world > 1 and backend == "nccl"
     searcher = ShardedSearcher(ix, native=args.native_exchange and nccl, lexical_k=args.k)
     Q = Qf.to(dev, torch.float32 if faithful else torch.bfloat16)

@@ -662,7 +662,7 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
   int o, sz;
   if (task_docs > 0) {
     o = atomicAdd(ctr, 1) * task_docs;
-    sz = o < dyn ? task_docs : 0;
+    sz = o < dyn ? (dyn - o < task_docs ? dyn - o : task_docs) : 0;
   } else {
     o = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
@@ -678,6 +678,32 @@ __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int 
   }
   slot[0] = o;
   slot[1] = sz;
+}
+
+// The tail in nsl XCD-local slices (nsl = 8, or 1 = one shared tail): slice s
+// = [lo(s), lo(s+1)) with its own counter ctr[s] per query group.  A
+// workgroup drains the slice of its XCD (blockIdx % 8: blocks b and b + 8
+// share an XCD) before the others', so the query groups reading the same
+// tail docs on one XCD share its L2 (with one shared tail the tasks of a doc
+// range land on up to 8 XCDs: PMC, r02h, +3.3 GB per 1M-doc launch).
+__device__ __forceinline__ int tail_slice_lo(int s, int nsl, int dyn) {
+  return s >= nsl ? dyn : (int)(((int64_t)dyn * s / nsl) & ~15LL);
+}
+__device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int task_docs, int dyn, int P,
+                                                 int* slot) {
+  for (int r = 0; r < nsl; ++r) {
+    const int sl = (xcd + r) % nsl;
+    const int lo = tail_slice_lo(sl, nsl, dyn);
+    // guided sizes as if every workgroup of the query group shared the slice:
+    // small tasks, so the fast XCDs' steals at the end stay fine-grained
+    next_task(ctr + sl, task_docs, tail_slice_lo(sl + 1, nsl, dyn) - lo, P, slot);
+    if (slot[1] > 0) {
+      slot[0] += lo;
+      return;
+    }
+  }
+  slot[0] = 0;
+  slot[1] = 0;
 }
 
 // Work split (per query group of QPB queries): docs [0, static_docs) in equal
@@ -711,7 +737,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
     int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr, int task_docs,
-    uint64_t* __restrict__ stamps, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0) {
+    uint64_t* __restrict__ stamps, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0,
+    int tail_slices = 1) {
   // TPI tokens of 4 docs per iteration (32: 32 KiB, 64: 64 KiB), IPG per group
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kRowBytes;
@@ -961,7 +988,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     // next dynamic task; the barrier also retires every wave's reads of the
     // ring before the next range refills it (two slots: a slow wave may still
     // read slot k&1 while thread 0 fills slot (k+1)&1).
-    if (threadIdx.x == 0) next_task(task_ctr + qg, task_docs, (int)(n - static_docs), nwg / nq_groups, task_slot + 2 * (k & 1));
+    if (threadIdx.x == 0)
+      next_task_sliced(task_ctr + tail_slices * qg, tail_slices, bid & 7, task_docs, (int)(n - static_docs),
+                       nwg / nq_groups, task_slot + 2 * (k & 1));
     __syncthreads();
     const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1)]);
     const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1) + 1]);
@@ -1379,7 +1408,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
     float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr,
-    int task_docs, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0) {
+    int task_docs, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0, int tail_slices = 1) {
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kDim;                 // e4m3 bytes per iteration
   constexpr int kIterStage = kIterBytes + 4 * TPI * 2;        // + 2 scale bytes per row
@@ -1522,7 +1551,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   }
   }
     if (task_ctr == nullptr) break;
-    if (threadIdx.x == 0) next_task(task_ctr + qg, task_docs, (int)(n - static_docs), nwg / nq_groups, task_slot + 2 * (kt & 1));
+    if (threadIdx.x == 0)
+      next_task_sliced(task_ctr + tail_slices * qg, tail_slices, bid & 7, task_docs, (int)(n - static_docs),
+                       nwg / nq_groups, task_slot + 2 * (kt & 1));
     __syncthreads();
     const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (kt & 1)]);
     const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (kt & 1) + 1]);
@@ -2747,9 +2778,13 @@ struct cbv2_index {
   bool ring_ev_used[128] = {};
   // Work split of the most recent scan launch (cbv2_index_last_scan_plan).
   int64_t last_plan[4] = {0, 0, 0, 0};
-  bool fused_topk = true;    // CBV2_OPT_FUSED_TOPK != 0
-  int fused_topk_mode = 1;   // its value (2: also the MXFP8 scan, A/B only)
-  bool dynamic_tail = true;  // CBV2_OPT_DYNAMIC_TAIL
+  // CBV2_OPT_FUSED_TOPK: off by default.  In-process A/B on MI355X (round 2,
+  // profiles/r02k_fused_ab.jsonl): cbv2_search fused 145.9 vs unfused 145.2 ms
+  // at 1M docs B=256, 38.7 vs 38.2 at B=64, 18.6 vs 18.4 at 125k (the fused
+  // scan runs ~1 % longer than the unfused scan + its radix top-k).
+  bool fused_topk = false;   // CBV2_OPT_FUSED_TOPK != 0
+  int fused_topk_mode = 0;   // its value (2: also the MXFP8 scan, A/B only)
+  int dynamic_tail = 1;      // CBV2_OPT_DYNAMIC_TAIL (1: XCD-sliced tail, 2: one shared tail, 0: off)
   int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
@@ -2801,8 +2836,9 @@ struct DeviceGuard {
 };
 
 constexpr int kRingSlots = 128;   // cbv2_score launches in flight before a slot is reused
-constexpr int kRingInts = 64;     // query groups per launch with a dynamic tail (B <= 64 * 32)
-constexpr size_t kCtrBytes = 256; // counter block at the head of a search workspace (kRingInts ints)
+constexpr int kTailSlices = 8;    // XCD-local slices of the dynamic tail (next_task_sliced)
+constexpr int kRingInts = 64 * kTailSlices;  // counters per launch: 64 query groups x slices (B <= 64 * 32)
+constexpr size_t kCtrBytes = kRingInts * sizeof(int);  // counter block at the head of a search workspace
 
 // The handle's task-counter ring and its per-slot events (index creation;
 // failure leaves cbv2_score on the static split).
@@ -2914,6 +2950,7 @@ struct ScanSplit {
   int64_t n_chunks = 1, chunk_docs = 0, static_docs = 0;
   int* ctr = nullptr;
   int task_docs = 0;
+  int slices = 1;       // counters per query group (XCD-local tail slices)
   int ring_slot = -1;   // >= 0: the handle's ring slot, released by finish_split
 };
 
@@ -2927,7 +2964,9 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
   sp->ring_slot = -1;
   const int64_t tail_chunk = ((int64_t)((double)ix->n * (1.0 - (double)dyn_frac)) / n_chunks) & ~(int64_t)63;
   const bool have_ctr = ctr_ws != nullptr || ix->task_ring != nullptr;
-  if (have_ctr && ix->dynamic_tail && dyn_frac > 0.0f && nq_groups <= kRingInts && tail_chunk >= kMinChunkDocs) {
+  sp->slices = ix->dynamic_tail == 2 ? 1 : kTailSlices;
+  if (have_ctr && ix->dynamic_tail && dyn_frac > 0.0f && nq_groups * sp->slices <= kRingInts &&
+      tail_chunk >= kMinChunkDocs) {
     sp->chunk_docs = tail_chunk;
     sp->static_docs = sp->chunk_docs * n_chunks;
     if (ctr_ws != nullptr) {
@@ -2944,7 +2983,7 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
       sp->ctr = ix->task_ring + (size_t)slot * kRingInts;
       sp->ring_slot = (int)slot;
     }
-    CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sizeof(int), st));
+    CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sp->slices * sizeof(int), st));
   } else {
     sp->chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
     n_chunks = (ix->n + sp->chunk_docs - 1) / sp->chunk_docs;
@@ -2995,7 +3034,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
   hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
-                     ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0);
+                     ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
   if ((rc = launch_check("maxsim_scan16x4_kernel"))) return rc;
   return finish_split(ix, sp, st);
 }
@@ -3083,7 +3122,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
   hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC, FK>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
-                     sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0);
+                     sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
   if ((rc = launch_check("maxsim_scan_f8x4_kernel"))) return rc;
   return finish_split(ix, sp, st);
 }
@@ -3556,7 +3595,7 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
       ix->fused_topk_mode = (int)value;
       return CBV2_OK;
     case CBV2_OPT_DYNAMIC_TAIL:
-      ix->dynamic_tail = value != 0;
+      ix->dynamic_tail = (int)value;
       return CBV2_OK;
     case CBV2_OPT_BAND_DOC_MAJOR:
       ix->band_doc_major = (int)value;

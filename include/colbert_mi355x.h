@@ -88,9 +88,11 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 /* Handle options (A/B and tests; defaults = production):
  *  CBV2_OPT_FUSED_TOPK   1: cbv2_search fuses the top-k into eligible scans
  *                        (the bf16 doc-interleaved scan; 2 also fuses the
- *                        MXFP8 scan, which is slower fused: A/B only).
+ *                        MXFP8 scan).  Default 0: on MI355X the fused scan
+ *                        runs ~1 % longer than the scan + radix top-k.
  *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
- *                        as dynamic tasks (0: static chunks only).
+ *                        as dynamic tasks, in 8 XCD-local slices (2: one
+ *                        shared tail; 0: static chunks only).
  *  CBV2_OPT_BAND_DOC_MAJOR 1: cbv2_search_f32 rescores its band grouped by
  *                        doc (each band doc read once per batch; 0: pair by
  *                        pair).  Identical results either way.
@@ -147,10 +149,10 @@ int cbv2_score(cbv2_index* index, int32_t scorer, const void* Q, int32_t q_dtype
  * counters, so concurrent calls on distinct streams need distinct workspaces)
  * must hold cbv2_search_workspace_size(index, B, k, scorer) bytes;
  * cbv2_search_workspace_bytes(index, B) is enough for any k and scorer.
- * MaxSim with k <= 104 on the bf16 doc-interleaved scan (B > 16) fuses the
- * top-k into the scan (no [B][n] score matrix: each workgroup keeps
- * its best k per query in LDS, then one selection per query); results are
- * those of the unfused path bit for bit (CBV2_OPT_FUSED_TOPK turns it off).
+ * With CBV2_OPT_FUSED_TOPK on, MaxSim with k <= 104 on the bf16
+ * doc-interleaved scan (B > 16) fuses the top-k into the scan (no [B][n]
+ * score matrix: each workgroup keeps its best k per query in LDS, then one
+ * selection per query); results are those of the unfused path bit for bit.
  * Any k >= 1 (torch.topk takes any k): k > 1024 selects in passes of 4096
  * keys, each bounded below the previous pass's last key (same tie rule).
  * Extends §8(b)'s prototype with scorer / q_dtype / workspace.  */

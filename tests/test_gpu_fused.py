@@ -104,6 +104,8 @@ def test_fused_workspace_is_small_and_large_k_unfused(dev):
     docs, doclens = _corpus(dev, 100000, 1, ragged=False)
     ix = ColbertIndex(docs, doclens)
     L = _lib.lib()
+    assert ix.fused_topk_slots(256, 100) == 0        # off by default (A/B: the unfused path is faster)
+    ix.set_option(_lib.OPT_FUSED_TOPK, 1)
     fused = L.cbv2_search_workspace_size(ix._h, 256, 100, 0)
     unfused = L.cbv2_search_workspace_size(ix._h, 256, 200, 0)
     assert fused < 8 << 20 < 100 << 20 < unfused, (fused, unfused)

@@ -387,3 +387,28 @@ def test_dynamic_tail_b16_bit_identical(dev):
     for a, e in [(0, 900), (N - 3000, N)]:
         part = ColbertIndex(docs[a:e].contiguous(), doclens[a:e].contiguous()).score(Q)
         assert torch.equal(part, full[:, a:e]), (a, e)
+
+
+def test_dynamic_tail_xcd_slices_equal_shared_tail(dev):
+    """The tail handed out in 8 XCD-local slices (default), as one shared tail
+    (OPT_DYNAMIC_TAIL 2) and with no tail (0): identical scores and identical
+    fused top-k lists, bf16 and MXFP8."""
+    from hybrid_rag_colbertv2_amd.index import quantize_mxfp8
+    N, B = 150000, 64
+    g = torch.Generator(device=dev).manual_seed(13)
+    docs = torch.randn(N, 128, 128, device=dev, generator=g)
+    docs = (docs / docs.norm(dim=-1, keepdim=True)).bfloat16()
+    doclens = torch.randint(0, 129, (N,), device=dev, generator=g, dtype=torch.int32)
+    Q = torch.randn(B, 32, 128, device=dev, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16()
+    q8, s8 = quantize_mxfp8(docs)
+    for ix in (ColbertIndex(docs, doclens), ColbertIndex(q8, doclens, scales=s8)):
+        res = {}
+        for mode in (1, 2, 0):
+            ix.set_option(_lib.OPT_DYNAMIC_TAIL, mode)
+            sc = ix.score(Q)
+            assert ix.last_scan_plan()["dynamic_tail"] == (mode != 0)
+            res[mode] = (sc, ix.search(Q, 50))
+        for mode in (2, 0):
+            assert torch.equal(res[mode][0], res[1][0]), mode
+            assert torch.equal(res[mode][1][0], res[1][1][0]) and torch.equal(res[mode][1][1], res[1][1][1]), mode
