@@ -361,7 +361,20 @@ def main():
     # ---- N > 1 over RCCL: the same K steps with the native (in-ABI) exchange
     native = nsearch = None
     if nccl and not faithful:
-        nsearch = searcher if args.native_exchange else ShardedSearcher(ix, native=True, lexical_k=args.k)
+        # every rank builds the native exchange (cbv2_comm_init on torch's RCCL
+        # comm); the leg runs only if all of them could, so a failure there is
+        # reported in the line instead of stranding the other ranks in a collective
+        init_err = None
+        try:
+            nsearch = searcher if args.native_exchange else ShardedSearcher(ix, native=True, lexical_k=args.k)
+        except Exception as e:   # noqa: BLE001  reported, not fatal
+            init_err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if init_err else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            native = {"error": init_err or "the native exchange failed to initialise on another rank"}
+            nsearch = None
+    if nsearch is not None:
         nouts, nel = timed_steps(stepper(nsearch, Q), args.steps, args.warmup, world)
         nfi = nouts[-1][1].cpu().numpy()
         native = {"value": round(B * args.steps / nel, 2), "ms_per_step": round(nel / args.steps * 1e3, 3),
@@ -419,8 +432,9 @@ def main():
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
                        "parallelism": f"corpus sharded x{world}" + (
-                           (" (RCCL all-gather + all-reduce, " + ("native in-ABI" if args.native_exchange
-                                                                  else "torch.distributed") + " exchange)")
+                           ((" (RCCL all-gather + all-reduce, " + ("native in-ABI" if args.native_exchange
+                                                                   else "torch.distributed") + " exchange)")
+                            if nccl else f" ({backend} rehearsal: ranks share one GPU)")
                            if world > 1 else "")},
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
             "p99_ms_b1": round(p99, 3) if p99 is not None else None,
