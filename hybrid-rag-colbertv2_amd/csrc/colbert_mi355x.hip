@@ -732,7 +732,7 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
-          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0>
+          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -742,7 +742,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   // TPI tokens of 4 docs per iteration (32: 32 KiB, 64: 64 KiB), IPG per group
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kRowBytes;
-  constexpr int IPG = kLd / TPI, NT = TPI / 4;
+  // LD token slots per doc (128; 256 / 512 / 1024 for long documents: a doc
+  // group then spans LD / TPI iterations, the row maxima carried across them)
+  static_assert(LD % TPI == 0 && LD >= 128 && LD <= 1024, "LD: 128, 256, 512 or 1024 token slots");
+  constexpr int IPG = LD / TPI, NT = TPI / 4;
+  constexpr size_t kDocStride = (size_t)LD * kRowBytes;
   constexpr int kPieces = kIterBytes / 1024;
   constexpr int kLoadWaves = SPLITLOAD ? WAVES / 2 : WAVES;
   constexpr int kPiecesPerWave = kPieces / kLoadWaves;   // per loading wave
@@ -838,7 +842,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
         const uint32_t poff = piece_src(jj, pdoc);
         int d = 4 * G + pdoc;
         d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocBytes + (size_t)j * TPI * kRowBytes + poff;
+        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
                                          0, 0);
       };
@@ -918,7 +922,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
 #pragma unroll
           for (int x = 0; x < 4; ++x) {
             const int v = (4 * G + x < nd) ? doclens[d_begin + 4 * G + x] : 0;
-            dl4[x] = v < 0 ? 0 : (v > kLd ? kLd : v);
+            dl4[x] = v < 0 ? 0 : (v > LD ? LD : v);
           }
           dl_min = min(min(dl4[0], dl4[1]), min(dl4[2], dl4[3]));
           dl_max = max(max(dl4[0], dl4[1]), max(dl4[2], dl4[3]));
@@ -1033,11 +1037,14 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
 // flight per CU.  Same tile order, masking and epilogue as doc16, so scores are
 // bit-identical to the LDS kernel's and the rerank kernel's.
 // ---------------------------------------------------------------------------
-template <int QW>
+// LONG: docs of ld = 256 / 512 / 1024 token slots, scored 128 tokens at a time
+// with the row maxima carried across the blocks (same tile order: the bits of
+// a doc of <= 128 tokens do not depend on ld).
+template <int QW, bool LONG = false>
 __global__ __launch_bounds__(256, 2) void maxsim_scan_direct_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
-    int64_t chunk_docs) {
+    int64_t chunk_docs, int ld = kLd) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -1058,21 +1065,25 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_direct_kernel(
   for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
 
   for (int i = 0; i < nd; ++i) {
+    const int lmax = LONG ? ld : kLd;
     int dl = doclens[d_begin + i];
-    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kDocBytes;
-    bf16x8 af[kLd / 16][4];
-#pragma unroll
-    for (int rt = 0; rt < kLd / 16; ++rt)
-      if (16 * rt < dl) gbl_afrag16(dbase, rt, lane, af[rt]);
+    dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
     float m[QW][2];
 #pragma unroll
     for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {   // one block unless LONG
+      const int dlb = dl - kLd * blk;
+      const uint8_t* dbase = tokens + (size_t)(d_begin + i) * (size_t)lmax * kRowBytes + (size_t)blk * kDocBytes;
+      bf16x8 af[kLd / 16][4];
 #pragma unroll
-    for (int rt = 0; rt < kLd / 16; ++rt) {
-      if (16 * rt < dl) {
-        const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-        tile16<QW>(af[rt], qf, init, m);
+      for (int rt = 0; rt < kLd / 16; ++rt)
+        if (16 * rt < dlb) gbl_afrag16(dbase, rt, lane, af[rt]);
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; ++rt) {
+        if (16 * rt < dlb) {
+          const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+          tile16<QW>(af[rt], qf, init, m);
+        }
       }
     }
 #pragma unroll
@@ -2057,24 +2068,29 @@ constexpr int kRerankMaxC = 32768;   // BIG: 128 KiB of scores + 16 KiB of selec
 
 __device__ __forceinline__ float rerank_one_bf16(const uint8_t* __restrict__ tokens,
                                                  const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
-                                                 const bf16x8 (&qf)[1][2][4], int lq, int32_t id, int lane) {
+                                                 const bf16x8 (&qf)[1][2][4], int lq, int32_t id, int lane,
+                                                 int ld) {
   const int64_t loc = (int64_t)id - id_base;
   if (id < 0 || loc < 0 || loc >= n) return neg_inf();
   const int g = lane >> 4;
   int dl = doclens[loc];
-  dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-  const uint8_t* dbase = tokens + (size_t)loc * kDocBytes;
-  // the whole doc in flight at once (32 KiB per wave), then the scan's math
-  bf16x8 af[kLd / 16][4];
-#pragma unroll
-  for (int rt = 0; rt < kLd / 16; ++rt)
-    if (16 * rt < dl) gbl_afrag16(dbase, rt, lane, af[rt]);
+  dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
   float m[1][2] = {{neg_inf(), neg_inf()}};
+  // 128 tokens at a time (one block unless the index holds long docs): the
+  // whole block in flight at once (32 KiB per wave), then the scan's math
+  for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {
+    const int dlb = dl - kLd * blk;
+    const uint8_t* dbase = tokens + (size_t)loc * (size_t)ld * kRowBytes + (size_t)blk * kDocBytes;
+    bf16x8 af[kLd / 16][4];
 #pragma unroll
-  for (int rt = 0; rt < kLd / 16; ++rt) {
-    if (16 * rt < dl) {
-      const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-      tile16<1>(af[rt], qf, init, m);
+    for (int rt = 0; rt < kLd / 16; ++rt)
+      if (16 * rt < dlb) gbl_afrag16(dbase, rt, lane, af[rt]);
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt) {
+      if (16 * rt < dlb) {
+        const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+        tile16<1>(af[rt], qf, init, m);
+      }
     }
   }
   return reduce16(m[0][0], m[0][1], lane, lq);
@@ -2106,7 +2122,7 @@ template <bool BIG = false>
 __global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
     const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, int k,
-    float* __restrict__ out_s, int32_t* __restrict__ out_i, int32_t* __restrict__ out_p) {
+    float* __restrict__ out_s, int32_t* __restrict__ out_i, int32_t* __restrict__ out_p, int ld) {
   extern __shared__ float sc_dyn[];
   __shared__ float sc_fix[BIG ? 1 : kSmallMax];
   __shared__ uint64_t keys[BIG ? kTopkMax : kSmallMax];
@@ -2120,7 +2136,7 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
   load_qfrag16(Q, b, b + 1, lq, lane, qf[0]);
   const int32_t* crow = cand + (size_t)b * C;
   for (int c = wave; c < C; c += kRrWaves) {
-    const float v = rerank_one_bf16(tokens, doclens, n, id_base, qf, lq, crow[c], lane);
+    const float v = rerank_one_bf16(tokens, doclens, n, id_base, qf, lq, crow[c], lane, ld);
     if (lane == 0) sc[c] = v;
   }
   rerank_finish<BIG>(sc, keys, hist, misc, b, crow, C, k, out_s, out_i, out_p);
@@ -3017,7 +3033,7 @@ int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
 }
 
 template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
-          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0>
+          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
                     int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
@@ -3031,7 +3047,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE>),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
                      ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3051,14 +3067,44 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
   const int64_t waves = (int64_t)nq_groups * n_chunks;
   const int64_t grid = (waves + 3) / 4;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL(maxsim_scan_direct_kernel<QW>, dim3((unsigned)grid), dim3(256), 0, st, ix->tokens, ix->doclens,
-                     ix->n, Q, B, lq, out, ld_out, chunk_docs);
+  if (ix->ld != kLd)
+    hipLaunchKernelGGL((maxsim_scan_direct_kernel<QW, true>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                       ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
+  else
+    hipLaunchKernelGGL((maxsim_scan_direct_kernel<QW, false>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                       ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, kLd);
   return launch_check("maxsim_scan_direct_kernel");
+}
+
+// Long documents (index ld = 256 / 512 / 1024): B <= 8 the direct scan in
+// 128-token blocks, larger B the production 8-wave doc-interleaved scan with
+// its doc group spanning ld / 64 iterations (the row maxima carried across).
+int scan_maxsim_long(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
+                     int* ctr_ws) {
+  if (B <= kDirectMaxB)
+    return B == 1 ? launch_direct<1>(ix, Q, B, lq, out, ld_out, st) : launch_direct<2>(ix, Q, B, lq, out, ld_out, st);
+  switch (ix->ld) {
+    case 256:
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 0, 256>(
+          ix, Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs, nullptr, ctr_ws);
+    case 512:
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 0, 512>(
+          ix, Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs, nullptr, ctr_ws);
+    case 1024:
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 0, 1024>(
+          ix, Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs, nullptr, ctr_ws);
+    default:
+      return fail(CBV2_EUNSUPPORTED, "index ld %d not built", (int)ix->ld);
+  }
 }
 
 int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                 int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   if (ix->n == 0) return CBV2_OK;
+  if (ix->ld != kLd) {
+    if (ft != nullptr || variant != kScanAuto) return fail(CBV2_EUNSUPPORTED, "long-doc index: automatic scan only");
+    return scan_maxsim_long(ix, Q, B, lq, out, ld_out, st, ctr_ws);
+  }
   if (ft != nullptr)   // fused top-k: the B > 16 doc-interleaved scan only (fused_eligible)
     return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, true>(ix, Q, B, lq, nullptr, 0, st,
                                                                                kScanDynFrac, kScanTaskDocs, nullptr,
@@ -3177,7 +3223,7 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
 // scores, a few MB, and the selection over their many per-wave lists would
 // cost more than the matrix.
 int64_t fused_slots(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) {
-  if (!ix->fused_topk || scorer != CBV2_SCORER_MAXSIM || ix->n == 0 || k > kFusedMaxK) return 0;
+  if (!ix->fused_topk || scorer != CBV2_SCORER_MAXSIM || ix->n == 0 || k > kFusedMaxK || ix->ld != kLd) return 0;
   // MXFP8: the fused build of the f8 scan spills (its query fragments fill the
   // VGPR file): 78.1 vs 74.1 ms at 1M, B=256 (profiles/r02b_fused_ab.jsonl),
   // so MXFP8 searches stay unfused; CBV2_OPT_FUSED_TOPK = 2 forces it (A/B).
@@ -3419,8 +3465,9 @@ int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, 
   CBV2_REQUIRE(n >= 0 && n <= 0x7fffffffLL, "n out of range (%lld)", (long long)n);
   CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "global ids must fit int32");
   if (dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "index dtype %d not built (bf16 only)", dtype);
-  if (ld != kLd || d != kDim)
-    return fail(CBV2_EUNSUPPORTED, "index geometry ld=%d d=%d not built (ld=128, d=128)", ld, d);
+  if ((ld != 128 && ld != 256 && ld != 512 && ld != 1024) || d != kDim)
+    return fail(CBV2_EUNSUPPORTED, "index geometry ld=%d d=%d not built (ld = 128, 256, 512 or 1024; d = 128)", ld,
+                d);
   if (n > 0) {
     CBV2_REQUIRE(tokens != nullptr && doclens != nullptr, "null tokens/doclens");
     CBV2_REQUIRE(aligned16(tokens), "tokens must be 16-byte aligned");
@@ -3651,10 +3698,12 @@ int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int3
     CBV2_HIP(hipFuncSetAttribute((const void*)rerank_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)dyn));
     hipLaunchKernelGGL(rerank_kernel<true>, dim3((unsigned)B), dim3(kRrWaves * 64), dyn, st, ix->tokens, ix->doclens,
-                       ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids, out_pos);
+                       ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids, out_pos,
+                       (int)ix->ld);
   } else {
     hipLaunchKernelGGL(rerank_kernel<false>, dim3((unsigned)B), dim3(kRrWaves * 64), 0, st, ix->tokens, ix->doclens,
-                       ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids, out_pos);
+                       ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, k, out_scores, out_ids, out_pos,
+                       (int)ix->ld);
   }
   return launch_check("rerank_kernel");
 }
@@ -3690,6 +3739,7 @@ int cbv2_split_f32(const float* x, int64_t rows, int32_t ld, const int32_t* docl
 int cbv2_index_attach_residual(cbv2_index* ix, const void* lo, float resid_max, float norm_max) {
   CBV2_REQUIRE(ix != nullptr, "null index");
   CBV2_REQUIRE(ix->dtype == CBV2_DTYPE_BF16, "a residual attaches to a bf16 index");
+  CBV2_REQUIRE(ix->ld == kLd, "the fp32-faithful index holds docs of 128 token slots (ld %d)", (int)ix->ld);
   CBV2_REQUIRE(ix->n == 0 || (lo != nullptr && aligned16(lo)), "residual must be non-null and 16-byte aligned");
   CBV2_REQUIRE(resid_max >= 0.0f && norm_max >= 0.0f && resid_max < 3.0e38f && norm_max < 3.0e38f,
                "bounds must be finite and >= 0");

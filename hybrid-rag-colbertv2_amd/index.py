@@ -6,7 +6,9 @@ Replaces the reference's ``self.corpus_embeddings`` tensor
 is a contiguous id range ``[id_base, id_base + n)`` of the corpus laid out for
 the MI355X scan kernel:
 
-    tokens   bf16 [n, 128, 128]  (32 KiB per doc, rows >= doclen are padding)
+    tokens   bf16 [n, ld, 128]   (ld = 128 token slots: 32 KiB per doc; long
+                                  documents: ld = 256 / 512 / 1024, bf16 only;
+                                  rows >= doclen are padding)
     doclens  int32 [n]
     means    f32  [n, 128]       (optional: literal-reference scorer only)
     residual bf16 [n, 128, 128]  (optional: fp32-faithful index, lo = bf16(x - tokens))
@@ -25,6 +27,7 @@ import torch
 from . import _lib
 
 LD = 128
+LONG_LDS = (128, 256, 512, 1024)   # token slots per doc a bf16 index can hold (long documents: bf16 MaxSim)
 DIM = 128
 LQ_MAX = 32
 BAND_CAP = 16384   # fp32-faithful search: largest band rescored per query
@@ -39,6 +42,14 @@ def _require_cuda(t: torch.Tensor, name: str):
         raise ValueError(f"{name} must be a ROCm device tensor (got {t.device})")
 
 
+def long_ld(max_len: int) -> int:
+    """Token slots for docs of up to ``max_len`` tokens: the smallest of LONG_LDS."""
+    for ld in LONG_LDS:
+        if max_len <= ld:
+            return ld
+    raise ValueError(f"documents of up to {LONG_LDS[-1]} tokens are supported (got {max_len})")
+
+
 def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
                 ld: int = LD, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
     """Token matrices -> (``dtype`` [n, ld, 128] padded with zeros, int32 doclens [n]).
@@ -46,7 +57,16 @@ def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
     Accepts a dense ``[n, L, D]`` tensor (every doc has L tokens, as the
     reference's stacked encode output), a pooled ``[n, D]`` tensor (one token
     per doc: the shape ``encode`` returns by default), or a list of ``[L_i, D]``.
+    ``ld=None``: the smallest supported slot count that holds the longest doc
+    (128, or 256 / 512 / 1024 for long documents).
     """
+    if ld is None:
+        if isinstance(embs, torch.Tensor):
+            L = 1 if embs.dim() == 2 else int(embs.shape[1])
+        else:
+            embs = list(embs)
+            L = max([1] + [1 if e.dim() == 1 else int(e.shape[0]) for e in embs])
+        ld = long_ld(L)
     if isinstance(embs, torch.Tensor):
         if embs.dim() == 2:
             embs = embs.unsqueeze(1)
@@ -93,7 +113,8 @@ def quantize_mxfp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
 class ColbertIndex:
     """One shard of the corpus resident in HBM, with a C handle borrowing it.
 
-    bf16 tokens (default), or MXFP8 (``tokens`` uint8 e4m3 [n, 128, 128] plus
+    bf16 tokens (default; [n, ld, 128] with ld = 128, or 256 / 512 / 1024 for
+    long documents), or MXFP8 (``tokens`` uint8 e4m3 [n, 128, 128] plus
     ``scales`` uint8 E8M0 [n, 128, 2]; see ``ColbertIndex.mxfp8``)."""
 
     def __init__(self, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0,
@@ -103,9 +124,11 @@ class ColbertIndex:
         _require_cuda(doclens, "doclens")
         self.fp8 = tokens.dtype == torch.uint8
         want = torch.uint8 if self.fp8 else torch.bfloat16
-        if tokens.dtype != want or tokens.dim() != 3 or tuple(tokens.shape[1:]) != (LD, DIM):
-            raise ValueError(f"tokens must be bf16 or MXFP8 uint8 [n, {LD}, {DIM}] "
-                             f"(got {tokens.dtype} {tuple(tokens.shape)})")
+        lds = (LD,) if self.fp8 or residual is not None else LONG_LDS
+        if tokens.dtype != want or tokens.dim() != 3 or tokens.shape[2] != DIM or tokens.shape[1] not in lds:
+            raise ValueError(f"tokens must be bf16 [n, ld, {DIM}] (ld in {LONG_LDS}) or MXFP8 uint8 "
+                             f"[n, {LD}, {DIM}] (got {tokens.dtype} {tuple(tokens.shape)})")
+        self.ld = int(tokens.shape[1])
         if doclens.dtype != torch.int32 or doclens.shape != (tokens.shape[0],):
             raise ValueError("doclens must be int32 [n]")
         if self.fp8 and (scales is None or scales.dtype != torch.uint8
@@ -127,7 +150,7 @@ class ColbertIndex:
                 self.id_base, ctypes.byref(h)))
         else:
             _lib.check(_lib.lib().cbv2_index_create(
-                dev, self.tokens.data_ptr(), _lib.DTYPE_BF16, self.n, LD, DIM, self.doclens.data_ptr(),
+                dev, self.tokens.data_ptr(), _lib.DTYPE_BF16, self.n, self.ld, DIM, self.doclens.data_ptr(),
                 self.id_base, ctypes.byref(h)))
         self._h = h
         self.residual: Optional[torch.Tensor] = None
@@ -188,7 +211,9 @@ class ColbertIndex:
         device = torch.device(device)
         if dtype not in ("bf16", "fp8", "fp32"):
             raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
-        tokens, doclens = pack_tokens(embs, device, dtype=torch.float32 if dtype == "fp32" else torch.bfloat16)
+        # bf16 indexes take long documents (ld = 256 / 512 / 1024); MXFP8 and fp32-faithful hold 128 slots
+        tokens, doclens = pack_tokens(embs, device, ld=None if dtype == "bf16" else LD,
+                                      dtype=torch.float32 if dtype == "fp32" else torch.bfloat16)
         if dtype == "fp32":
             ix = cls.faithful_f32(tokens, doclens, id_base=id_base)
         elif dtype == "fp8":
@@ -201,7 +226,7 @@ class ColbertIndex:
                 f32 = embs if embs.dim() == 3 else embs.unsqueeze(1)
                 f32 = f32.to(device=device, dtype=torch.float32).contiguous()
             else:
-                f32 = torch.zeros((ix.n, LD, DIM), dtype=torch.float32, device=device)
+                f32 = torch.zeros((ix.n, ix.ld, DIM), dtype=torch.float32, device=device)
                 for i, e in enumerate(embs):
                     e = e if e.dim() == 2 else e.unsqueeze(0)
                     f32[i, : e.shape[0]] = e.to(device=device, dtype=torch.float32)
@@ -213,6 +238,8 @@ class ColbertIndex:
         """Write this shard to the native index file (include/colbert_mi355x.h)."""
         if self.faithful:
             raise ValueError("the native file holds bf16/MXFP8 tokens; save an fp32-faithful index's fp32 source")
+        if self.ld != LD:
+            raise ValueError(f"the native file holds docs of {LD} token slots (this index: {self.ld})")
         dt = _lib.DTYPE_MXFP8 if self.fp8 else _lib.DTYPE_BF16
         torch.cuda.current_stream(self.device).synchronize()
         _lib.check(_lib.lib().cbv2_index_file_write(

@@ -25,9 +25,12 @@
  *    :789) leave tie order unspecified; this is the defined refinement.
  *
  * Index layout in HBM (see DESIGN.md "Data layout"):
- *    tokens   bf16 [n][ld = 128][d = 128], row-major, 16-byte aligned;
+ *    tokens   bf16 [n][ld][d = 128], row-major, 16-byte aligned; ld = 128
+ *             token slots (every path), or 256 / 512 / 1024 for long
+ *             documents (bf16 MaxSim scan, search and rerank; the MXFP8 and
+ *             fp32-faithful indexes and the native file hold ld = 128);
  *             rows t >= doclens[i] of doc i are padding and never score.
- *    doclens  int32 [n], 0 <= doclens[i] <= 128.
+ *    doclens  int32 [n], 0 <= doclens[i] <= ld.
  *    Local doc i has global id  id_base + i  (contiguous shard of the corpus).
  */
 #ifndef COLBERT_MI355X_H

@@ -1,0 +1,107 @@
+"""Long documents (index ld = 256 / 512 / 1024 token slots, bf16): the
+reference's chunks run to 1024 BERT tokens (local_rag_complete.py:63-64);
+MaxSim over a long doc is the same sum over query tokens of the max over ALL
+its tokens (LRC:807-812 docstring / north_star).  The doc-interleaved scan
+spans ld/64 iterations per doc group and the direct scan and the rerank work
+128 tokens at a time, carrying the row maxima.  Checked against the float64
+oracle (1e-3), the oracle's selection of the GPU's own scores (bit for bit),
+and bit-identity with the 128-slot index on docs of <= 128 tokens."""
+import numpy as np
+import pytest
+import torch
+
+from _parity import assert_ranking_consistent, assert_selection_exact
+from hybrid_rag_colbertv2_amd.index import ColbertIndex
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-3
+
+
+def rand_unit(g, *shape):
+    x = torch.randn(*shape, generator=g)
+    return x / x.norm(dim=-1, keepdim=True)
+
+
+def make_case(seed, N, ld, B):
+    g = torch.Generator().manual_seed(seed)
+    docs = rand_unit(g, N, ld, 128).bfloat16()
+    doclens = torch.randint(0, ld + 1, (N,), generator=g, dtype=torch.int32)
+    doclens[:6] = torch.tensor([0, 1, 127, 128, 129, ld], dtype=torch.int32)
+    Q = rand_unit(g, B, 32, 128).bfloat16()
+    return docs, doclens, Q
+
+
+@pytest.mark.parametrize("ld,N", [(256, 3000), (512, 1200), (1024, 500)])
+@pytest.mark.parametrize("B", [1, 5, 40])
+def test_long_docs_score_search_rerank(dev, ld, N, B):
+    docs, doclens, Q = make_case(ld + B, N, ld, B)
+    ix = ColbertIndex(docs.to(dev), doclens.to(dev), id_base=3)
+    assert ix.ld == ld
+    got = ix.score(Q.to(dev)).cpu().numpy()
+    ref = orc.maxsim(Q.float().numpy(), docs.float().numpy(), doclens.numpy())
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(got[fin], ref[fin], atol=ATOL, rtol=0)
+    s, i = ix.search(Q.to(dev), 50)
+    assert_selection_exact(i.cpu().numpy(), s.cpu().numpy(), got, 50, id_base=3)
+    assert_ranking_consistent(i.cpu().numpy(), ref, ATOL, id_base=3)
+    g = np.random.default_rng(ld)
+    cand = g.integers(0, N, size=(B, 60)).astype(np.int32) + 3
+    rs, ri, rp = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), 10)
+    raw = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), 0).cpu().numpy()
+    np.testing.assert_array_equal(raw, got[np.arange(B)[:, None], cand - 3])     # same bits as the scan
+    for b in range(B):
+        exp = orc.rerank_select(raw[b], 10)
+        assert [int(x) for x in rp[b].cpu()] == [e[0] for e in exp], b
+
+
+@pytest.mark.parametrize("ld", [256, 1024])
+def test_long_index_of_short_docs_bit_identical(dev, ld):
+    """Docs of <= 128 tokens in a long-doc index score exactly as in the
+    128-slot index (every scan path: B = 1, 5, 40)."""
+    g = torch.Generator().manual_seed(ld)
+    N = 2000
+    short = rand_unit(g, N, 128, 128).bfloat16()
+    doclens = torch.randint(0, 129, (N,), generator=g, dtype=torch.int32)
+    long = torch.zeros((N, ld, 128), dtype=torch.bfloat16)
+    long[:, :128] = short
+    long[:, 128:] = 7.0                                    # padding rows never score
+    a = ColbertIndex(short.to(dev), doclens.to(dev))
+    b = ColbertIndex(long.to(dev), doclens.to(dev))
+    for B in (1, 5, 40):
+        Q = rand_unit(g, B, 32, 128).bfloat16().to(dev)
+        assert torch.equal(a.score(Q), b.score(Q)), B
+
+
+def test_long_docs_dynamic_tail(dev):
+    """ld = 256 over a corpus large enough for the dynamic tail (B = 40: two
+    query groups): every score equals a small static-split index's."""
+    N, ld, B = 12000, 256, 40
+    g = torch.Generator(device=dev).manual_seed(3)
+    docs = torch.randn(N, ld, 128, device=dev, generator=g)
+    docs = (docs / docs.norm(dim=-1, keepdim=True)).bfloat16()
+    doclens = torch.randint(0, ld + 1, (N,), device=dev, generator=g, dtype=torch.int32)
+    Q = torch.randn(B, 32, 128, device=dev, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16()
+    ix = ColbertIndex(docs, doclens)
+    full = ix.score(Q)
+    assert ix.last_scan_plan()["dynamic_tail"]
+    for a, e in [(0, 500), (N - 1500, N)]:
+        part = ColbertIndex(docs[a:e].contiguous(), doclens[a:e].contiguous()).score(Q)
+        assert torch.equal(part, full[:, a:e]), (a, e)
+
+
+def test_from_embeddings_picks_long_ld(dev):
+    g = torch.Generator().manual_seed(1)
+    embs = [rand_unit(g, L, 128) for L in (5, 130, 300, 64)]
+    ix = ColbertIndex.from_embeddings(embs, device=dev)
+    assert ix.ld == 512 and ix.doclens.cpu().tolist() == [5, 130, 300, 64]
+    Q = rand_unit(g, 2, 32, 128)
+    docs = torch.zeros((4, 512, 128))
+    for i, e in enumerate(embs):
+        docs[i, : e.shape[0]] = e.bfloat16().float()
+    ref = orc.maxsim(Q.bfloat16().float().numpy(), docs.numpy(), np.array([5, 130, 300, 64]))
+    np.testing.assert_allclose(ix.score(Q.to(dev)).cpu().numpy(), ref, atol=ATOL, rtol=0)
+    with pytest.raises(ValueError):
+        ColbertIndex.from_embeddings(embs, device=dev, dtype="fp8")   # MXFP8 holds 128 slots

@@ -69,16 +69,54 @@ def run(config, n, batches, dtype, out):
     torch.cuda.empty_cache()
 
 
+def run_long(n, ld, batches, out):
+    """Long documents (not a BASELINE config): n docs of ld token slots, all
+    full, random unit tokens (the index bytes of n * ld / 128 standard docs)."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    tokens = torch.empty((n, ld, 128), dtype=torch.bfloat16, device=dev)
+    for a in range(0, n, 8192):
+        x = torch.randn((min(8192, n - a), ld, 128), device=dev, generator=g)
+        tokens[a:a + x.shape[0]] = (x / x.norm(dim=-1, keepdim=True)).bfloat16()
+    doclens = torch.full((n,), ld, dtype=torch.int32, device=dev)
+    ix = ColbertIndex(tokens, doclens)
+    Qf = synth.make_queries(max(batches), 32, seed=1)
+    flop = 2 * 32 * ld * 128
+    for B in batches:
+        Q = Qf[:B].to(dev, torch.bfloat16)
+        ms = timed(lambda: ix.search(Q, 100))
+        if B >= 16:
+            ach = B * n * flop / (ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": 2500.0, "unit": "TFLOP/s",
+                    "frac": round(ach / 2500.0, 4)}
+        else:
+            ach = n * ld * 256 / (ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+                    "frac": round(ach / 8000.0, 4)}
+        line = {"config": f"long documents (ld={ld})", "docs": n, "ld": ld, "batch": B, "dtype": "bf16", "k": 100,
+                "ms": round(ms, 3), "qps": round(B / (ms * 1e-3), 1), "roofline": roof}
+        print(json.dumps(line), flush=True)
+        out.write(json.dumps(line) + "\n")
+    del ix, tokens
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "config_sweep.jsonl"))
+    ap.add_argument("--long-only", action="store_true", help="only the long-document rows")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as out:
+        if a.long_only:
+            run_long(250_000, 512, [1, 256], out)
+            run_long(125_000, 1024, [1, 256], out)
+            return
         run("C2 (100k docs, MaxSim-only top-100)", 100_000, [1, 16, 64, 256], "bf16", out)
         run("C3 stage 2 (1M docs)", 1_000_000, [1, 16, 64, 256], "bf16", out)
         run("C4 per-GPU shard (10M / 8)", 1_250_000, [256], "bf16", out)
         run("C5 per-GPU shard (10M / 8, MXFP8)", 1_250_000, [1, 256], "fp8", out)
+        run_long(250_000, 512, [1, 256], out)
 
 
 if __name__ == "__main__":
