@@ -362,9 +362,30 @@ class ColbertIndex:
         except KeyError:
             raise ValueError(f"unknown scorer {scorer!r}; expected one of {sorted(_lib.SCORERS)}") from None
 
+    # ----------------------------------------------------------------- long queries
+    @staticmethod
+    def _query_blocks(Q: torch.Tensor, scorer: str):
+        """MaxSim queries of more than 32 tokens -> blocks of <= 32 tokens (None
+        otherwise).  MaxSim is a sum over query tokens (LRC:807-812), so the
+        score of a long query is the sum of its blocks' scores, each block one
+        pass of the kernels (which hold 32 query tokens per MFMA column pair)."""
+        if scorer != "maxsim":
+            return None
+        if Q.dim() == 2:
+            Q = Q.unsqueeze(0)
+        if Q.dim() != 3 or Q.shape[1] <= LQ_MAX:
+            return None
+        return [Q[:, a:a + LQ_MAX].contiguous() for a in range(0, Q.shape[1], LQ_MAX)]
+
     # ----------------------------------------------------------------- compute
     def score(self, Q: torch.Tensor, scorer: str = "maxsim") -> torch.Tensor:
         """f32 [B, n] scores of every doc of the shard (the reference's _maxsim_score)."""
+        blocks = self._query_blocks(Q, scorer)
+        if blocks is not None:     # long queries: the blocks' scores summed in block order
+            out = self.score(blocks[0], scorer).clone()
+            for q in blocks[1:]:
+                out += self.score(q, scorer)
+            return out
         sid = self._scorer(scorer)
         _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
         out = torch.empty((B, max(self.n, 1)), dtype=torch.float32, device=self.device)
@@ -379,6 +400,8 @@ class ColbertIndex:
 
     def search(self, Q: torch.Tensor, k: int, scorer: str = "maxsim") -> Tuple[torch.Tensor, torch.Tensor]:
         """Top-k over the shard: (f32 [B, k] scores, int32 [B, k] global ids), -inf/-1 padded."""
+        if self._query_blocks(Q, scorer) is not None:   # long queries: summed block scores + radix top-k
+            return topk_rows(self.score(Q, scorer), int(k), id_base=self.id_base)
         sid = self._scorer(scorer)
         _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
         if self.faithful and scorer == "maxsim":
@@ -414,6 +437,15 @@ class ColbertIndex:
 
         k > 0: (scores [B, k], ids [B, k], positions [B, k]); k == 0: raw scores [B, C].
         """
+        blocks = self._query_blocks(Q, "maxsim")
+        if blocks is not None:     # long queries: the blocks' raw candidate scores summed, then selected
+            raw = self.rerank(blocks[0], cand, 0).clone()
+            for q in blocks[1:]:
+                raw += self.rerank(q, cand, 0)
+            if k == 0:
+                return raw
+            cand = cand.to(device=self.device, dtype=torch.int32)
+            return select_topk(raw, int(k), ids=cand if cand.dim() == 2 else cand.unsqueeze(0))
         _keep, qptr, _, Bq, lq = self._prep_query(Q, "maxsim")
         cand = cand.to(device=self.device, dtype=torch.int32).contiguous()
         if cand.dim() == 1:

@@ -248,7 +248,7 @@ def test_errors_raise_without_launch(dev):
     with pytest.raises(ValueError):
         ix.rerank(Q.to(dev), torch.zeros((2, 40000), dtype=torch.int32, device=dev), k=5)   # C > 32768
     with pytest.raises(ValueError):
-        ix.score(torch.zeros(1, 33, 128, device=dev))
+        ix.score(torch.zeros(1, 33, 64, device=dev))             # wrong embedding dim
     with pytest.raises(ValueError):
         ix.score(Q.to(dev), scorer="nope")
     with pytest.raises(Exception):
@@ -412,3 +412,25 @@ def test_dynamic_tail_xcd_slices_equal_shared_tail(dev):
         for mode in (2, 0):
             assert torch.equal(res[mode][0], res[1][0]), mode
             assert torch.equal(res[mode][1][0], res[1][1][0]) and torch.equal(res[mode][1][1], res[1][1][1]), mode
+
+
+@pytest.mark.parametrize("lq,B", [(70, 3), (33, 40), (64, 1)])
+def test_long_queries_sum_of_blocks(dev, lq, B):
+    """Queries of more than 32 tokens: MaxSim is a sum over query tokens
+    (LRC:807-812), so score / search / rerank run the kernels on blocks of
+    <= 32 tokens and add the blocks' scores."""
+    docs, doclens, Q = make_case(lq * 7 + B, 900, B, lq)
+    ix = ColbertIndex(docs.to(dev), doclens.to(dev), id_base=9)
+    got = ix.score(Q.to(dev)).cpu().numpy()
+    ref = orc.maxsim(Q.float().numpy(), docs.float().numpy(), doclens.numpy())
+    np.testing.assert_allclose(got, ref, atol=ATOL, rtol=0)
+    s, i = ix.search(Q.to(dev), 30)
+    assert_selection_exact(i.cpu().numpy(), s.cpu().numpy(), got, 30, id_base=9)
+    cand = np.random.default_rng(lq).integers(9, 909, size=(B, 40)).astype(np.int32)
+    raw = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), 0).cpu().numpy()
+    np.testing.assert_array_equal(raw, got[np.arange(B)[:, None], cand - 9])
+    rs, ri, rp = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), 10)
+    for b in range(B):
+        exp = orc.rerank_select(raw[b], 10)
+        assert [int(x) for x in rp[b].cpu()] == [e[0] for e in exp], b
+        assert [int(x) for x in ri[b].cpu()] == [int(cand[b, e[0]]) for e in exp], b
