@@ -524,6 +524,48 @@ __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const b
   }
 }
 
+// k-step-major order (lab, MORDER 1): the NC chains of a tile advance one
+// k-step at a time with NC live accumulators, so NC consecutive MFMAs share
+// their A fragment (doc rows) and only B (the query) changes; tile t-1's row
+// maxima are taken between tile t's k-step-0 MFMAs (the accumulator a max
+// reads is rewritten by the MFMA right after it).  Per chain the same k order
+// and the same max: bit-identical to iter4_full.
+template <int QW, int NT = 8>
+__device__ __forceinline__ void iter4_full_kmajor(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
+                                                  float (&m)[QW][2]) {
+  constexpr int NC = 2 * QW;
+  const int c = lane & 15, g = lane >> 4;
+  const uint8_t* rowp = buf + (4 * NT * (c >> 2) + (c & 3)) * kRowBytes;
+  auto frag = [&](int t, bf16x8 (&a)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      a[s] = *reinterpret_cast<const bf16x8*>(rowp + 4 * t * kRowBytes + 16 * ((4 * g + s) ^ c));
+  };
+  auto fold = [&](int cc, const f32x4& y) {
+    float& mm = m[cc >> 1][cc & 1];
+    mm = fmaxf(fmaxf(fmaxf(fmaxf(mm, y[0]), y[1]), y[2]), y[3]);
+  };
+  bf16x8 a[2][4];
+  f32x4 acc[NC];
+  frag(0, a[0]);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t + 1 < NT) frag(t + 1, a[(t + 1) & 1]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int cc = 0; cc < NC; ++cc) {
+        if (s == 0 && t > 0) fold(cc, acc[cc]);
+        acc[cc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t & 1][s], qf[cc >> 1][cc & 1][s],
+                                                          s == 0 ? f32x4{} : acc[cc], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+#pragma unroll
+  for (int cc = 0; cc < NC; ++cc) fold(cc, acc[cc]);
+}
+
 // Iteration j with ragged docs: per-lane-group -inf C-init masks padding rows.
 template <int QW, int NT = 8>
 __device__ __forceinline__ void iter4_ragged(const uint8_t* buf, int lane, int j, int dl_g, int dl_max,
@@ -732,7 +774,8 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
-          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd>
+          bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd,
+          int MORDER = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -949,7 +992,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
             else
               iter4_full<QW, D, NT>(buf, lane, qf, m);
           } else {
-            iter4_full<QW, D, NT, NoTileHook, PROBE>(buf, lane, qf, m);
+            if constexpr (MORDER == 1)
+              iter4_full_kmajor<QW, NT>(buf, lane, qf, m);
+            else
+              iter4_full<QW, D, NT, NoTileHook, PROBE>(buf, lane, qf, m);
           }
         } else if (TPI * j < dl_max)
           iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
@@ -3033,7 +3079,7 @@ int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
 }
 
 template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
-          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd>
+          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd, int MORDER = 0>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
                     int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
@@ -3047,7 +3093,7 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD>),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD, MORDER>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
                      ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);

@@ -66,3 +66,21 @@ def test_band_contains_exact_topk():
         band = set(np.nonzero(T[b] >= tk - 2 * beta[b])[0].tolist())
         assert set(ids_exact[b].tolist()) <= band
         assert len(band) < len(T[b])          # the band is a real filter on this data
+
+
+def test_maxsim_additive_over_query_token_blocks():
+    """The identity the long-query path (ColbertIndex._query_blocks) rests on:
+    MaxSim sums over query tokens (LRC:807-812), so a query's score is the sum
+    of its 32-token blocks' scores -- checked on the oracle in float64, with
+    ragged and empty docs."""
+    import numpy as np
+    from oracle import oracle as orc
+    g = np.random.default_rng(4)
+    Q = g.standard_normal((3, 70, 128))
+    docs = g.standard_normal((50, 128, 128))
+    doclens = g.integers(0, 129, 50)
+    full = orc.maxsim(Q, docs, doclens)
+    parts = sum(orc.maxsim(Q[:, a:a + 32], docs, doclens) for a in range(0, 70, 32))
+    fin = np.isfinite(full)
+    assert (np.isneginf(full) == np.isneginf(parts)).all()
+    np.testing.assert_allclose(parts[fin], full[fin], rtol=0, atol=1e-9)

@@ -387,6 +387,15 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   if (kind == 24)
     return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 2>(ix, q, B, lq, out, ld, st, dyn_frac,
                                                                                  task_docs);
+  // kind 25: kind 13 with the k-step-major MFMA order (iter4_full_kmajor: 8 live
+  // accumulators, consecutive MFMAs share the doc fragment); bit-identical
+  if (kind == 25)
+    return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 0, kLd, 1>(ix, q, B, lq, out, ld, st,
+                                                                                         dyn_frac, task_docs);
+  // kind 26: the B <= 16 shape (kind 6) with the k-step-major MFMA order
+  if (kind == 26)
+    return launch_scan16x4<4, 4, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 1>(ix, q, B, lq, out, ld, st,
+                                                                                          dyn_frac, task_docs);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
