@@ -19,6 +19,7 @@ owned here and borrowed by the C handle.
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
@@ -235,9 +236,12 @@ class ColbertIndex:
 
     # ----------------------------------------------------------------- native file
     def save(self, path: str) -> None:
-        """Write this shard to the native index file (include/colbert_mi355x.h)."""
-        if self.faithful:
-            raise ValueError("the native file holds bf16/MXFP8 tokens; save an fp32-faithful index's fp32 source")
+        """Write this shard to the native index file (include/colbert_mi355x.h).
+
+        An fp32-faithful index is two bf16 files of the same layout -- ``path``
+        (hi, the tokens every scan reads) and ``path + ".resid"`` (lo) -- plus
+        ``path + ".bounds.json"`` (the split's bounds), so a rank loads its doc
+        range of both exactly as for a bf16 index."""
         if self.ld != LD:
             raise ValueError(f"the native file holds docs of {LD} token slots (this index: {self.ld})")
         dt = _lib.DTYPE_MXFP8 if self.fp8 else _lib.DTYPE_BF16
@@ -245,6 +249,12 @@ class ColbertIndex:
         _lib.check(_lib.lib().cbv2_index_file_write(
             os.fsencode(path), dt, self.n, self.tokens.data_ptr(), self.scales.data_ptr() if self.fp8 else None,
             self.doclens.data_ptr(), self.id_base, _stream_ptr(self.device)))
+        if self.faithful:
+            _lib.check(_lib.lib().cbv2_index_file_write(
+                os.fsencode(path + ".resid"), _lib.DTYPE_BF16, self.n, self.residual.data_ptr(), None,
+                self.doclens.data_ptr(), self.id_base, _stream_ptr(self.device)))
+            with open(path + ".bounds.json", "w") as f:
+                json.dump({"resid_max": self.bounds[0], "norm_max": self.bounds[1]}, f)
 
     @classmethod
     def load(cls, path: str, device="cuda", begin: int = 0, end: Optional[int] = None) -> "ColbertIndex":
@@ -266,6 +276,20 @@ class ColbertIndex:
                 os.fsencode(path), begin, end, tokens.data_ptr() if m else None,
                 scales.data_ptr() if (fp8 and m) else None, doclens.data_ptr() if m else None,
                 _stream_ptr(device)))
+        if not fp8 and os.path.exists(path + ".resid") and os.path.exists(path + ".bounds.json"):
+            # fp32-faithful: the residual file's same doc range, and the split's bounds
+            resid = torch.empty((m, LD, DIM), dtype=torch.bfloat16, device=device)
+            dl2 = torch.empty((m,), dtype=torch.int32, device=device)
+            with torch.cuda.device(device):
+                _lib.check(_lib.lib().cbv2_index_file_read(
+                    os.fsencode(path + ".resid"), begin, end, resid.data_ptr() if m else None, None,
+                    dl2.data_ptr() if m else None, _stream_ptr(device)))
+            with open(path + ".bounds.json") as f:
+                b = json.load(f)
+            if not torch.equal(dl2, doclens):
+                raise ValueError(f"{path}.resid does not match {path}")
+            return cls(tokens, doclens, id_base=id_base + begin, residual=resid,
+                       bounds=(float(b["resid_max"]), float(b["norm_max"])))
         return cls(tokens, doclens, id_base=id_base + begin, scales=scales)
 
     def close(self):

@@ -50,7 +50,7 @@ class JinaColBERTRetriever:
     def _build(self, embeddings) -> ColbertIndex:
         return ColbertIndex.from_embeddings(embeddings, device=self.device,
                                             build_means=(self.scorer == "ref_meanpool_cosine"),
-                                            dtype=getattr(self.config, "index_dtype", "bf16"))
+                                            dtype=getattr(self.config, "index_dtype", "fp32"))
 
     def _encode_docs(self, texts: List[str]):
         try:
@@ -74,7 +74,7 @@ class JinaColBERTRetriever:
         n = len(corpus)
         bs = int(batch_size or getattr(self.config, "ingest_batch", 256))
         keep_pt = n <= int(getattr(self.config, "index_pt_max_docs", 50_000))
-        dtype = getattr(self.config, "index_dtype", "bf16")
+        dtype = getattr(self.config, "index_dtype", "fp32")
         print(f"  Encoding {n} documents...")
         if self.scorer == "ref_meanpool_cosine" or n == 0:
             # the literal scorer needs every doc's fp32 means: one pass as the reference does
@@ -100,7 +100,7 @@ class JinaColBERTRetriever:
                 saved = [e for h in host for e in (h if isinstance(h, list) else list(h.unbind(0)))]
             torch.save({"embeddings": saved, "corpus": corpus},
                        os.path.join(self.config.colbert_index_path, "index.pt"))
-        elif not self.corpus_embeddings.faithful:
+        else:
             self.save_native()
 
     def load(self) -> None:

@@ -368,7 +368,7 @@ def test_jina_encoder_gpu_matches_fp32_cpu(dev):
     eager = gpu.encode_ids(ids, mask)
     gpu.capture_queries(len(qs))
     assert torch.equal(gpu.encode_ids(ids, mask), eager)
-    cfg = RAGConfig()
+    cfg = RAGConfig(index_dtype="bf16")     # the check below scores the bf16 index's own values
     r = JinaColBERTRetriever(cfg, encoder=gpu)
     corpus = [f"doc {i} about topic {i % 7} and thing {i % 3}" for i in range(50)]
     r.index_embeddings(gpu.encode(corpus, is_query=False), corpus=corpus)
@@ -379,3 +379,34 @@ def test_jina_encoder_gpu_matches_fp32_cpu(dev):
                      ix.doclens.cpu().numpy())[0]
     assert [x["document_id"] for x in res] == [int(i) for i in np.argsort(-ref, kind="stable")[:5]]
     np.testing.assert_allclose([x["score"] for x in res], np.sort(ref)[::-1][:5], atol=1e-3)
+
+
+def test_faithful_index_native_file_roundtrip(dev, tmp_path):
+    """An fp32-faithful index persists as hi + residual native files + bounds,
+    and loads back (whole and by rank shard) with identical search results."""
+    from hybrid_rag_colbertv2_amd.distributed import shard_range
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    g = torch.Generator().manual_seed(4)
+    N = 2500
+    x = torch.randn(N, 128, 128, generator=g)
+    x = x / x.norm(dim=-1, keepdim=True)
+    doclens = torch.randint(0, 129, (N,), generator=g, dtype=torch.int32)
+    Q = torch.randn(5, 32, 128, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).to(dev)
+    ix = ColbertIndex.faithful_f32(x.to(dev), doclens.to(dev), id_base=7)
+    path = str(tmp_path / "f.cbv2")
+    ix.save(path)
+    back = ColbertIndex.load(path, device=dev)
+    assert back.faithful and back.bounds == ix.bounds and back.id_base == 7
+    assert torch.equal(back.residual, ix.residual) and torch.equal(back.tokens, ix.tokens)
+    s0, i0 = ix.search(Q, 30)
+    s1, i1 = back.search(Q, 30)
+    assert torch.equal(s0, s1) and torch.equal(i0, i1)
+    a, b = shard_range(N, 1, 3)
+    sh = ColbertIndex.load(path, device=dev, begin=a, end=b)
+    assert sh.faithful and sh.id_base == 7 + a and torch.equal(sh.residual, ix.residual[a:b])
+
+
+def test_default_config_is_fp32_faithful():
+    from hybrid_rag_colbertv2_amd.config import RAGConfig
+    assert RAGConfig().index_dtype == "fp32"
