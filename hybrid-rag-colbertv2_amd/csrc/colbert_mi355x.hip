@@ -2602,23 +2602,40 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
   }
 }
 
-// Band collect: row b of the bf16 scan's scores T; every doc with T >= T_k -
-// 2 beta(b) is appended (global id) to cand[b][0..cap); count[b] = the band
-// size (may exceed cap: the search then recomputes that row in full).  Hits
-// gather in an LDS list (LDS atomics; the global counter of a row is hit by
-// one atomic per workgroup, not one per wave hit), flushed once at the end.
+// Exact lower bound of each row's k-th faithful score: the minimum of the
+// faithful scores of the k docs the bf16 scan ranked first (F[b][0..k), row
+// stride ld): k docs score at least that much, so the k-th best does too.
+__global__ __launch_bounds__(64) void band_lb_kernel(const float* __restrict__ F, int ld, int k,
+                                                     float* __restrict__ lb) {
+  const int b = blockIdx.x;
+  float m = __builtin_inff();
+  for (int j = threadIdx.x; j < k; j += 64) m = fminf(m, F[(size_t)b * ld + j]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+  if (threadIdx.x == 0) lb[b] = m;
+}
+
+// Band collect: row b of the bf16 scan's scores T; every doc with T >= thr is
+// appended (global id) to cand[b][0..cap); count[b] = the band size (may
+// exceed cap: the search then recomputes that row in full).  thr = lb[b] -
+// beta(b) when the exact lower bound lb of the k-th score is given (every doc
+// of the exact top-k has T >= S - beta >= S_k - beta >= lb - beta), else T_k -
+// 2 beta(b) (S_k >= T_k - beta).  Hits gather in an LDS list (LDS atomics; the
+// global counter of a row is hit by one atomic per workgroup, not one per
+// wave hit), flushed once at the end.
 constexpr int kBandLds = 2048;
 __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restrict__ T, int64_t n,
                                                            const float* __restrict__ topk_s, int k,
                                                            const float* __restrict__ beta, int64_t id_base,
                                                            int cap, int32_t* __restrict__ cand,
-                                                           int32_t* __restrict__ count) {
+                                                           int32_t* __restrict__ count,
+                                                           const float* __restrict__ lb = nullptr) {
   __shared__ int32_t s_ids[kBandLds];
   __shared__ int s_n, s_base;
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
-  const float thr = topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b];
+  const float thr = lb != nullptr ? lb[b] - beta[b] : topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b];
   const float* row = T + (size_t)b * n;
   int32_t* crow = cand + (size_t)b * cap;
   constexpr int U = 8;  // 8 coalesced loads in flight per thread, then the ballots
@@ -2848,6 +2865,7 @@ struct cbv2_index {
   int fused_topk_mode = 0;   // its value (2: also the MXFP8 scan, A/B only)
   int dynamic_tail = 1;      // CBV2_OPT_DYNAMIC_TAIL (1: XCD-sliced tail, 2: one shared tail, 0: off)
   int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
+  bool band_lower_bound = true;  // CBV2_OPT_BAND_LOWER_BOUND
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -3408,6 +3426,7 @@ struct F32Ws {
   uint16_t* qhi = nullptr;
   uint16_t* qlo = nullptr;
   float* beta = nullptr;
+  float* lb = nullptr;
   int32_t* count = nullptr;
   int32_t* cand = nullptr;
   float* F = nullptr;
@@ -3438,6 +3457,7 @@ size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8
   w->qhi = (uint16_t*)take(qbytes);
   w->qlo = (uint16_t*)take(qbytes);
   w->beta = (float*)take((size_t)B * sizeof(float));
+  if (op == CBV2_F32_SEARCH) w->lb = (float*)take((size_t)B * sizeof(float));
   if (op == CBV2_F32_RERANK) w->F = (float*)take((size_t)B * cap * sizeof(float));
   if (op == CBV2_F32_SEARCH) {
     w->count = (int32_t*)take((size_t)B * sizeof(int32_t));
@@ -3693,6 +3713,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
     case CBV2_OPT_BAND_DOC_MAJOR:
       ix->band_doc_major = (int)value;
       return CBV2_OK;
+    case CBV2_OPT_BAND_LOWER_BOUND:
+      ix->band_lower_bound = value != 0;
+      return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);
   }
@@ -3844,14 +3867,24 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr))) return rc;
   if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
     return rc;
-  // 2. band T >= T_k - 2 beta, 3. faithful rescoring, 4. exact top-k of the band
+  // 2. the band: every doc with T >= lb - beta, lb = an exact lower bound of
+  //    the k-th faithful score (the bf16 top-k's own faithful scores: the
+  //    minimum of k of them), or T_k - 2 beta without that pass (A/B);
+  // 3. faithful rescoring of the band, 4. exact top-k of the band
+  const float* lb = nullptr;
+  if (ix->band_lower_bound) {
+    if ((rc = launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, w.F, cap, st))) return rc;
+    hipLaunchKernelGGL(band_lb_kernel, dim3((unsigned)B), dim3(64), 0, st, w.F, cap, k, w.lb);
+    if ((rc = launch_check("band_lb_kernel"))) return rc;
+    lb = w.lb;
+  }
   CBV2_HIP(hipMemsetAsync(w.count, 0, (size_t)B * sizeof(int32_t), st));
   int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
   const int64_t max_splits = (ix->n + 8191) / 8192;
   splits = splits < max_splits ? splits : max_splits;
   splits = splits < 1 ? 1 : splits;
   hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
-                     out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count);
+                     out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb);
   if ((rc = launch_check("band_collect_kernel"))) return rc;
   if (ix->band_doc_major) {   // pairs grouped by doc: each band doc's tiles read once per batch
     CBV2_HIP(hipMemsetAsync(w.dcnt, 0, (size_t)ix->n * sizeof(int32_t), st));

@@ -99,6 +99,10 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *  CBV2_OPT_BAND_DOC_MAJOR 1: cbv2_search_f32 rescores its band grouped by
  *                        doc (each band doc read once per batch; 0: pair by
  *                        pair).  Identical results either way.
+ *  CBV2_OPT_BAND_LOWER_BOUND 1: cbv2_search_f32 first rescores the bf16
+ *                        top-k, whose minimum faithful score lb bounds the
+ *                        k-th from below, and bands T >= lb - beta (0: the
+ *                        wider T >= T_k - 2 beta).  Identical results.
  * cbv2_index_last_scan_plan: the work split of this handle's latest scan
  * launch: {workgroups, static chunk docs, static docs, dynamic tail 0/1}.
  * Thread safety: one handle may be used from several host threads and
@@ -107,6 +111,7 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_FUSED_TOPK 1
 #define CBV2_OPT_DYNAMIC_TAIL 2
 #define CBV2_OPT_BAND_DOC_MAJOR 3
+#define CBV2_OPT_BAND_LOWER_BOUND 4
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the
@@ -198,9 +203,10 @@ int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const i
  * cap = the band capacity (SEARCH) or C (RERANK), 0 for SCORE.
  *  - cbv2_score_f32: faithful scores of every doc, out[b * ld_out + i]
  *    (lo.qhi + hi.qlo + hi.qhi on the bf16 MFMA, fp32 accumulate).
- *  - cbv2_search_f32: bf16 scan of hi (T), the k-th T of each query, then
- *    every doc with T >= T_k - 2 beta(q) is rescored faithfully and the exact
- *    top-k of that band is returned.  beta(q) bounds |T - S| for every doc
+ *  - cbv2_search_f32: bf16 scan of hi (T), its top-k, whose faithful scores'
+ *    minimum lb bounds the k-th faithful score from below; then every doc
+ *    with T >= lb - beta(q) is rescored faithfully and the exact top-k of
+ *    that band is returned.  beta(q) bounds |T - S| for every doc
  *    (Cauchy-Schwarz on the residuals of docs and query, plus accumulation
  *    slack), so the band holds the faithful top-k of the whole corpus.
  *    out_status int32 [B]: the band size, or -1 when the band exceeded `cap`

@@ -2,7 +2,8 @@
 
 The reference keeps fp32 embeddings (local_rag_complete.py:735-746) and scores
 them in fp32 (:802-831).  The faithful search scans hi = bf16(x) with bf16(q)
-(score T), then rescores every doc with T >= T_k - 2 beta(q).  These tests pin
+(score T), then rescores every doc with T >= lb - beta(q) (lb: the minimum exact
+score of the bf16 top-k; or T >= T_k - 2 beta(q)).  These tests pin
 the two facts that make that exact: |T - S| <= beta(q) for every doc, and the
 band therefore holds the exact top-k.  (Parity unpinned by reference fixtures:
 the reference has no fp32-vs-bf16 case; the exact fp64 MaxSim of the fp32
@@ -84,3 +85,26 @@ def test_maxsim_additive_over_query_token_blocks():
     fin = np.isfinite(full)
     assert (np.isneginf(full) == np.isneginf(parts)).all()
     np.testing.assert_allclose(parts[fin], full[fin], rtol=0, atol=1e-9)
+
+
+def test_lower_bound_band_contains_exact_topk_and_is_narrower():
+    """The two-pass band of cbv2_search_f32 (CBV2_OPT_BAND_LOWER_BOUND): lb =
+    the minimum exact score of the k docs the bf16 scan ranks first is a lower
+    bound of the exact k-th score, so every exact top-k doc has T >= lb - beta;
+    that band is no wider than T >= T_k - 2 beta (lb >= T_k - beta)."""
+    for seed, k in ((3, 10), (4, 50), (5, 100)):
+        docs, doclens, Q = case(seed, N=1500)
+        hi, _, (E, M) = orc.split_f32(docs, doclens)
+        S = orc.maxsim(Q, docs, doclens)
+        T = orc.maxsim(orc.bf16_round(Q), hi, doclens)
+        beta = orc.band_beta(Q, E, M)
+        _, tk = orc.topk(T, k)                                  # the bf16 scan's top-k (ids)
+        lb = np.array([S[b, tk[b]].min() for b in range(len(Q))])
+        _, ek = orc.topk(S, k)                                  # the exact top-k
+        Tk = orc.topk(T, k)[0][:, -1]
+        for b in range(len(Q)):
+            band_lb = T[b] >= lb[b] - beta[b]
+            band_plain = T[b] >= Tk[b] - 2 * beta[b]
+            assert band_lb[ek[b]].all(), (seed, b)
+            assert lb[b] >= Tk[b] - beta[b] - 1e-12
+            assert band_lb.sum() <= band_plain.sum()

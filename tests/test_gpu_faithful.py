@@ -164,3 +164,23 @@ def test_band_doc_major_equals_pair_major(dev, N, dups):
     rs, _ = orc.topk(exact, 100, id_base=5)
     fin = np.isfinite(rs)
     np.testing.assert_allclose(s1.cpu().numpy()[fin], rs[fin], atol=ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("N,k", [(20000, 100), (3000, 10), (50, 100)])
+def test_band_lower_bound_equals_plain_band(dev, N, k):
+    """The two-pass band (the bf16 top-k rescored first; its minimum faithful
+    score lb bounds the k-th from below; band T >= lb - beta) returns the plain
+    band's (T >= T_k - 2 beta) results bit for bit, with a band no wider."""
+    docs, doclens, Q = make_case(N + k, N, 5, 32)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=11)
+    s1, i1 = ix.search(Q.to(dev), k)
+    b1 = ix.last_band.clone()
+    ix.set_option(_lib.OPT_BAND_LOWER_BOUND, 0)
+    s0, i0 = ix.search(Q.to(dev), k)
+    b0 = ix.last_band.clone()
+    assert torch.equal(i1, i0) and torch.equal(s1, s0)
+    assert (b1 >= 0).all() and (b1 <= b0).all(), (b1, b0)
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    rs, _ = orc.topk(exact, k, id_base=11)
+    fin = np.isfinite(rs)
+    np.testing.assert_allclose(s1.cpu().numpy()[fin], rs[fin], atol=ATOL, rtol=0)
