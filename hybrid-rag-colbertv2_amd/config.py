@@ -18,7 +18,7 @@ Added fields (no reference counterpart):
                           scores within ~1e-5 and their exact top-k, as the
                           north star's 1e-3 contract requires for an encoder
                           that returns fp32 embeddings),
-                          "bf16" (~9 % more queries/s; scores within ~5e-3 of
+                          "bf16" (~3 % more queries/s; scores within ~5e-3 of
                           fp32 on fp32 embeddings, exact on bf16-valued ones)
                           or "fp8" (MXFP8, config 5).
   * ``ingest_batch`` / ``index_pt_max_docs`` — batched, bounded-memory
