@@ -451,7 +451,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// The production B > 8 scan: doc-interleaved row tiles.  A 16-row A tile
+// The production B >= 3 scan: doc-interleaved row tiles.  A 16-row A tile
 // holds 4 consecutive tokens of each of 4 docs (rows 4g..4g+3 = doc g), so
 // the lanes of MFMA output group g accumulate exactly doc g's row maxima:
 // the per-doc epilogue needs no cross-group fold (no permlane swaps), just one
@@ -697,14 +697,40 @@ __device__ __forceinline__ void topk_flush(uint64_t* buf, uint8_t* state, int k,
 
 // Dynamic-tail task grab (one thread): writes (doc offset into the tail, size;
 // size 0 = done) to slot[0..1].  task_docs > 0: fixed tasks, the counter counts
-// tasks; task_docs < 0: guided, the counter counts docs and a task takes
-// max(-task_docs, remaining / (2 * workgroups per query group)) docs (CAS: every
-// failed CAS means another workgroup advanced, so the loop ends).
+// tasks; task_docs < 0: guided, by ticket: one atomicAdd draws ticket t, and
+// round r = the r-th group of P tickets (P = workgroups per query group) hands
+// out tasks of max(-task_docs, dyn / 2^(r+1) / P) docs (round r covers at most
+// half of what rounds 0..r-1 left), so the offset of every ticket is a closed
+// form and no grab ever retries.  (The earlier CAS form took remaining / 2P per
+// grab: with 64 workgroups on one counter, one CAS won per round trip, and the
+// serialized grants cost B=8 at 125k docs 0.78 -> 1.93 ms at a 30 % tail.
+// CBV2_TAIL_CAS=1 rebuilds it for lab A/Bs.)
+#ifndef CBV2_TAIL_CAS
+#define CBV2_TAIL_CAS 0
+#endif
+__device__ __forceinline__ void ticket_task(int t, int dyn, int P, int minsz, int& o, int& sz) {
+  int off = 0, s = minsz;
+  for (int r = 0; r < 31; ++r) {
+    s = ((dyn >> (r + 1)) / P) & ~15;
+    if (s <= minsz) {   // this round and all later ones: minsz-doc tasks
+      s = minsz;
+      break;
+    }
+    if (t < P) break;
+    off += s * P;
+    t -= P;
+  }
+  const int64_t o64 = (int64_t)off + (int64_t)t * s;
+  o = o64 < dyn ? (int)o64 : dyn;
+  sz = o < dyn ? (dyn - o < s ? dyn - o : s) : 0;
+}
 __device__ __forceinline__ void next_task(int* ctr, int task_docs, int dyn, int P, int* slot) {
   int o, sz;
   if (task_docs > 0) {
     o = atomicAdd(ctr, 1) * task_docs;
     sz = o < dyn ? (dyn - o < task_docs ? dyn - o : task_docs) : 0;
+  } else if (!CBV2_TAIL_CAS) {
+    ticket_task(atomicAdd(ctr, 1), dyn, P, -task_docs, o, sz);
   } else {
     o = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
@@ -2964,7 +2990,8 @@ int launch_check(const char* what) {
 enum ScanVariant {
   kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
-  kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScanAuto = -1
+  kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
+  kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
 // 1: 58.3 %, 2: 61.7 %, 3: 65.3 %, 4: 59.4 %, 5: 52.0 %, 6: 61.2 %, 8: 54.8 %
@@ -2973,11 +3000,17 @@ enum ScanVariant {
 // under the current doc's last MFMAs (carried fragments push the loop past 256
 // VGPRs; hipcc spills the query fragments: 12 % of peak).
 constexpr int kDefaultScan = kScanAuto;
-// Auto dispatch (measured, 1M docs, tools/scan_lab.py): B<=8 direct scan
-// (B=1: 5.0 ms = 6.5 TB/s of doc bytes; B=8: 13.7 ms vs 18.4 ms for the LDS
-// kernel), B<=16 the 16-query LDS kernel, larger B the 32-query LDS kernel.
-constexpr int kDirectMaxB = 8;
+// Auto dispatch (measured, tools/scan_lab.py, round 2, r02z): B <= 2 the
+// direct scan (HBM-bound: B=1 5.3 ms, B=2 5.3 ms at 1M docs); 3 <= B <= 8 the
+// 4-wave doc-interleaved scan with 2 queries per wave (B=8: 6.3 ms vs 13.8 for
+// the direct scan, whose 4 query groups each stream every doc into VGPRs;
+// B=3-4: ~6.3 vs 7.8 ms; at 125k docs 0.84 vs 1.79 ms at B=8); B <= 16 the
+// same with 4 queries per wave; larger B the 8-wave scan.  Long documents
+// keep the direct scan up to B=8 (kLongDirectMaxB).
+constexpr int kDirectMaxB = 2;
+constexpr int kSmallQ2MaxB = 8;
 constexpr int kSmallLdsMaxB = 16;
+constexpr int kLongDirectMaxB = 8;
 
 template <int WAVES, int QW, int PER_CU, typename Kern>
 int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
@@ -3145,7 +3178,7 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
 // its doc group spanning ld / 64 iterations (the row maxima carried across).
 int scan_maxsim_long(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                      int* ctr_ws) {
-  if (B <= kDirectMaxB)
+  if (B <= kLongDirectMaxB)
     return B == 1 ? launch_direct<1>(ix, Q, B, lq, out, ld_out, st) : launch_direct<2>(ix, Q, B, lq, out, ld_out, st);
   switch (ix->ld) {
     case 256:
@@ -3174,8 +3207,10 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
                                                                                kScanDynFrac, kScanTaskDocs, nullptr,
                                                                                ctr_ws, ft);
   if (variant == kScanAuto)
-    variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2)
-                               : (B <= kSmallLdsMaxB ? kScan16x4W4 : kScan16x4W8);
+    variant = B <= kDirectMaxB    ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2)
+              : B <= kSmallQ2MaxB ? kScan16x4W4Q2
+              : B <= kSmallLdsMaxB ? kScan16x4W4
+                                   : kScan16x4W8;
   switch (variant) {
     case kScanDirectQ1:
       return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
@@ -3205,12 +3240,20 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16x4W4:
       return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
                                                    nullptr, ctr_ws);
+    case kScan16x4W4Q2:   // 8 queries per workgroup (2 per wave)
+      return launch_scan16x4<4, 2, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
     default:
       return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
   }
 }
 
-constexpr int kF8DirectMaxB = 8;
+// B <= 2: the direct scan (HBM-bound); 3 <= B <= 8: the doc-interleaved scan
+// in 4-wave workgroups x 2 queries, two per CU (lab, r02aa, 1M docs: B=4 3.25
+// vs 4.75 ms direct, B=8 3.74 vs 8.93; 125k: B=8 0.46 vs 1.27 ms); larger B
+// 8 waves x 8 queries.
+constexpr int kF8DirectMaxB = 2;
+constexpr int kF8SmallMaxB = 8;
 constexpr int kF8Waves = 8, kF8QW = 8;
 
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
@@ -3245,7 +3288,9 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
     return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st, dyn_frac,
                                                                       task_docs, ctr_ws, ft);
-  if (B <= kF8DirectMaxB) {
+  if (B > kF8DirectMaxB && B <= kF8SmallMaxB && shape == 0)
+    return launch_f8x4<32, 3, true, 2, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+  if (B <= kF8DirectMaxB && shape == 0) {
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
     const int64_t target_waves = 8LL * cu_count(ix->device);
@@ -3276,6 +3321,9 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     // workgroups per CU (2 waves per SIMD from independent barrier domains)
     case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    // small batches (B <= 8): 4-wave workgroups x 2 queries, two / three per CU
+    case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
 #endif
     default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
   }
@@ -3292,7 +3340,7 @@ int64_t fused_slots(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) 
   // VGPR file): 78.1 vs 74.1 ms at 1M, B=256 (profiles/r02b_fused_ab.jsonl),
   // so MXFP8 searches stay unfused; CBV2_OPT_FUSED_TOPK = 2 forces it (A/B).
   if (ix->dtype == CBV2_DTYPE_MXFP8) {
-    if (B <= kF8DirectMaxB || ix->fused_topk_mode < 2) return 0;
+    if (B <= kF8SmallMaxB || ix->fused_topk_mode < 2) return 0;
     return scan_chunks(ix, (B + kF8Waves * kF8QW - 1) / (kF8Waves * kF8QW), cu_count(ix->device));
   }
   if (B <= kSmallLdsMaxB) return 0;

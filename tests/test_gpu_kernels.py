@@ -256,8 +256,9 @@ def test_errors_raise_without_launch(dev):
 
 
 def test_small_batch_scan_bit_identical_to_batched(dev):
-    """B<=8 runs the direct (HBM-streaming) scan, 9..16 the 4-wave and larger B the
-    8-wave doc-interleaved LDS scan: same bits."""
+    """B<=2 runs the direct (HBM-streaming) scan, 3..8 the 4-wave doc-interleaved
+    LDS scan with 2 queries per wave, 9..16 with 4, and larger B the 8-wave one:
+    same bits."""
     docs, doclens, Q = make_case(123, 900, 20, 32)
     ix = ColbertIndex(docs.to(dev), doclens.to(dev))
     full = ix.score(Q.to(dev))
@@ -317,17 +318,22 @@ def test_dynamic_tail_split_bit_identical(dev):
     np.testing.assert_allclose(full[:6, sel].cpu().numpy(), ref, atol=ATOL, rtol=0)
 
 
-def test_dynamic_tail_writes_every_score(dev):
+@pytest.mark.parametrize("N", [70000, 700000])
+def test_dynamic_tail_writes_every_score(dev, N):
     """Through the C ABI into a NaN-filled buffer: the static chunks and the
     dynamic tasks together cover every (query, doc) exactly as the small-index
-    static split scores it."""
+    static split scores it.  At 700k docs the tail's first ticket rounds hand
+    out tasks larger than the 16-doc minimum (shrinking round by round)."""
     import ctypes  # noqa: F401
     from hybrid_rag_colbertv2_amd import _lib
     from hybrid_rag_colbertv2_amd.index import _stream_ptr
-    N, B = 70000, 64                        # 2 query groups -> 128 chunks; tail active from 512 * 128 docs
+    B = 64                                  # 2 query groups -> 128 chunks; tail active from 512 * 128 docs
     g = torch.Generator(device=dev).manual_seed(9)
-    docs = torch.randn(N, 128, 128, device=dev, generator=g)
-    docs = (docs / docs.norm(dim=-1, keepdim=True)).bfloat16()
+    docs = torch.empty(N, 128, 128, device=dev, dtype=torch.bfloat16)
+    for a in range(0, N, 50000):
+        x = torch.randn(min(50000, N - a), 128, 128, device=dev, generator=g)
+        docs[a:a + x.shape[0]] = (x / x.norm(dim=-1, keepdim=True)).bfloat16()
+        del x
     doclens = torch.randint(0, 129, (N,), device=dev, generator=g, dtype=torch.int32)
     Q = torch.randn(B, 32, 128, device=dev, generator=g)
     Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16().contiguous()
@@ -340,6 +346,8 @@ def test_dynamic_tail_writes_every_score(dev):
     for a, b in [(0, 300), (N - 7000, N - 3000), (N - 3000, N)]:
         part = ColbertIndex(docs[a:b].contiguous(), doclens[a:b].contiguous()).score(Q)
         assert torch.equal(part, out[:, a:b]), (a, b)
+    ix.set_option(_lib.OPT_DYNAMIC_TAIL, 0)
+    assert torch.equal(ix.score(Q), out)                             # static split only
 
 
 @pytest.mark.gpu
@@ -387,6 +395,43 @@ def test_dynamic_tail_b16_bit_identical(dev):
     for a, e in [(0, 900), (N - 3000, N)]:
         part = ColbertIndex(docs[a:e].contiguous(), doclens[a:e].contiguous()).score(Q)
         assert torch.equal(part, full[:, a:e]), (a, e)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "mxfp8"])
+def test_small_batch_ticket_tail_covers_every_doc(dev, dtype):
+    """3 <= B <= 8 (4-wave scan, 2 queries per wave) over 460k docs: the 30 %
+    dynamic tail is handed out by ticket (rounds of shrinking tasks, then
+    16-doc tasks); through the C ABI into a NaN-filled buffer every score is
+    written and equals the B=1 direct scan's and the static split's bits."""
+    from hybrid_rag_colbertv2_amd.index import _stream_ptr, quantize_mxfp8
+    N, B = 460000, 5
+    g = torch.Generator(device=dev).manual_seed(21)
+    docs = torch.empty(N, 128, 128, device=dev, dtype=torch.bfloat16)
+    for a in range(0, N, 50000):
+        x = torch.randn(min(50000, N - a), 128, 128, device=dev, generator=g)
+        docs[a:a + x.shape[0]] = (x / x.norm(dim=-1, keepdim=True)).bfloat16()
+        del x
+    doclens = torch.randint(0, 129, (N,), device=dev, generator=g, dtype=torch.int32)
+    Q = torch.randn(B, 32, 128, device=dev, generator=g)
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).bfloat16().contiguous()
+    if dtype == "mxfp8":
+        q8, s8 = quantize_mxfp8(docs)
+        del docs
+        ix = ColbertIndex(q8, doclens, scales=s8)
+    else:
+        ix = ColbertIndex(docs, doclens)
+    out = torch.full((B, N), float("nan"), device=dev)
+    _keep, qptr, qdt, _, _ = ix._prep_query(Q, "maxsim")
+    _lib.check(_lib.lib().cbv2_score(ix._h, _lib.SCORERS["maxsim"], qptr, qdt, B, 32, out.data_ptr(), N,
+                                     _stream_ptr(dev)))
+    torch.cuda.synchronize()
+    plan = ix.last_scan_plan()
+    assert plan["dynamic_tail"] and 0 < plan["static_docs"] < N, plan
+    assert not torch.isnan(out).any()
+    for b in (0, 4):
+        assert torch.equal(ix.score(Q[b:b + 1]), out[b:b + 1]), b      # B=1: the direct scan
+    ix.set_option(_lib.OPT_DYNAMIC_TAIL, 0)
+    assert torch.equal(ix.score(Q), out)                             # static split only
 
 
 def test_dynamic_tail_xcd_slices_equal_shared_tail(dev):

@@ -6,6 +6,8 @@
 //           instruction) into a private LDS ring of S slots, vmcnt-throttled;
 //   ldsr  : as lds, and the wave also reads each landed KiB back from LDS
 //           (ds_read_b128: the scan's A-fragment reads).
+// "nt" rows: the same with the non-temporal cache policy (nt loads; aux = 2
+// on the LDS-DMA), the streaming hint for bytes read once.
 // Grid = CUs x WPC waves (256-thread workgroups).  Development tool
 // (tools/probes/), not product.  usage: bw_probe [GiB]
 #include <hip/hip_runtime.h>
@@ -27,7 +29,7 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
     }                                                                                 \
   } while (0)
 
-template <int U>
+template <int U, bool NT = false>
 __global__ __launch_bounds__(256) void vgpr_stream(const uint8_t* __restrict__ buf, size_t per_wave,
                                                    unsigned* __restrict__ sink) {
   const int lane = threadIdx.x & 63;
@@ -37,7 +39,10 @@ __global__ __launch_bounds__(256) void vgpr_stream(const uint8_t* __restrict__ b
   for (size_t off = 0; off < per_wave; off += (size_t)U * 1024) {
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(base + off + u * 1024 + lane * 16);
+    for (int u = 0; u < U; ++u) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(base + off + u * 1024 + lane * 16);
+      v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) acc ^= v[u];
   }
@@ -46,7 +51,7 @@ __global__ __launch_bounds__(256) void vgpr_stream(const uint8_t* __restrict__ b
 }
 
 // S slots of 1 KiB per wave; vmcnt(S-1) keeps S-1 pieces in flight.
-template <int S, bool READ>
+template <int S, bool READ, int AUX = 0>
 __global__ __launch_bounds__(256) void lds_stream(const uint8_t* __restrict__ buf, size_t per_wave,
                                                   unsigned* __restrict__ sink) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * S * 1024];
@@ -60,7 +65,7 @@ __global__ __launch_bounds__(256) void lds_stream(const uint8_t* __restrict__ bu
   for (size_t i = 0; i < n; ++i) {
     const int slot = (int)(i % S);
     __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + i * 1024 + lane * 16),
-                                     (lds_void_t*)(ring + slot * 1024), 16, 0, 0);
+                                     (lds_void_t*)(ring + slot * 1024), 16, 0, AUX);
     if (i + 1 >= (size_t)S) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S - 1) : "memory");
       if (READ) acc ^= *reinterpret_cast<const u32x4*>(ring + ((i + 1) % S) * 1024 + lane * 16);
@@ -113,11 +118,15 @@ int main(int argc, char** argv) {
     rep("vgpr U=4", time_it(vgpr_stream<4>, grid, buf, per_wave, sink));
     rep("vgpr U=8", time_it(vgpr_stream<8>, grid, buf, per_wave, sink));
     rep("vgpr U=16", time_it(vgpr_stream<16>, grid, buf, per_wave, sink));
+    rep("vgpr U=8 nt", time_it(vgpr_stream<8, true>, grid, buf, per_wave, sink));
+    rep("vgpr U=16 nt", time_it(vgpr_stream<16, true>, grid, buf, per_wave, sink));
     if (wpc <= 8) {
       rep("lds S=8", time_it(lds_stream<8, false>, grid, buf, per_wave, sink));
       rep("lds S=16", time_it(lds_stream<16, false>, grid, buf, per_wave, sink));
       rep("lds S=32", time_it(lds_stream<32, false>, grid, buf, per_wave, sink));
       rep("ldsr S=16", time_it(lds_stream<16, true>, grid, buf, per_wave, sink));
+      rep("lds S=16 nt", time_it(lds_stream<16, false, 2>, grid, buf, per_wave, sink));
+      rep("lds S=32 nt", time_it(lds_stream<32, false, 2>, grid, buf, per_wave, sink));
     }
   }
   CHECK(hipFree(buf));

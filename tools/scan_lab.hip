@@ -396,6 +396,12 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   if (kind == 26)
     return launch_scan16x4<4, 4, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 1>(ix, q, B, lq, out, ld, st,
                                                                                           dyn_frac, task_docs);
+  // kind 27 / 28: the 4-wave shape with 2 queries per wave (8 per workgroup:
+  // production kScan16x4W4Q2) / its phase-stamped build
+  if (kind == 27)
+    return launch_scan16x4<4, 2, 2, 2, 2, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
+  if (kind == 28 && stamps != nullptr)
+    return launch_scan16x4<4, 2, 2, 2, 2, true, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
@@ -434,9 +440,9 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
   const uint8_t* Qb = (const uint8_t*)Qbuf;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   hipStream_t st = (hipStream_t)stream;
-  if (variant == 1 || B <= kF8DirectMaxB) return scan_f8(ix, Qb, B, lq, out, ld, st);
+  if (variant == 1 || (B <= kF8SmallMaxB && variant < 10)) return scan_f8(ix, Qb, B, lq, out, ld, st);
   if (variant == 2) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.0f);  // doc-interleaved, static split only
-  if (variant >= 10 && variant <= 18) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
+  if (variant >= 10 && variant <= 20) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
                                                      variant - 10);  // iteration shapes, see scan_f8
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;

@@ -4,7 +4,8 @@ rule 24), on the bench's synthetic corpus; check every variant's scores
 against variant 0 and the oracle.  usage: scan_lab.py [--docs N] [--batch B] [--rounds R] [--variants 0,1,2]
 Variants: an int = a production/lab scan variant (lab_scan); "f<frac>t<docs>" =
 the production B > 16 scan with that dynamic-tail split (lab_scan16x4), e.g.
-f0t128 (static), f0.1t128; a suffix k<kind> selects a lab kernel build of lab_scan16x4."""
+f0t128 (static), f0.1t128; a suffix k<kind> selects a lab kernel build of lab_scan16x4; a prefix "n:" runs the variant
+from the alternate build (-D flags in env SCANLAB_ALT_DEFS)."""
 import argparse
 import ctypes
 import os
@@ -22,15 +23,27 @@ from hybrid_rag_colbertv2_amd.index import ColbertIndex  # noqa: E402
 from oracle import oracle as orc  # noqa: E402
 
 LAB = os.path.join(ROOT, "tools", "_build", "libscanlab.so")
+# "n:" variants run in a second build with the -D flags of ALT_DEFS (env
+# SCANLAB_ALT_DEFS; default: the round-1 CAS task grab of the dynamic tail)
+LAB_NT = os.path.join(ROOT, "tools", "_build", "libscanlab_alt.so")
+ALT_DEFS = os.environ.get("SCANLAB_ALT_DEFS", "-DCBV2_TAIL_CAS=1").split()
 
 
 def build():
     src = os.path.join(ROOT, "tools", "scan_lab.hip")
-    if not os.path.exists(LAB) or os.path.getmtime(LAB) < max(os.path.getmtime(src), os.path.getmtime(
-            os.path.join(ROOT, "hybrid-rag-colbertv2_amd", "csrc", "colbert_mi355x.hip"))):
-        os.makedirs(os.path.dirname(LAB), exist_ok=True)
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                        "-fno-honor-nans", "-I", os.path.join(ROOT, "include"), src, "-o", LAB], check=True)
+    stamp = LAB_NT + ".defs"
+    if not os.path.exists(stamp) or open(stamp).read() != " ".join(ALT_DEFS):
+        if os.path.exists(LAB_NT):
+            os.remove(LAB_NT)
+    for lib, defs in ((LAB, []), (LAB_NT, ALT_DEFS)):
+        if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(src), os.path.getmtime(
+                os.path.join(ROOT, "hybrid-rag-colbertv2_amd", "csrc", "colbert_mi355x.hip"))):
+            os.makedirs(os.path.dirname(lib), exist_ok=True)
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                            "-fno-honor-nans", *defs, "-I", os.path.join(ROOT, "include"), src, "-o", lib],
+                           check=True)
+    with open(stamp, "w") as f:
+        f.write(" ".join(ALT_DEFS))
 
 
 def main():
@@ -48,13 +61,16 @@ def main():
     build()
     if a.build_only:
         return
-    L = ctypes.CDLL(LAB)
-    L.lab_scan.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                           ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
-    L.lab_scan_f8.argtypes = L.lab_scan.argtypes
-    L.lab_scan16x4.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p,
-                               ctypes.c_int]
+    libs = {}
+    for key, path in (("", LAB), ("n:", LAB_NT)):
+        L = ctypes.CDLL(path)
+        L.lab_scan.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        L.lab_scan_f8.argtypes = L.lab_scan.argtypes
+        L.lab_scan16x4.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_int]
+        libs[key] = L
     dev = torch.device("cuda:0")
     Qf = synth.make_queries(a.batch, 32, seed=1)
     planted = synth.planted_ids(max(a.batch, 8), a.docs, 10, seed=2)[: a.batch]
@@ -75,7 +91,7 @@ def main():
         Q = Qf.to(dev, torch.bfloat16)
         qptr = Q.data_ptr()
     st = torch.cuda.current_stream()
-    variants = [v if v.startswith("f") else int(v) for v in a.variants.split(",")]
+    variants = a.variants.split(",")
     outs = {v: torch.empty((a.batch, a.docs), device=dev) for v in variants}
 
     def split(v):
@@ -86,13 +102,15 @@ def main():
         return float(fr), int(td), int(kind)
 
     def run(v, stamps=None):
-        if isinstance(v, str):
-            fr, td, kind = split(v)
+        L = libs["n:" if v.startswith("n:") else ""]
+        v0 = v[2:] if v.startswith("n:") else v
+        if v0.startswith("f"):
+            fr, td, kind = split(v0)
             rc = L.lab_scan16x4(ix._h, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream, fr, td,
                                 stamps, kind)
         else:
             fn = L.lab_scan_f8 if fp8 else L.lab_scan
-            rc = fn(ix._h, v, qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
+            rc = fn(ix._h, int(v0), qptr, a.batch, 32, outs[v].data_ptr(), a.docs, st.cuda_stream)
         assert rc == 0, rc
 
     for v in variants:
