@@ -3008,9 +3008,35 @@ constexpr int kDefaultScan = kScanAuto;
 // same with 4 queries per wave; larger B the 8-wave scan.  Long documents
 // keep the direct scan up to B=8 (kLongDirectMaxB).
 constexpr int kDirectMaxB = 2;
-constexpr int kSmallQ2MaxB = 8;
 constexpr int kSmallLdsMaxB = 16;
 constexpr int kLongDirectMaxB = 8;
+
+// Auto shape for B > kDirectMaxB: the doc-interleaved shape with the least
+// ceil(B / queries per workgroup) x (time per query group), from per-group
+// times measured at 1M docs over B = 8..256 (lab r02af: every shape at every
+// B, same process).  The query groups of a doc chunk share its tiles through
+// L2, so a launch costs about its group count times the group time; ties go
+// to the larger shape.  Checked against the measured best at every B of the
+// sweep (bf16 B = 24/40/48/80/96/128: Q2/Q2/W4/W4/W8/W8; MXFP8 24/40/80/96/
+// 128/192: 9/9/7/8/5/5).
+struct ShapeCost {
+  int qpb;      // queries per workgroup
+  float ms;     // one query group over 1M docs
+  int id;       // scan variant / f8 shape
+};
+template <int N>
+int pick_shape(const ShapeCost (&c)[N], int B) {
+  int best = c[0].id;
+  float best_ms = 1e30f;
+  for (int i = 0; i < N; ++i) {
+    const float ms = (float)((B + c[i].qpb - 1) / c[i].qpb) * c[i].ms;
+    if (ms <= best_ms) best_ms = ms, best = c[i].id;
+  }
+  return best;
+}
+// bf16: 4 waves x 2 queries (5.5 ms per group; B=8 alone 6.3), 4 x 4 (9.6;
+// B=16 alone 10.6), 8 x 4 (17.4; B=256 = 8 groups 139 ms)
+constexpr ShapeCost kBf16Shapes[] = {{8, 5.5f, kScan16x4W4Q2}, {16, 9.6f, kScan16x4W4}, {32, 17.4f, kScan16x4W8}};
 
 template <int WAVES, int QW, int PER_CU, typename Kern>
 int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
@@ -3018,7 +3044,7 @@ int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, flo
   constexpr int QPB = WAVES * QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   const int64_t target = (int64_t)PER_CU * cu_count(ix->device);  // resident workgroups
-  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  int64_t n_chunks = target / nq_groups;   // never more workgroups than resident slots
   if (n_chunks < 1) n_chunks = 1;
   if (n_chunks > ix->n) n_chunks = ix->n;
   const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
@@ -3069,7 +3095,7 @@ struct ScanSplit {
 
 int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, int task_docs, hipStream_t st,
                ScanSplit* sp, int* ctr_ws) {
-  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  int64_t n_chunks = target / nq_groups;   // never more workgroups than resident slots
   if (n_chunks < 1) n_chunks = 1;
   if (n_chunks > ix->n) n_chunks = ix->n;
   sp->task_docs = task_docs > 0 ? std::max(64, task_docs & ~63) : -std::max(16, (-task_docs) & ~15);
@@ -3123,7 +3149,7 @@ int finish_split(cbv2_index* ix, const ScanSplit& sp, hipStream_t st) {
 // Static chunks per query group of a launch (plan_split's first step): the
 // slot count a fused top-k launch writes at most.
 int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
-  int64_t n_chunks = (target + nq_groups - 1) / nq_groups;
+  int64_t n_chunks = target / nq_groups;   // never more workgroups than resident slots
   if (n_chunks < 1) n_chunks = 1;
   if (n_chunks > ix->n) n_chunks = ix->n;
   return n_chunks;
@@ -3156,7 +3182,7 @@ template <int QW>
 int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
   const int nq_groups = (B + QW - 1) / QW;
   const int64_t target_waves = 8LL * cu_count(ix->device);  // 2 waves per SIMD
-  int64_t n_chunks = (target_waves + nq_groups - 1) / nq_groups;
+  int64_t n_chunks = target_waves / nq_groups;
   if (n_chunks > ix->n) n_chunks = ix->n;
   if (n_chunks < 1) n_chunks = 1;
   const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
@@ -3207,10 +3233,7 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
                                                                                kScanDynFrac, kScanTaskDocs, nullptr,
                                                                                ctr_ws, ft);
   if (variant == kScanAuto)
-    variant = B <= kDirectMaxB    ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2)
-              : B <= kSmallQ2MaxB ? kScan16x4W4Q2
-              : B <= kSmallLdsMaxB ? kScan16x4W4
-                                   : kScan16x4W8;
+    variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2) : pick_shape(kBf16Shapes, B);
   switch (variant) {
     case kScanDirectQ1:
       return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
@@ -3254,6 +3277,13 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
 // 8 waves x 8 queries.
 constexpr int kF8DirectMaxB = 2;
 constexpr int kF8SmallMaxB = 8;
+// MXFP8 shapes (scan_f8's shape ids), ms per query group at 1M docs: 9 = 4
+// waves x 2 queries, two per CU (3.0; B=8 alone 3.74); 7 = 4 x 4, three per
+// CU (5.2; B=16 alone 5.81); 8 = 4 x 8, two per CU (9.5); 5 = 8 x 8, one per
+// CU (18.2; B=256 = 4 groups 72.5).  Against the 8 x 8 shape for every B > 8
+// (round 1): B=16 17.93 -> 5.81 ms, B=32 18.45 -> 10.77, B=48 19.63 -> 16.88
+// (lab r02ad), B=80 35.1 -> 26.2 (r02af).
+constexpr ShapeCost kF8Shapes[] = {{8, 3.0f, 9}, {16, 5.2f, 7}, {32, 9.5f, 8}, {64, 18.2f, 5}};
 constexpr int kF8Waves = 8, kF8QW = 8;
 
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
@@ -3288,13 +3318,12 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
     return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st, dyn_frac,
                                                                       task_docs, ctr_ws, ft);
-  if (B > kF8DirectMaxB && B <= kF8SmallMaxB && shape == 0)
-    return launch_f8x4<32, 3, true, 2, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+  if (B > kF8DirectMaxB && shape == 0) shape = pick_shape(kF8Shapes, B);
   if (B <= kF8DirectMaxB && shape == 0) {
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
     const int64_t target_waves = 8LL * cu_count(ix->device);
-    int64_t n_chunks = (target_waves + nq_groups - 1) / nq_groups;
+    int64_t n_chunks = target_waves / nq_groups;
     if (n_chunks > ix->n) n_chunks = ix->n;
     if (n_chunks < 1) n_chunks = 1;
     const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
@@ -3304,10 +3333,12 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                        ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
     return launch_check("maxsim_scan_f8_direct_kernel");
   }
-  // shape (lab A/B): 0 production = 32-token iterations / 3-deep ring with the
-  // prefetch after each tile's first MFMA (PF: 75.7 -> 73.5 ms at 1M, B=256);
-  // 1 = the same without PF, 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 /
-  // 2-deep (2-4 spill at 8 queries per wave), 5 = 0, 6 = 2 with PF
+  // shape: 0 = auto (above); 5 = 8 waves x 8 queries, 32-token iterations /
+  // 3-deep ring with the prefetch after each tile's first MFMA (PF: 75.7 ->
+  // 73.5 ms at 1M, B=256); 7 / 8 / 9 = the 4-wave shapes of kF8Shapes.  Lab
+  // A/B only: 1 = 5 without PF, 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 /
+  // 2-deep (2-4 spill at 8 queries per wave), 6 = 2 with PF, 10 = 9 with
+  // three workgroups per CU.
   switch (shape) {
     case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
@@ -3315,14 +3346,14 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 5: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-#ifdef CBV2_LAB
-    // lab, 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave,
-    // three workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two
-    // workgroups per CU (2 waves per SIMD from independent barrier domains)
+    // 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave, three
+    // workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two per CU
+    // (2 waves per SIMD from independent barrier domains); 9 = 2 queries per
+    // wave, two per CU
     case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    // small batches (B <= 8): 4-wave workgroups x 2 queries, two / three per CU
     case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+#ifdef CBV2_LAB
     case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
 #endif
     default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);

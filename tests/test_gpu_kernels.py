@@ -256,15 +256,26 @@ def test_errors_raise_without_launch(dev):
 
 
 def test_small_batch_scan_bit_identical_to_batched(dev):
-    """B<=2 runs the direct (HBM-streaming) scan, 3..8 the 4-wave doc-interleaved
-    LDS scan with 2 queries per wave, 9..16 with 4, and larger B the 8-wave one:
-    same bits."""
-    docs, doclens, Q = make_case(123, 900, 20, 32)
+    """B<=2 runs the direct (HBM-streaming) scan; larger B the doc-interleaved
+    LDS scan in the shape the cost model picks (4 waves x 2 or 4 queries, 8
+    waves x 4, over 1-8 query groups): same bits for every batch size, and the
+    same as the oracle, for bf16 and MXFP8."""
+    from hybrid_rag_colbertv2_amd.index import quantize_mxfp8
+    docs, doclens, Q = make_case(123, 900, 130, 32)
     ix = ColbertIndex(docs.to(dev), doclens.to(dev))
     full = ix.score(Q.to(dev))
-    for lo, hi in [(0, 1), (3, 5), (7, 10), (10, 14), (5, 6), (2, 14), (0, 16), (1, 18)]:
+    spans = [(0, 1), (3, 5), (7, 10), (10, 14), (5, 6), (2, 14), (0, 16), (1, 18), (0, 24), (3, 43), (0, 48),
+             (10, 90), (2, 98), (0, 130)]
+    for lo, hi in spans:
         part = ix.score(Q[lo:hi].to(dev))
         assert torch.equal(part, full[lo:hi]), (lo, hi)
+    ref = orc.maxsim(Q[:40].float().numpy(), docs.float().numpy(), doclens.numpy())
+    np.testing.assert_allclose(full[:40].cpu().numpy(), ref, atol=ATOL, rtol=0)
+    q8, s8 = quantize_mxfp8(docs.to(dev))
+    ix8 = ColbertIndex(q8, doclens.to(dev), scales=s8)
+    full8 = ix8.score(Q.to(dev))
+    for lo, hi in spans:
+        assert torch.equal(ix8.score(Q[lo:hi].to(dev)), full8[lo:hi]), ("mxfp8", lo, hi)
     s1, i1 = ix.search(Q[:1].to(dev), k=30)
     s, i = ix.search(Q.to(dev), k=30)
     assert torch.equal(i1[0], i[0]) and torch.equal(s1[0], s[0])

@@ -446,7 +446,7 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
                                                      variant - 10);  // iteration shapes, see scan_f8
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;
-  int64_t n_chunks = (cu_count(ix->device) + nq_groups - 1) / nq_groups;
+  int64_t n_chunks = cu_count(ix->device) / nq_groups;
   if (n_chunks > ix->n) n_chunks = ix->n;
   const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
