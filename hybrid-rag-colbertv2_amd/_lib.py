@@ -64,6 +64,11 @@ _SIGS = {
     "cbv2_index_file_write_host": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _p, _p, _p, _i64]),
     "cbv2_index_file_read_host": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _p, _p, _p]),
     "cbv2_index_writer_open": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_index_file_info_ld": (ctypes.c_int, [ctypes.c_char_p, _p, _p, _p, _p]),
+    "cbv2_index_file_write_ld": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _i32, _p, _p, _p, _i64, _p]),
+    "cbv2_index_file_write_host_ld": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _i32, _p, _p, _p, _i64]),
+    "cbv2_index_writer_open_ld": (ctypes.c_int, [ctypes.c_char_p, _i32, _i64, _i32, _i64,
+                                                 ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_index_writer_append": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i32, _p]),
     "cbv2_index_writer_count": (_i64, [_p]),
     "cbv2_index_writer_close": (ctypes.c_int, [_p]),

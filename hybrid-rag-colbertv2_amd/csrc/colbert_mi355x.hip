@@ -2415,7 +2415,7 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
-    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg) {
+    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld) {
   const int lane = threadIdx.x & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
@@ -2438,27 +2438,32 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
     float v = neg_inf();
     if (id >= 0 && loc >= 0 && loc < n) {
       int dl = doclens[loc];
-      dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-      const uint8_t* dh = hi + (size_t)loc * kDocBytes;
-      const uint8_t* dlo = lo + (size_t)loc * kDocBytes;
+      dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
       float m[2] = {neg_inf(), neg_inf()};
+      // long documents (ld > 128): 128-token blocks, the row maxima carried
+      for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {
+        const int dlb = dl - kLd * blk;
+        const size_t at = ((size_t)loc * ld + (size_t)kLd * blk) * kRowBytes;
+        const uint8_t* dh = hi + at;
+        const uint8_t* dlo = lo + at;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        bf16x8 ah[4][4], al[4][4];
+        for (int half = 0; half < 2; ++half) {
+          bf16x8 ah[4][4], al[4][4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int rt = 4 * half + t;
-          if (16 * rt < dl) {
-            gbl_afrag16(dh, rt, lane, ah[t]);
-            gbl_afrag16(dlo, rt, lane, al[t]);
+          for (int t = 0; t < 4; ++t) {
+            const int rt = 4 * half + t;
+            if (16 * rt < dlb) {
+              gbl_afrag16(dh, rt, lane, ah[t]);
+              gbl_afrag16(dlo, rt, lane, al[t]);
+            }
           }
-        }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int rt = 4 * half + t;
-          if (16 * rt < dl) {
-            const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-            tile16_x3(ah[t], al[t], qh, ql, init, m);
+          for (int t = 0; t < 4; ++t) {
+            const int rt = 4 * half + t;
+            if (16 * rt < dlb) {
+              const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+              tile16_x3(ah[t], al[t], qh, ql, init, m);
+            }
           }
         }
       }
@@ -2558,7 +2563,7 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
     const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int B, int lq,
     const int32_t* __restrict__ act, const int32_t* __restrict__ act_off, const int32_t* __restrict__ act_cnt,
     const int32_t* __restrict__ ctr, const int32_t* __restrict__ pair_b, const int32_t* __restrict__ pair_c,
-    float* __restrict__ F, int cap) {
+    float* __restrict__ F, int cap, int ld) {
   const int lane = threadIdx.x & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n_act = ctr[1];
@@ -2566,9 +2571,10 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
     const int64_t d = act[a];
     const int o = act_off[a], cnt = act_cnt[a];
     int dl = doclens[d];
-    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-    const uint8_t* dh = hi + (size_t)d * kDocBytes;
-    const uint8_t* dlo = lo + (size_t)d * kDocBytes;
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    const uint8_t* dh0 = hi + (size_t)d * ld * kRowBytes;
+    const uint8_t* dlo0 = lo + (size_t)d * ld * kRowBytes;
+    const int nblk = dl > kLd ? (dl + kLd - 1) / kLd : 1;   // long documents: 128-token blocks
     if constexpr (PAIR_OUTER) {
 #pragma unroll 1
       for (int p = 0; p < cnt; ++p) {
@@ -2577,23 +2583,28 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
         load_qfrag16(qhi, b, B, lq, lane, qh);
         load_qfrag16(qlo, b, B, lq, lane, ql);
         float m[2] = {neg_inf(), neg_inf()};
+        for (int blk = 0; blk < nblk; ++blk) {
+          const int dlb = dl - kLd * blk;
+          const uint8_t* dh = dh0 + (size_t)blk * kDocBytes;
+          const uint8_t* dlo = dlo0 + (size_t)blk * kDocBytes;
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          bf16x8 ah[4][4], al[4][4];
+          for (int half = 0; half < 2; ++half) {
+            bf16x8 ah[4][4], al[4][4];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int rt = 4 * half + t;
-            if (16 * rt < dl) {
-              gbl_afrag16(dh, rt, lane, ah[t]);
-              gbl_afrag16(dlo, rt, lane, al[t]);
+            for (int t = 0; t < 4; ++t) {
+              const int rt = 4 * half + t;
+              if (16 * rt < dlb) {
+                gbl_afrag16(dh, rt, lane, ah[t]);
+                gbl_afrag16(dlo, rt, lane, al[t]);
+              }
             }
-          }
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int rt = 4 * half + t;
-            if (16 * rt < dl) {
-              const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-              tile16_x3(ah[t], al[t], qh, ql, init, m);
+            for (int t = 0; t < 4; ++t) {
+              const int rt = 4 * half + t;
+              if (16 * rt < dlb) {
+                const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+                tile16_x3(ah[t], al[t], qh, ql, init, m);
+              }
             }
           }
         }
@@ -2607,13 +2618,17 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
       float m[kDocPairs][2];
 #pragma unroll
       for (int q = 0; q < kDocPairs; ++q) m[q][0] = m[q][1] = neg_inf();
+      for (int blk = 0; blk < nblk; ++blk)
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
+        const int dlb = dl - kLd * blk;
+        const uint8_t* dh = dh0 + (size_t)blk * kDocBytes;
+        const uint8_t* dlo = dlo0 + (size_t)blk * kDocBytes;
         bf16x8 ah[4][4], al[4][4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int rt = 4 * half + t;
-          if (16 * rt < dl) {
+          if (16 * rt < dlb) {
             gbl_afrag16(dh, rt, lane, ah[t]);
             gbl_afrag16(dlo, rt, lane, al[t]);
           }
@@ -2628,8 +2643,8 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int rt = 4 * half + t;
-            if (16 * rt < dl) {
-              const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+            if (16 * rt < dlb) {
+              const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
               tile16_x3(ah[t], al[t], qh, ql, init, mm);
             }
           }
@@ -3613,7 +3628,7 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
   gx = gx < 1024 ? gx : 1024;
   hipLaunchKernelGGL(rescore_x3_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, st, ix->tokens, ix->resid,
                      ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out,
-                     only_neg);
+                     only_neg, (int)ix->ld);
   return launch_check("rescore_x3_kernel");
 }
 }  // namespace
@@ -3911,7 +3926,6 @@ int cbv2_split_f32(const float* x, int64_t rows, int32_t ld, const int32_t* docl
 int cbv2_index_attach_residual(cbv2_index* ix, const void* lo, float resid_max, float norm_max) {
   CBV2_REQUIRE(ix != nullptr, "null index");
   CBV2_REQUIRE(ix->dtype == CBV2_DTYPE_BF16, "a residual attaches to a bf16 index");
-  CBV2_REQUIRE(ix->ld == kLd, "the fp32-faithful index holds docs of 128 token slots (ld %d)", (int)ix->ld);
   CBV2_REQUIRE(ix->n == 0 || (lo != nullptr && aligned16(lo)), "residual must be non-null and 16-byte aligned");
   CBV2_REQUIRE(resid_max >= 0.0f && norm_max >= 0.0f && resid_max < 3.0e38f && norm_max < 3.0e38f,
                "bounds must be finite and >= 0");
@@ -4006,10 +4020,12 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
     const unsigned gr = (unsigned)(2 * cu_count(ix->device) * 4);   // 4 waves each; grid-stride over docs
     if (ix->band_doc_major == 2)
       hipLaunchKernelGGL(rescore_docs_kernel<true>, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
-                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
+                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap,
+                         (int)ix->ld);
     else
       hipLaunchKernelGGL(rescore_docs_kernel<false>, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
-                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
+                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap,
+                         (int)ix->ld);
     if ((rc = launch_check("rescore_docs_kernel"))) return rc;
   } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) {
     return rc;

@@ -11,6 +11,9 @@
 //   tokens_off         [n][ld][d] bf16 (2 B) or e4m3 (1 B)         4 KiB-aligned
 //   scales_off         [n][ld][2] E8M0 bytes (MXFP8 only)            4 KiB-aligned
 //
+// ld = 128 token slots per doc, or 256 / 512 / 1024 for long documents (bf16:
+// the layouts the kernels scan).
+//
 // A rank loads docs [begin, end) of the file: three contiguous byte ranges.
 // Reads go through two pinned staging buffers: a reader thread fills one with
 // pread (O_DIRECT for the 4 KiB-aligned token range, so a cold load is not
@@ -43,7 +46,7 @@ struct cbv2_file_header {
   uint32_t version;    // 1
   int32_t dtype;       // CBV2_DTYPE_BF16 or CBV2_DTYPE_MXFP8
   int64_t n;           // docs in the file
-  int32_t ld, d;       // 128, 128
+  int32_t ld, d;       // token slots per doc (128, or 256 / 512 / 1024 for bf16), 128
   int64_t id_base;     // global id of the file's doc 0
   uint64_t doclens_off, tokens_off, scales_off;  // scales_off 0 for bf16
   uint64_t file_bytes;
@@ -62,23 +65,28 @@ int err(int code, const char* fmt, ...) {
 
 uint64_t up(uint64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 size_t tok_bytes(int32_t dtype) { return dtype == CBV2_DTYPE_MXFP8 ? 1 : 2; }
+// bytes of one doc's tokens / scales
+size_t doc_bytes(const cbv2_file_header& h) { return (size_t)h.ld * 128 * tok_bytes(h.dtype); }
+size_t scale_bytes(const cbv2_file_header& h) { return h.scales_off ? (size_t)h.ld * 2 : 0; }
 
-int layout(int32_t dtype, int64_t n, int64_t id_base, cbv2_file_header& h) {
+int layout(int32_t dtype, int64_t n, int32_t ld, int64_t id_base, cbv2_file_header& h) {
   if (dtype != CBV2_DTYPE_BF16 && dtype != CBV2_DTYPE_MXFP8) return err(CBV2_EINVAL, "dtype %d not storable", dtype);
   if (n < 0 || id_base < 0) return err(CBV2_EINVAL, "bad n / id_base");
+  if (ld != 128 && (dtype != CBV2_DTYPE_BF16 || (ld != 256 && ld != 512 && ld != 1024)))
+    return err(CBV2_EINVAL, "ld %d not storable (128; bf16 also 256 / 512 / 1024)", ld);
   memset(&h, 0, sizeof(h));
   memcpy(h.magic, kMagic, 8);
   h.version = 1;
   h.dtype = dtype;
   h.n = n;
-  h.ld = 128;
+  h.ld = ld;
   h.d = 128;
   h.id_base = id_base;
   h.doclens_off = kAlign;
   h.tokens_off = up(h.doclens_off + 4ull * n);
-  const uint64_t tok_end = h.tokens_off + (uint64_t)n * 128 * 128 * tok_bytes(dtype);
+  const uint64_t tok_end = h.tokens_off + (uint64_t)n * doc_bytes(h);
   h.scales_off = dtype == CBV2_DTYPE_MXFP8 ? up(tok_end) : 0;
-  h.file_bytes = dtype == CBV2_DTYPE_MXFP8 ? h.scales_off + (uint64_t)n * 256 : tok_end;
+  h.file_bytes = dtype == CBV2_DTYPE_MXFP8 ? h.scales_off + (uint64_t)n * scale_bytes(h) : tok_end;
   return CBV2_OK;
 }
 
@@ -86,8 +94,8 @@ int read_header(int fd, const char* path, cbv2_file_header& h) {
   if (pread(fd, &h, sizeof(h), 0) != (ssize_t)sizeof(h)) return err(CBV2_EINVAL, "%s: short header", path);
   if (memcmp(h.magic, kMagic, 8) != 0 || h.version != 1) return err(CBV2_EINVAL, "%s: not a cbv2 index file", path);
   cbv2_file_header want;
-  if (layout(h.dtype, h.n, h.id_base, want) != CBV2_OK || want.tokens_off != h.tokens_off ||
-      want.scales_off != h.scales_off || h.ld != 128 || h.d != 128)
+  if (layout(h.dtype, h.n, h.ld, h.id_base, want) != CBV2_OK || want.tokens_off != h.tokens_off ||
+      want.scales_off != h.scales_off || h.d != 128)
     return err(CBV2_EINVAL, "%s: inconsistent header", path);
   struct stat st;
   if (fstat(fd, &st) != 0 || (uint64_t)st.st_size < h.file_bytes) return err(CBV2_EINVAL, "%s: truncated", path);
@@ -241,6 +249,10 @@ int check_range(const cbv2_file_header& h, int64_t begin, int64_t end) {
 extern "C" {
 
 int cbv2_index_file_info(const char* path, int32_t* dtype, int64_t* n, int64_t* id_base) {
+  return cbv2_index_file_info_ld(path, dtype, n, id_base, nullptr);
+}
+
+int cbv2_index_file_info_ld(const char* path, int32_t* dtype, int64_t* n, int64_t* id_base, int32_t* ld) {
   if (!path) return err(CBV2_EINVAL, "null path");
   Fd f;
   f.fd = open(path, O_RDONLY);
@@ -250,21 +262,27 @@ int cbv2_index_file_info(const char* path, int32_t* dtype, int64_t* n, int64_t* 
   if (dtype) *dtype = h.dtype;
   if (n) *n = h.n;
   if (id_base) *id_base = h.id_base;
+  if (ld) *ld = h.ld;
   return CBV2_OK;
 }
 
 int cbv2_index_file_write_host(const char* path, int32_t dtype, int64_t n, const void* tokens, const void* scales,
                                const int32_t* doclens, int64_t id_base) {
+  return cbv2_index_file_write_host_ld(path, dtype, n, 128, tokens, scales, doclens, id_base);
+}
+
+int cbv2_index_file_write_host_ld(const char* path, int32_t dtype, int64_t n, int32_t ld, const void* tokens,
+                                  const void* scales, const int32_t* doclens, int64_t id_base) {
   cbv2_file_header h;
-  if (int rc = layout(dtype, n, id_base, h)) return rc;
+  if (int rc = layout(dtype, n, ld, id_base, h)) return rc;
   if (!path || (n > 0 && (!tokens || !doclens || (dtype == CBV2_DTYPE_MXFP8 && !scales))))
     return err(CBV2_EINVAL, "null pointer");
   Fd f;
   f.fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
   if (f.fd < 0) return err(CBV2_EINVAL, "%s: cannot create (%s)", path, strerror(errno));
   if (pwrite_full(f.fd, &h, sizeof(h), 0) || (n && pwrite_full(f.fd, doclens, 4ull * n, h.doclens_off)) ||
-      (n && pwrite_full(f.fd, tokens, (size_t)n * 128 * 128 * tok_bytes(dtype), h.tokens_off)) ||
-      (n && h.scales_off && pwrite_full(f.fd, scales, (size_t)n * 256, h.scales_off)) ||
+      (n && pwrite_full(f.fd, tokens, (size_t)n * doc_bytes(h), h.tokens_off)) ||
+      (n && h.scales_off && pwrite_full(f.fd, scales, (size_t)n * scale_bytes(h), h.scales_off)) ||
       ftruncate(f.fd, (off_t)h.file_bytes) != 0)
     return err(CBV2_EINVAL, "%s: write failed (%s)", path, strerror(errno));
   return CBV2_OK;
@@ -282,18 +300,23 @@ int cbv2_index_file_read_host(const char* path, int64_t begin, int64_t end, void
   const int64_t m = end - begin;
   if (m == 0) return CBV2_OK;
   if (!tokens || !doclens || (h.scales_off && !scales)) return err(CBV2_EINVAL, "null output");
-  const size_t per = 128 * 128 * tok_bytes(h.dtype);
+  const size_t per = doc_bytes(h), sper = scale_bytes(h);
   if (pread_full(f.fd, doclens, 4ull * m, h.doclens_off + 4ull * begin) ||
       pread_full(f.fd, tokens, per * m, h.tokens_off + per * begin) ||
-      (h.scales_off && pread_full(f.fd, scales, 256ull * m, h.scales_off + 256ull * begin)))
+      (h.scales_off && pread_full(f.fd, scales, sper * m, h.scales_off + sper * begin)))
     return err(CBV2_EINVAL, "%s: read failed", path);
   return CBV2_OK;
 }
 
 int cbv2_index_file_write(const char* path, int32_t dtype, int64_t n, const void* tokens, const void* scales,
                           const int32_t* doclens, int64_t id_base, void* stream) {
+  return cbv2_index_file_write_ld(path, dtype, n, 128, tokens, scales, doclens, id_base, stream);
+}
+
+int cbv2_index_file_write_ld(const char* path, int32_t dtype, int64_t n, int32_t ld, const void* tokens,
+                             const void* scales, const int32_t* doclens, int64_t id_base, void* stream) {
   cbv2_file_header h;
-  if (int rc = layout(dtype, n, id_base, h)) return rc;
+  if (int rc = layout(dtype, n, ld, id_base, h)) return rc;
   if (!path || (n > 0 && (!tokens || !doclens || (dtype == CBV2_DTYPE_MXFP8 && !scales))))
     return err(CBV2_EINVAL, "null pointer");
   Fd f;
@@ -304,11 +327,12 @@ int cbv2_index_file_write(const char* path, int32_t dtype, int64_t n, const void
   if (int rc = pin.alloc()) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (int rc = range_from_device(path, f.fd, h.doclens_off, 4ull * n, (const uint8_t*)doclens, pin.p, st)) return rc;
-  if (int rc = range_from_device(path, f.fd, h.tokens_off, (size_t)n * 128 * 128 * tok_bytes(dtype),
-                                 (const uint8_t*)tokens, pin.p, st))
+  if (int rc = range_from_device(path, f.fd, h.tokens_off, (size_t)n * doc_bytes(h), (const uint8_t*)tokens, pin.p,
+                                 st))
     return rc;
   if (h.scales_off)
-    if (int rc = range_from_device(path, f.fd, h.scales_off, (size_t)n * 256, (const uint8_t*)scales, pin.p, st))
+    if (int rc = range_from_device(path, f.fd, h.scales_off, (size_t)n * scale_bytes(h), (const uint8_t*)scales,
+                                   pin.p, st))
       return rc;
   if (ftruncate(f.fd, (off_t)h.file_bytes) != 0) return err(CBV2_EINVAL, "%s: truncate failed", path);
   return CBV2_OK;
@@ -330,13 +354,13 @@ int cbv2_index_file_read(const char* path, int64_t begin, int64_t end, void* tok
   Pinned pin;
   if (int rc = pin.alloc()) return rc;
   hipStream_t st = (hipStream_t)stream;
-  const size_t per = 128 * 128 * tok_bytes(h.dtype);
+  const size_t per = doc_bytes(h), sper = scale_bytes(h);
   if (int rc = range_to_device(path, f.fd, -1, h.doclens_off + 4ull * begin, 4ull * m, (uint8_t*)doclens, pin.p, st))
     return rc;
   if (int rc = range_to_device(path, f.fd, fdir.fd, h.tokens_off + per * begin, per * m, (uint8_t*)tokens, pin.p, st))
     return rc;
   if (h.scales_off)
-    if (int rc = range_to_device(path, f.fd, -1, h.scales_off + 256ull * begin, 256ull * m, (uint8_t*)scales, pin.p,
+    if (int rc = range_to_device(path, f.fd, -1, h.scales_off + sper * begin, sper * m, (uint8_t*)scales, pin.p,
                                  st))
       return rc;
   return CBV2_OK;
@@ -357,11 +381,16 @@ struct cbv2_index_writer {
 };
 
 int cbv2_index_writer_open(const char* path, int32_t dtype, int64_t n, int64_t id_base, cbv2_index_writer** out) {
+  return cbv2_index_writer_open_ld(path, dtype, n, 128, id_base, out);
+}
+
+int cbv2_index_writer_open_ld(const char* path, int32_t dtype, int64_t n, int32_t ld, int64_t id_base,
+                              cbv2_index_writer** out) {
   if (!out) return err(CBV2_EINVAL, "null output handle pointer");
   *out = nullptr;
   if (!path || strlen(path) >= 1024) return err(CBV2_EINVAL, "bad path");
   auto* w = new cbv2_index_writer;
-  if (int rc = layout(dtype, n, id_base, w->h)) {
+  if (int rc = layout(dtype, n, ld, id_base, w->h)) {
     delete w;
     return rc;
   }
@@ -392,7 +421,7 @@ int cbv2_index_writer_append(cbv2_index_writer* w, int64_t count, const void* to
   if (count == 0) return CBV2_OK;
   const bool fp8 = w->h.scales_off != 0;
   if (!tokens || !doclens || (fp8 && !scales)) return err(CBV2_EINVAL, "null pointer");
-  const size_t per = 128 * 128 * tok_bytes(w->h.dtype);
+  const size_t per = doc_bytes(w->h), sper = scale_bytes(w->h);
   const uint64_t d0 = (uint64_t)w->written;
   if (on_device) {
     if (!w->pinned) {
@@ -407,12 +436,12 @@ int cbv2_index_writer_append(cbv2_index_writer* w, int64_t count, const void* to
                                    w->pin.p, st))
       return rc;
     if (fp8)
-      if (int rc = range_from_device(w->path, w->fd, w->h.scales_off + 256 * d0, 256ull * count,
+      if (int rc = range_from_device(w->path, w->fd, w->h.scales_off + sper * d0, sper * count,
                                      (const uint8_t*)scales, w->pin.p, st))
         return rc;
   } else if (pwrite_full(w->fd, doclens, 4ull * count, w->h.doclens_off + 4 * d0) ||
              pwrite_full(w->fd, tokens, per * count, w->h.tokens_off + per * d0) ||
-             (fp8 && pwrite_full(w->fd, scales, 256ull * count, w->h.scales_off + 256 * d0))) {
+             (fp8 && pwrite_full(w->fd, scales, sper * count, w->h.scales_off + sper * d0))) {
     return err(CBV2_EINVAL, "%s: write failed (%s)", w->path, strerror(errno));
   }
   w->written += count;

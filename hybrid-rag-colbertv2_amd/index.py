@@ -11,7 +11,7 @@ the MI355X scan kernel:
                                   rows >= doclen are padding)
     doclens  int32 [n]
     means    f32  [n, 128]       (optional: literal-reference scorer only)
-    residual bf16 [n, 128, 128]  (optional: fp32-faithful index, lo = bf16(x - tokens))
+    residual bf16 [n, ld, 128]   (optional: fp32-faithful index, lo = bf16(x - tokens))
 
 All compute goes through libcolbert_mi355x.so (``_lib``); the tensors are
 owned here and borrowed by the C handle.
@@ -125,7 +125,7 @@ class ColbertIndex:
         _require_cuda(doclens, "doclens")
         self.fp8 = tokens.dtype == torch.uint8
         want = torch.uint8 if self.fp8 else torch.bfloat16
-        lds = (LD,) if self.fp8 or residual is not None else LONG_LDS
+        lds = (LD,) if self.fp8 else LONG_LDS
         if tokens.dtype != want or tokens.dim() != 3 or tokens.shape[2] != DIM or tokens.shape[1] not in lds:
             raise ValueError(f"tokens must be bf16 [n, ld, {DIM}] (ld in {LONG_LDS}) or MXFP8 uint8 "
                              f"[n, {LD}, {DIM}] (got {tokens.dtype} {tuple(tokens.shape)})")
@@ -159,7 +159,8 @@ class ColbertIndex:
         if residual is not None:
             if self.fp8 or residual.dtype != torch.bfloat16 or residual.shape != self.tokens.shape \
                     or residual.device != self.device or bounds is None:
-                raise ValueError("a residual is bf16 [n, 128, 128] on the index device, with (resid_max, norm_max)")
+                raise ValueError("a residual is bf16 [n, ld, 128] like the tokens, on the index device, "
+                                 "with (resid_max, norm_max)")
             self.residual = residual.contiguous()
             self.bounds = (float(bounds[0]), float(bounds[1]))
             _lib.check(_lib.lib().cbv2_index_attach_residual(self._h, self.residual.data_ptr(), self.bounds[0],
@@ -172,12 +173,14 @@ class ColbertIndex:
 
     @classmethod
     def faithful_f32(cls, tokens_f32: torch.Tensor, doclens: torch.Tensor, id_base: int = 0) -> "ColbertIndex":
-        """Index fp32 [n, 128, 128] device tokens (as the reference stores them) so that
-        scores match fp32 arithmetic within ~1e-5: hi = bf16(x) is scanned, lo =
-        bf16(x - hi) is gathered for the candidates (cbv2_split_f32, HIP)."""
+        """Index fp32 [n, ld, 128] device tokens (as the reference stores them; ld =
+        128, or 256 / 512 / 1024 for long documents) so that scores match fp32
+        arithmetic within ~1e-5: hi = bf16(x) is scanned, lo = bf16(x - hi) is
+        gathered for the candidates (cbv2_split_f32, HIP)."""
         _require_cuda(tokens_f32, "tokens_f32")
-        if tokens_f32.dtype != torch.float32 or tokens_f32.dim() != 3 or tuple(tokens_f32.shape[1:]) != (LD, DIM):
-            raise ValueError(f"tokens_f32 must be f32 [n, {LD}, {DIM}] (got {tokens_f32.dtype} "
+        if tokens_f32.dtype != torch.float32 or tokens_f32.dim() != 3 or tokens_f32.shape[2] != DIM \
+                or tokens_f32.shape[1] not in LONG_LDS:
+            raise ValueError(f"tokens_f32 must be f32 [n, ld, {DIM}], ld in {LONG_LDS} (got {tokens_f32.dtype} "
                              f"{tuple(tokens_f32.shape)})")
         x = tokens_f32.contiguous()
         hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
@@ -187,8 +190,8 @@ class ColbertIndex:
         if doclens.dtype != torch.int32 or doclens.shape != (x.shape[0],):
             raise ValueError("doclens must be int32 [n]")
         doclens = doclens.contiguous()
-        _lib.check(_lib.lib().cbv2_split_f32(x.data_ptr(), x.numel() // DIM, LD, doclens.data_ptr(), hi.data_ptr(),
-                                             lo.data_ptr(), bounds.data_ptr(), _stream_ptr(x.device)))
+        _lib.check(_lib.lib().cbv2_split_f32(x.data_ptr(), x.numel() // DIM, x.shape[1], doclens.data_ptr(),
+                                             hi.data_ptr(), lo.data_ptr(), bounds.data_ptr(), _stream_ptr(x.device)))
         b = bounds.tolist()  # synchronises: x may be freed after this
         return cls(hi, doclens, id_base=id_base, residual=lo, bounds=(b[0], b[1]))
 
@@ -212,8 +215,8 @@ class ColbertIndex:
         device = torch.device(device)
         if dtype not in ("bf16", "fp8", "fp32"):
             raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
-        # bf16 indexes take long documents (ld = 256 / 512 / 1024); MXFP8 and fp32-faithful hold 128 slots
-        tokens, doclens = pack_tokens(embs, device, ld=None if dtype == "bf16" else LD,
+        # bf16 and fp32-faithful indexes take long documents (ld = 256 / 512 / 1024); MXFP8 holds 128 slots
+        tokens, doclens = pack_tokens(embs, device, ld=LD if dtype == "fp8" else None,
                                       dtype=torch.float32 if dtype == "fp32" else torch.bfloat16)
         if dtype == "fp32":
             ix = cls.faithful_f32(tokens, doclens, id_base=id_base)
@@ -241,17 +244,17 @@ class ColbertIndex:
         An fp32-faithful index is two bf16 files of the same layout -- ``path``
         (hi, the tokens every scan reads) and ``path + ".resid"`` (lo) -- plus
         ``path + ".bounds.json"`` (the split's bounds), so a rank loads its doc
-        range of both exactly as for a bf16 index."""
-        if self.ld != LD:
-            raise ValueError(f"the native file holds docs of {LD} token slots (this index: {self.ld})")
+        range of both exactly as for a bf16 index.  Long-document indexes keep
+        their ld (the file header records it)."""
         dt = _lib.DTYPE_MXFP8 if self.fp8 else _lib.DTYPE_BF16
         torch.cuda.current_stream(self.device).synchronize()
-        _lib.check(_lib.lib().cbv2_index_file_write(
-            os.fsencode(path), dt, self.n, self.tokens.data_ptr(), self.scales.data_ptr() if self.fp8 else None,
-            self.doclens.data_ptr(), self.id_base, _stream_ptr(self.device)))
+        _lib.check(_lib.lib().cbv2_index_file_write_ld(
+            os.fsencode(path), dt, self.n, self.ld, self.tokens.data_ptr(),
+            self.scales.data_ptr() if self.fp8 else None, self.doclens.data_ptr(), self.id_base,
+            _stream_ptr(self.device)))
         if self.faithful:
-            _lib.check(_lib.lib().cbv2_index_file_write(
-                os.fsencode(path + ".resid"), _lib.DTYPE_BF16, self.n, self.residual.data_ptr(), None,
+            _lib.check(_lib.lib().cbv2_index_file_write_ld(
+                os.fsencode(path + ".resid"), _lib.DTYPE_BF16, self.n, self.ld, self.residual.data_ptr(), None,
                 self.doclens.data_ptr(), self.id_base, _stream_ptr(self.device)))
             with open(path + ".bounds.json", "w") as f:
                 json.dump({"resid_max": self.bounds[0], "norm_max": self.bounds[1]}, f)
@@ -261,15 +264,15 @@ class ColbertIndex:
         """Load docs [begin, end) of a native index file straight into HBM
         (a rank's shard); global ids start at the file's id_base + begin."""
         device = torch.device(device)
-        dt, n, id_base = index_file_info(path)
+        dt, n, id_base, ld = index_file_layout(path)
         end = n if end is None else int(end)
         begin = int(begin)
         m = end - begin
         if begin < 0 or m < 0 or end > n:
             raise ValueError(f"doc range [{begin}, {end}) outside [0, {n})")
         fp8 = dt == _lib.DTYPE_MXFP8
-        tokens = torch.empty((m, LD, DIM), dtype=torch.uint8 if fp8 else torch.bfloat16, device=device)
-        scales = torch.empty((m, LD, 2), dtype=torch.uint8, device=device) if fp8 else None
+        tokens = torch.empty((m, ld, DIM), dtype=torch.uint8 if fp8 else torch.bfloat16, device=device)
+        scales = torch.empty((m, ld, 2), dtype=torch.uint8, device=device) if fp8 else None
         doclens = torch.empty((m,), dtype=torch.int32, device=device)
         with torch.cuda.device(device):
             _lib.check(_lib.lib().cbv2_index_file_read(
@@ -278,7 +281,9 @@ class ColbertIndex:
                 _stream_ptr(device)))
         if not fp8 and os.path.exists(path + ".resid") and os.path.exists(path + ".bounds.json"):
             # fp32-faithful: the residual file's same doc range, and the split's bounds
-            resid = torch.empty((m, LD, DIM), dtype=torch.bfloat16, device=device)
+            if index_file_layout(path + ".resid")[1:] != (n, id_base, ld):
+                raise ValueError(f"{path}.resid does not match {path}")
+            resid = torch.empty((m, ld, DIM), dtype=torch.bfloat16, device=device)
             dl2 = torch.empty((m,), dtype=torch.int32, device=device)
             with torch.cuda.device(device):
                 _lib.check(_lib.lib().cbv2_index_file_read(
@@ -502,9 +507,10 @@ class ColbertIndex:
 
 
 # --------------------------------------------------------------------- bounded-memory ingest
-def _as_batch(embs, device, dtype):
-    """Encoder output of one batch -> (tokens ``dtype`` [m, 128, 128], int32 doclens [m]) on ``device``."""
-    return pack_tokens(embs, device, dtype=dtype)
+def _as_batch(embs, device, dtype, ld=LD):
+    """Encoder output of one batch -> (tokens ``dtype`` [m, ld, 128], int32 doclens [m]) on ``device``
+    (ld=None: the smallest of LONG_LDS that holds the batch's longest doc)."""
+    return pack_tokens(embs, device, ld=ld, dtype=dtype)
 
 
 class IndexBuilder:
@@ -514,12 +520,21 @@ class IndexBuilder:
     encoder output is packed on the GPU and written into preallocated shard
     tensors: cast to bf16, quantised to MXFP8 by the HIP quantizer, or split
     into bf16 hi/lo by cbv2_split_f32 (fp32-faithful; the residual bounds
-    accumulate over the batches).  ``finish()`` returns the ColbertIndex."""
+    accumulate over the batches).  ``finish()`` returns the ColbertIndex.
 
-    def __init__(self, n: int, device="cuda", dtype: str = "bf16", id_base: int = 0):
+    Long documents (bf16 and fp32-faithful): with ``ld=None`` the slot count
+    starts at 128 and grows to 256 / 512 / 1024 when a batch holds a longer
+    doc (the docs so far are re-laid on the GPU); a fixed ``ld`` rejects
+    longer docs.  MXFP8 holds 128 slots."""
+
+    def __init__(self, n: int, device="cuda", dtype: str = "bf16", id_base: int = 0, ld: Optional[int] = None):
         if dtype not in ("bf16", "fp8", "fp32"):
             raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
+        if ld is not None and (ld not in LONG_LDS or (dtype == "fp8" and ld != LD)):
+            raise ValueError(f"ld must be one of {LONG_LDS} ({LD} for fp8; got {ld})")
         self.n, self.dtype, self.id_base = int(n), dtype, int(id_base)
+        self.grow = ld is None and dtype != "fp8"
+        self.ld = LD if ld is None else int(ld)
         self.device = torch.device(device)
         self.pos = 0
         self.doclens = torch.zeros((self.n,), dtype=torch.int32, device=self.device)
@@ -527,19 +542,35 @@ class IndexBuilder:
             self.tokens = torch.empty((self.n, LD, DIM), dtype=torch.uint8, device=self.device)
             self.scales = torch.empty((self.n, LD, 2), dtype=torch.uint8, device=self.device)
         else:
-            self.tokens = torch.empty((self.n, LD, DIM), dtype=torch.bfloat16, device=self.device)
+            self.tokens = torch.zeros((self.n, self.ld, DIM), dtype=torch.bfloat16, device=self.device)
             self.scales = None
         if dtype == "fp32":
-            self.residual = torch.empty((self.n, LD, DIM), dtype=torch.bfloat16, device=self.device)
+            self.residual = torch.zeros((self.n, self.ld, DIM), dtype=torch.bfloat16, device=self.device)
             self.bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
+
+    def _relayout(self, ld: int) -> None:
+        """Grow every doc to ld token slots (padding rows zero, never scored)."""
+        def grown(x):
+            y = torch.zeros((self.n, ld, DIM), dtype=x.dtype, device=self.device)
+            y[: self.pos, : self.ld] = x[: self.pos]
+            return y
+        self.tokens = grown(self.tokens)
+        if self.dtype == "fp32":
+            self.residual = grown(self.residual)
+        self.ld = ld
 
     def append(self, embs) -> int:
         """Add the next batch of encoder output (dense [m, L, D], pooled [m, D] or a list
         of [L_i, D]); returns the number of docs added."""
-        t, dl = _as_batch(embs, self.device, torch.float32 if self.dtype == "fp32" else torch.bfloat16)
+        t, dl = _as_batch(embs, self.device, torch.float32 if self.dtype == "fp32" else torch.bfloat16,
+                          ld=None if self.grow else self.ld)
         m = int(t.shape[0])
         if self.pos + m > self.n:
             raise ValueError(f"batch of {m} docs past the declared {self.n} (have {self.pos})")
+        if int(t.shape[1]) > self.ld:
+            self._relayout(int(t.shape[1]))
+        if int(t.shape[1]) < self.ld:     # a batch of shorter docs: pad to the index's slots
+            t = torch.nn.functional.pad(t, (0, 0, 0, self.ld - int(t.shape[1])))
         a, b = self.pos, self.pos + m
         self.doclens[a:b] = dl
         if self.dtype == "fp8":
@@ -549,7 +580,7 @@ class IndexBuilder:
         elif self.dtype == "fp32":
             t = t.contiguous()
             hi, lo = self.tokens[a:b], self.residual[a:b]
-            _lib.check(_lib.lib().cbv2_split_f32(t.data_ptr(), m * LD, LD, self.doclens[a:b].data_ptr(),
+            _lib.check(_lib.lib().cbv2_split_f32(t.data_ptr(), m * self.ld, self.ld, self.doclens[a:b].data_ptr(),
                                                  hi.data_ptr(), lo.data_ptr(), self.bounds.data_ptr(),
                                                  _stream_ptr(self.device)))
         else:
@@ -573,16 +604,21 @@ class IndexWriter:
     for corpora larger than HBM: each batch is cast (bf16) or quantised
     (MXFP8, HIP) on the GPU and written through two 64 MiB pinned buffers, so
     host memory does not grow with the corpus.  The file is valid only after
-    ``close()`` with every declared doc written."""
+    ``close()`` with every declared doc written.  ``ld``: token slots per doc
+    (fixed up front, as the file's layout depends on it; bf16 long documents
+    256 / 512 / 1024)."""
 
-    def __init__(self, path: str, n: int, dtype: str = "bf16", id_base: int = 0, device="cuda"):
+    def __init__(self, path: str, n: int, dtype: str = "bf16", id_base: int = 0, device="cuda", ld: int = LD):
         if dtype not in ("bf16", "fp8"):
             raise ValueError("the native file holds bf16 or MXFP8 tokens")
-        self.path, self.n, self.dtype = path, int(n), dtype
+        if ld not in LONG_LDS or (dtype == "fp8" and ld != LD):
+            raise ValueError(f"ld must be one of {LONG_LDS} ({LD} for fp8; got {ld})")
+        self.path, self.n, self.dtype, self.ld = path, int(n), dtype, int(ld)
         self.device = torch.device(device)
         h = ctypes.c_void_p()
-        _lib.check(_lib.lib().cbv2_index_writer_open(os.fsencode(path), _lib.DTYPE_MXFP8 if dtype == "fp8"
-                                                     else _lib.DTYPE_BF16, self.n, int(id_base), ctypes.byref(h)))
+        _lib.check(_lib.lib().cbv2_index_writer_open_ld(os.fsencode(path), _lib.DTYPE_MXFP8 if dtype == "fp8"
+                                                        else _lib.DTYPE_BF16, self.n, self.ld, int(id_base),
+                                                        ctypes.byref(h)))
         self._h = h
 
     @property
@@ -590,7 +626,7 @@ class IndexWriter:
         return int(_lib.lib().cbv2_index_writer_count(self._h))
 
     def append(self, embs) -> int:
-        t, dl = _as_batch(embs, self.device, torch.bfloat16)
+        t, dl = _as_batch(embs, self.device, torch.bfloat16, ld=self.ld)
         m = int(t.shape[0])
         sc = None
         if self.dtype == "fp8":
@@ -626,6 +662,14 @@ def index_file_info(path: str):
     _lib.check(_lib.lib().cbv2_index_file_info(os.fsencode(path), ctypes.byref(dt), ctypes.byref(n),
                                                ctypes.byref(base)))
     return int(dt.value), int(n.value), int(base.value)
+
+
+def index_file_layout(path: str):
+    """(ABI dtype, doc count, id_base, token slots per doc) of a native index file."""
+    dt, n, base, ld = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+    _lib.check(_lib.lib().cbv2_index_file_info_ld(os.fsencode(path), ctypes.byref(dt), ctypes.byref(n),
+                                                  ctypes.byref(base), ctypes.byref(ld)))
+    return int(dt.value), int(n.value), int(base.value), int(ld.value)
 
 
 def select_topk(scores: torch.Tensor, k: int, ids: Optional[torch.Tensor] = None):

@@ -27,8 +27,9 @@
  * Index layout in HBM (see DESIGN.md "Data layout"):
  *    tokens   bf16 [n][ld][d = 128], row-major, 16-byte aligned; ld = 128
  *             token slots (every path), or 256 / 512 / 1024 for long
- *             documents (bf16 MaxSim scan, search and rerank; the MXFP8 and
- *             fp32-faithful indexes and the native file hold ld = 128);
+ *             documents (bf16 MaxSim scan, search and rerank, the
+ *             fp32-faithful index and the native file; the MXFP8 index
+ *             holds ld = 128);
  *             rows t >= doclens[i] of doc i are padding and never score.
  *    doclens  int32 [n], 0 <= doclens[i] <= ld.
  *    Local doc i has global id  id_base + i  (contiguous shard of the corpus).
@@ -314,18 +315,26 @@ int cbv2_stem_en(const char* words, const int64_t* offsets, int64_t n, char* out
 /* Native index file (replaces the torch.save/torch.load of
  * indexes/colbert/index.pt at local_rag_complete.py:743-746, 751 for large
  * corpora — the index.pt reader stays in Python).  One flat file: a 4 KiB
- * header, int32 doclens [n], tokens [n][128][128] (bf16, or e4m3 bytes) and,
- * for MXFP8, E8M0 scales [n][128][2]; each section 4 KiB-aligned.
+ * header, int32 doclens [n], tokens [n][ld][128] (bf16, or e4m3 bytes) and,
+ * for MXFP8, E8M0 scales [n][ld][2]; each section 4 KiB-aligned.  ld = 128
+ * token slots (the functions without _ld), or 256 / 512 / 1024 for a bf16
+ * long-document index (the _ld variants); readers take ld from the header.
  * cbv2_index_file_write  — DEVICE pointers (an HBM-resident index), D2H in
  *                          64 MiB pinned chunks overlapped with pwrite.
  * cbv2_index_file_read   — docs [begin, end) into DEVICE buffers (tokens
- *                          (end-begin)*128*128*elem bytes, scales, doclens):
+ *                          (end-begin)*ld*128*elem bytes, scales, doclens):
  *                          pread (O_DIRECT where aligned) into two pinned
  *                          buffers overlapped with H2D copies on `stream`;
  *                          returns when the data is in HBM.
- * cbv2_index_file_info   — dtype, doc count and id_base of a file.
+ * cbv2_index_file_info   — dtype, doc count and id_base of a file
+ *                          (cbv2_index_file_info_ld: and its ld).
  * *_host variants: HOST pointers, no GPU involved.                          */
 int cbv2_index_file_info(const char* path, int32_t* dtype, int64_t* n, int64_t* id_base);
+int cbv2_index_file_info_ld(const char* path, int32_t* dtype, int64_t* n, int64_t* id_base, int32_t* ld);
+int cbv2_index_file_write_ld(const char* path, int32_t dtype, int64_t n, int32_t ld, const void* tokens,
+                             const void* scales, const int32_t* doclens, int64_t id_base, void* stream);
+int cbv2_index_file_write_host_ld(const char* path, int32_t dtype, int64_t n, int32_t ld, const void* tokens,
+                                  const void* scales, const int32_t* doclens, int64_t id_base);
 int cbv2_index_file_write(const char* path, int32_t dtype, int64_t n, const void* tokens, const void* scales,
                           const int32_t* doclens, int64_t id_base, void* stream);
 int cbv2_index_file_read(const char* path, int64_t begin, int64_t end, void* tokens, void* scales, int32_t* doclens,
@@ -343,6 +352,8 @@ int cbv2_index_file_read_host(const char* path, int64_t begin, int64_t end, void
  * Host memory is two staging buffers whatever the corpus size.             */
 typedef struct cbv2_index_writer cbv2_index_writer;
 int cbv2_index_writer_open(const char* path, int32_t dtype, int64_t n, int64_t id_base, cbv2_index_writer** out);
+int cbv2_index_writer_open_ld(const char* path, int32_t dtype, int64_t n, int32_t ld, int64_t id_base,
+                              cbv2_index_writer** out);
 int cbv2_index_writer_append(cbv2_index_writer* w, int64_t count, const void* tokens, const void* scales,
                              const int32_t* doclens, int32_t on_device, void* stream);
 int64_t cbv2_index_writer_count(const cbv2_index_writer* w);

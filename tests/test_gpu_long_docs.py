@@ -105,3 +105,83 @@ def test_from_embeddings_picks_long_ld(dev):
     np.testing.assert_allclose(ix.score(Q.to(dev)).cpu().numpy(), ref, atol=ATOL, rtol=0)
     with pytest.raises(ValueError):
         ColbertIndex.from_embeddings(embs, device=dev, dtype="fp8")   # MXFP8 holds 128 slots
+
+
+def make_f32_case(seed, N, ld, B):
+    """fp32 docs of up to ld tokens (the reference keeps fp32 encoder output,
+    LRC:735-746) with 3 planted docs per query whose best-matching tokens sit
+    past token 128."""
+    g = torch.Generator().manual_seed(seed)
+    docs = rand_unit(g, N, ld, 128)
+    doclens = torch.randint(0, ld + 1, (N,), generator=g, dtype=torch.int32)
+    doclens[:5] = torch.tensor([0, 1, 128, 129, ld], dtype=torch.int32)
+    Q = rand_unit(g, B, 32, 128)
+    for b in range(B):
+        for j in range(3):
+            d = 5 + (97 * b + 31 * j) % (N - 5)
+            docs[d, ld - 40: ld - 8] = Q[b] + 0.2 * rand_unit(g, 32, 128)
+            doclens[d] = ld
+    return docs, doclens, Q
+
+
+@pytest.mark.parametrize("ld,N", [(256, 2500), (512, 1200)])
+def test_faithful_long_docs(dev, ld, N):
+    """fp32-faithful index of long documents: scores within 1e-4 of the fp64
+    oracle of the fp32 values, the certified band search, doc-major ==
+    pair-major rescoring bit for bit, rerank."""
+    from _parity import assert_ids_match_separated
+    from hybrid_rag_colbertv2_amd import _lib
+    B, k = 5, 50
+    docs, doclens, Q = make_f32_case(ld + N, N, ld, B)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=7)
+    assert ix.ld == ld and ix.faithful
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    got = ix.score(Q.to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(exact))
+    fin = np.isfinite(exact)
+    np.testing.assert_allclose(got[fin], exact[fin], atol=1e-4, rtol=0)
+    s, i = ix.search(Q.to(dev), k)
+    assert (ix.last_band.cpu().numpy() >= k).all()
+    rs, ri = orc.topk(exact, k, id_base=7)
+    np.testing.assert_allclose(s.cpu().numpy(), rs, atol=1e-4, rtol=0)
+    assert_ranking_consistent(i.cpu().numpy(), exact, 1e-4, id_base=7)
+    assert_ids_match_separated(i.cpu().numpy(), ri, rs, 1e-4, min_frac=0.02)
+    planted = {(b, 5 + (97 * b + 31 * j) % (N - 5) + 7) for b in range(B) for j in range(3)}
+    assert planted <= {(b, int(x)) for b in range(B) for x in i[b, :3].cpu()}
+    ix.set_option(_lib.OPT_BAND_DOC_MAJOR, 0)
+    s0, i0 = ix.search(Q.to(dev), k)
+    assert torch.equal(s0, s) and torch.equal(i0, i)
+    cand = torch.from_numpy(np.random.default_rng(ld).integers(0, N, size=(B, 40)).astype(np.int32) + 7)
+    cs, ci, cp = ix.rerank(Q.to(dev), cand.to(dev), 10)
+    es, ei, ep = orc.rerank(Q.numpy(), docs.numpy(), doclens.numpy(), cand.numpy(), 10, id_base=7)
+    np.testing.assert_allclose(cs.cpu().numpy(), es, atol=1e-4, rtol=0)
+    assert_ids_match_separated(ci.cpu().numpy(), ei, es, 1e-4)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_long_docs_native_file_and_builder(dev, tmp_path, dtype):
+    """A long-document index (bf16, or fp32-faithful: hi + residual files)
+    through the native file (whole and by doc range) scores bit-identically;
+    IndexBuilder grows its token slots 128 -> 512 when a later batch holds a
+    longer doc and equals from_embeddings of the whole list."""
+    from hybrid_rag_colbertv2_amd.index import IndexBuilder, index_file_layout
+    g = torch.Generator().manual_seed(11)
+    lens = [int(x) for x in torch.randint(1, 129, (300,), generator=g)] + [300, 17, 512, 90] + [5] * 40
+    embs = [rand_unit(g, L, 128) for L in lens]
+    Q = rand_unit(g, 3, 32, 128).to(dev)
+    Qs = Q if dtype == "fp32" else Q.bfloat16()
+    ix = ColbertIndex.from_embeddings(embs, device=dev, dtype=dtype, id_base=100)
+    assert ix.ld == 512
+    ref = ix.score(Qs)
+    b = IndexBuilder(len(embs), device=dev, dtype=dtype, id_base=100)
+    for a in range(0, len(embs), 150):
+        b.append(embs[a:a + 150])
+    bx = b.finish()
+    assert bx.ld == 512 and torch.equal(bx.score(Qs), ref)
+    path = str(tmp_path / "long.cbv2")
+    ix.save(path)
+    assert index_file_layout(path)[1:] == (len(embs), 100, 512)
+    assert torch.equal(ColbertIndex.load(path, device=dev).score(Qs), ref)
+    part = ColbertIndex.load(path, device=dev, begin=290, end=310)
+    assert part.id_base == 390 and part.faithful == (dtype == "fp32")
+    assert torch.equal(part.score(Qs), ref[:, 290:310])

@@ -126,3 +126,40 @@ def test_streaming_writer_incomplete_file_is_invalid(tmp_path):
     from hybrid_rag_colbertv2_amd.index import index_file_info
     with pytest.raises(ValueError):
         index_file_info(path)
+
+
+@pytest.mark.parametrize("ld", [256, 1024])
+def test_long_document_file(tmp_path, ld):
+    """bf16 long-document files (ld = 256 / 512 / 1024 token slots, the layout
+    of a long-document index): the header records ld, ranges read back exactly,
+    the streaming writer gives the same bytes; MXFP8 and other ld are refused."""
+    import ctypes
+    L = _lib()
+    from hybrid_rag_colbertv2_amd.index import index_file_info, index_file_layout
+    rng = np.random.default_rng(ld)
+    n = 9
+    tokens = rng.integers(0, 65535, size=(n, ld, 128)).astype(np.uint16)
+    doclens = rng.integers(0, ld + 1, size=n).astype(np.int32)
+    path, streamed = str(tmp_path / "long.cbv2"), str(tmp_path / "long_s.cbv2")
+    L.check(L.lib().cbv2_index_file_write_host_ld(os.fsencode(path), L.DTYPE_BF16, n, ld, tokens.ctypes.data, None,
+                                                  doclens.ctypes.data, 40))
+    assert index_file_layout(path) == (L.DTYPE_BF16, n, 40, ld)
+    assert index_file_info(path) == (L.DTYPE_BF16, n, 40)
+    assert os.path.getsize(path) == 8192 + n * ld * 256
+    for a, b in [(0, n), (3, 7), (8, 9)]:
+        tok = np.zeros((b - a, ld, 128), np.uint16)
+        dl = np.zeros(b - a, np.int32)
+        L.check(L.lib().cbv2_index_file_read_host(os.fsencode(path), a, b, tok.ctypes.data, None, dl.ctypes.data))
+        assert np.array_equal(tok, tokens[a:b]) and np.array_equal(dl, doclens[a:b])
+    h = ctypes.c_void_p()
+    L.check(L.lib().cbv2_index_writer_open_ld(os.fsencode(streamed), L.DTYPE_BF16, n, ld, 40, ctypes.byref(h)))
+    for a, b in [(0, 4), (4, 9)]:
+        t, d = np.ascontiguousarray(tokens[a:b]), np.ascontiguousarray(doclens[a:b])
+        L.check(L.lib().cbv2_index_writer_append(h, b - a, t.ctypes.data, None, d.ctypes.data, 0, None))
+    L.check(L.lib().cbv2_index_writer_close(h))
+    assert open(path, "rb").read() == open(streamed, "rb").read()
+    for dt, bad_ld in [(L.DTYPE_MXFP8, ld), (L.DTYPE_BF16, 384), (L.DTYPE_BF16, 64)]:
+        with pytest.raises(ValueError):
+            L.check(L.lib().cbv2_index_file_write_host_ld(os.fsencode(str(tmp_path / "x.cbv2")), dt, n, bad_ld,
+                                                          tokens.ctypes.data, tokens.ctypes.data,
+                                                          doclens.ctypes.data, 0))
