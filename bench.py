@@ -304,18 +304,20 @@ def main():
     sorted_ok = bool((torch.diff(fs, dim=1) <= 0).all().item())
 
     # ---- p50 / p99 latency at batch 1 (whole hot path, one query)
-    lat = []
-    for it in range(args.p50_iters + 3):
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t = time.perf_counter()
-        step(searcher, Q1, bm_one)
-        torch.cuda.synchronize()
-        if it >= 3:
-            lat.append((time.perf_counter() - t) * 1e3)
-    p50 = statistics.median(lat) if lat else None
-    p99 = float(np.percentile(lat, 99)) if lat else None
+    def latency(srch, Qb):
+        lat = []
+        for it in range(args.p50_iters + 3):
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t = time.perf_counter()
+            step(srch, Qb, bm_one)
+            torch.cuda.synchronize()
+            if it >= 3:
+                lat.append((time.perf_counter() - t) * 1e3)
+        return lat, (statistics.median(lat) if lat else None), (float(np.percentile(lat, 99)) if lat else None)
+
+    lat, p50, p99 = latency(searcher, Q1)
     bm_ms = []
     for _ in range(3):                                  # stage 1 alone (host), for the record
         t = time.perf_counter()
@@ -405,10 +407,13 @@ def main():
         ffs, ffi = fouts[-1]
         ffi_h = ffi.cpu().numpy()
         bs = fix.last_band.float()
+        _, fp50, fp99 = latency(fsearch, Qf32[:1].contiguous())
         fbad = spot_check(ffs, ffi_h, Qf32.cpu().numpy(), lambda sel: f32[sel].cpu().numpy(), begin, end,
                           check_rows, 1e-4, world, dev)
         fleg = {"value": round(B * args.steps / fel, 2), "ms_per_step": round(fel / args.steps * 1e3, 3),
                 "scan_avg_ms": round(sum(fscan) / len(fscan), 3) if fscan else None,
+                "p50_ms_b1": round(fp50, 3) if fp50 is not None else None,
+                "p99_ms_b1": round(fp99, 3) if fp99 is not None else None,
                 "band": {"mean": round(float(bs.mean()), 1), "max": int(bs.max()),
                          "overflow_rows": int((bs < 0).sum())},
                 "tolerance": 1e-4, "oracle_mismatch_queries": fbad,

@@ -1486,7 +1486,7 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
 }
 
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
-          int FK = 0>
+          int FK = 0, int LD = kLd>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1495,7 +1495,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kDim;                 // e4m3 bytes per iteration
   constexpr int kIterStage = kIterBytes + 4 * TPI * 2;        // + 2 scale bytes per row
-  constexpr int IPG = kLd / TPI;
+  // LD token slots per doc (128; 256 / 512 / 1024 for long documents: a doc
+  // group then spans LD / TPI iterations, the row maxima carried across them)
+  static_assert(LD % TPI == 0 && LD >= 128 && LD <= 1024, "LD: 128, 256, 512 or 1024 token slots");
+  constexpr int IPG = LD / TPI;
+  constexpr size_t kDocStride = (size_t)LD * kDim, kScaleStride = (size_t)LD * 2;
   constexpr int kScaleDma = 4 * TPI * 2 / 256;                // 256-B scale DMAs per iteration
   constexpr int kPieces = kIterBytes / 1024;
   constexpr int kPiecesPerWave = kPieces / WAVES;
@@ -1546,13 +1550,13 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       const int R = 8 * piece + (lane >> 3);
       const uint32_t off = (R % TPI) * kDim + 16 * ((lane & 7) ^ swz_f8<TPI>(R));
       const int d = clamp_doc(4 * G + 8 * piece / TPI);
-      const uint8_t* src = tokens + (size_t)(d_begin + d) * kF8DocBytes + (size_t)j * TPI * kDim + off;
+      const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kDim + off;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + piece * 1024), 16, 0, 0);
     }
     if (wave < kScaleDma) {  // scale bytes b = 256 * wave + 4L: row b/2 = TPI * doc + token
       const int R = (256 * wave + 4 * lane) / 2;
       const int d = clamp_doc(4 * G + R / TPI);
-      const uint8_t* src = tscales + (size_t)(d_begin + d) * kF8ScaleBytes + (size_t)(j * TPI + R % TPI) * 2;
+      const uint8_t* src = tscales + (size_t)(d_begin + d) * kScaleStride + (size_t)(j * TPI + R % TPI) * 2;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + kIterBytes + 256 * wave), 4, 0, 0);
     }
   };
@@ -1593,7 +1597,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const int v = (4 * G + x < nd) ? doclens[d_begin + 4 * G + x] : 0;
-        dl4[x] = v < 0 ? 0 : (v > kLd ? kLd : v);
+        dl4[x] = v < 0 ? 0 : (v > LD ? LD : v);
       }
       dl_min = min(min(dl4[0], dl4[1]), min(dl4[2], dl4[3]));
       dl_max = max(max(dl4[0], dl4[1]), max(dl4[2], dl4[3]));
@@ -1656,11 +1660,14 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
 }
 
 // Small-batch f8 scan: one doc chunk per wave, docs streamed to VGPRs.
-template <int QW>
+// LONG: docs of ld = 256 / 512 / 1024 token slots, 128 tokens at a time with
+// the row maxima carried (same tile order: a doc of <= 128 tokens scores the
+// same bits whatever ld).
+template <int QW, bool LONG = false>
 __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
-    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs) {
+    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int ld = kLd) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
@@ -1679,24 +1686,28 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
   float sc[QW];
 #pragma unroll
   for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+  const int lmax = LONG ? ld : kLd;
   for (int i = 0; i < nd; ++i) {
     int dl = doclens[d_begin + i];
-    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-    const uint8_t* dbase = tokens + (size_t)(d_begin + i) * kF8DocBytes;
-    const uint8_t* dsc = tscales + (size_t)(d_begin + i) * kF8ScaleBytes;
-    i32x8 af[kLd / 16];
-    int as[kLd / 16];
-#pragma unroll
-    for (int rt = 0; rt < kLd / 16; ++rt)
-      if (16 * rt < dl) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+    dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
     float m[QW][2];
 #pragma unroll
     for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {   // one block unless LONG
+      const int dlb = dl - kLd * blk;
+      const uint8_t* dbase = tokens + ((size_t)(d_begin + i) * lmax + (size_t)kLd * blk) * kDim;
+      const uint8_t* dsc = tscales + ((size_t)(d_begin + i) * lmax + (size_t)kLd * blk) * 2;
+      i32x8 af[kLd / 16];
+      int as[kLd / 16];
 #pragma unroll
-    for (int rt = 0; rt < kLd / 16; ++rt) {
-      if (16 * rt < dl) {
-        const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-        tile_f8<QW>(af[rt], as[rt], qa, qs, init, m);
+      for (int rt = 0; rt < kLd / 16; ++rt)
+        if (16 * rt < dlb) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+#pragma unroll
+      for (int rt = 0; rt < kLd / 16; ++rt) {
+        if (16 * rt < dlb) {
+          const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+          tile_f8<QW>(af[rt], as[rt], qa, qs, init, m);
+        }
       }
     }
 #pragma unroll
@@ -2243,7 +2254,7 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, int64_t id_base, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int lq,
     const int32_t* __restrict__ cand, int C, int k, float* __restrict__ out_s, int32_t* __restrict__ out_i,
-    int32_t* __restrict__ out_p) {
+    int32_t* __restrict__ out_p, int ld) {
   extern __shared__ float sc_dyn[];
   __shared__ float sc_fix[BIG ? 1 : kSmallMax];
   __shared__ uint64_t keys[BIG ? kTopkMax : kSmallMax];
@@ -2264,20 +2275,23 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
     float v = neg_inf();
     if (id >= 0 && loc >= 0 && loc < n) {
       int dl = doclens[loc];
-      dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-      const uint8_t* dbase = tokens + (size_t)loc * kF8DocBytes;
-      const uint8_t* dsc = tscales + (size_t)loc * kF8ScaleBytes;
-      i32x8 af[kLd / 16];
-      int as[kLd / 16];
-#pragma unroll
-      for (int rt = 0; rt < kLd / 16; ++rt)
-        if (16 * rt < dl) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+      dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
       float m[1][2] = {{neg_inf(), neg_inf()}};
+      for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {   // long documents: 128-token blocks
+        const int dlb = dl - kLd * blk;
+        const uint8_t* dbase = tokens + ((size_t)loc * ld + (size_t)kLd * blk) * kDim;
+        const uint8_t* dsc = tscales + ((size_t)loc * ld + (size_t)kLd * blk) * 2;
+        i32x8 af[kLd / 16];
+        int as[kLd / 16];
 #pragma unroll
-      for (int rt = 0; rt < kLd / 16; ++rt) {
-        if (16 * rt < dl) {
-          const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
-          tile_f8<1>(af[rt], as[rt], qa, qs, init, m);
+        for (int rt = 0; rt < kLd / 16; ++rt)
+          if (16 * rt < dlb) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+#pragma unroll
+        for (int rt = 0; rt < kLd / 16; ++rt) {
+          if (16 * rt < dlb) {
+            const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+            tile_f8<1>(af[rt], as[rt], qa, qs, init, m);
+          }
         }
       }
       v = reduce16(m[0][0], m[0][1], lane, lq);
@@ -2410,7 +2424,10 @@ __device__ __forceinline__ void tile16_x3(const bf16x8 (&ah)[4], const bf16x8 (&
 // grid-stride over blockIdx.x; out[b*ld_out + c].  count (nullable) bounds c
 // per query (the band collected by the search); only_neg (nullable) skips
 // every query whose status is >= 0 (the search's full-scan fallback).
+// LONG: docs of ld = 256 / 512 / 1024 token slots (128-token blocks, the row
+// maxima carried); the 128-slot build keeps its single-block code.
 constexpr int kRsPerWave = 4;
+template <bool LONG = false>
 __global__ __launch_bounds__(256) void rescore_x3_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
@@ -2437,13 +2454,13 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
     const int64_t loc = id - id_base;
     float v = neg_inf();
     if (id >= 0 && loc >= 0 && loc < n) {
+      const int lmax = LONG ? ld : kLd;
       int dl = doclens[loc];
-      dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+      dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
       float m[2] = {neg_inf(), neg_inf()};
-      // long documents (ld > 128): 128-token blocks, the row maxima carried
-      for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {
+      for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {
         const int dlb = dl - kLd * blk;
-        const size_t at = ((size_t)loc * ld + (size_t)kLd * blk) * kRowBytes;
+        const size_t at = ((size_t)loc * lmax + (size_t)kLd * blk) * kRowBytes;
         const uint8_t* dh = hi + at;
         const uint8_t* dlo = lo + at;
 #pragma unroll
@@ -2557,7 +2574,7 @@ constexpr int kDocPairs = 4;   // pairs of one doc held per pass (their running 
 // fragments loaded once and the doc's tiles re-read per pair (cache-served
 // after the first); otherwise the doc's tiles are loaded once per half and
 // the query fragments re-read per pair and half.
-template <bool PAIR_OUTER = false>
+template <bool PAIR_OUTER = false, bool LONG = false>
 __global__ __launch_bounds__(256) void rescore_docs_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens,
     const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int B, int lq,
@@ -2570,11 +2587,12 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
   for (int a = blockIdx.x * 4 + wave; a < n_act; a += gridDim.x * 4) {   // one doc per wave
     const int64_t d = act[a];
     const int o = act_off[a], cnt = act_cnt[a];
+    const int lmax = LONG ? ld : kLd;
     int dl = doclens[d];
-    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
-    const uint8_t* dh0 = hi + (size_t)d * ld * kRowBytes;
-    const uint8_t* dlo0 = lo + (size_t)d * ld * kRowBytes;
-    const int nblk = dl > kLd ? (dl + kLd - 1) / kLd : 1;   // long documents: 128-token blocks
+    dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
+    const uint8_t* dh0 = hi + (size_t)d * lmax * kRowBytes;
+    const uint8_t* dlo0 = lo + (size_t)d * lmax * kRowBytes;
+    const int nblk = LONG && dl > kLd ? (dl + kLd - 1) / kLd : 1;   // long documents: 128-token blocks
     if constexpr (PAIR_OUTER) {
 #pragma unroll 1
       for (int p = 0; p < cnt; ++p) {
@@ -3328,7 +3346,7 @@ constexpr int kF8Waves = 8, kF8QW = 8;
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
-          int FK = 0>
+          int FK = 0, int LD = kLd>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -3341,7 +3359,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC, FK>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC, FK, LD>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3349,11 +3367,53 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
   return finish_split(ix, sp, st);
 }
 
+// MXFP8 long documents (index ld = 256 / 512 / 1024): B <= 2 the direct scan
+// in 128-token blocks; larger B the doc-interleaved scan with its doc group
+// spanning ld / 32 iterations (the row maxima carried across), B <= 8 in the
+// 4-wave x 2-query shape, two per CU, else the production 8 waves x 8 queries.
+template <int LD>
+int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
+                   hipStream_t st, int* ctr_ws) {
+  if (B <= kF8SmallMaxB)
+    return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, LD>(ix, Qb, Qs, B, lq, out, ld_out, st, kScanDynFrac,
+                                                       kScanTaskDocs, ctr_ws);
+  return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, LD>(ix, Qb, Qs, B, lq, out, ld_out, st, kScanDynFrac,
+                                                                kScanTaskDocs, ctr_ws);
+}
+
+int scan_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
+                 hipStream_t st, int* ctr_ws) {
+  if (B <= kF8DirectMaxB) {
+    constexpr int QW = 2;
+    const int nq_groups = (B + QW - 1) / QW;
+    int64_t n_chunks = 8LL * cu_count(ix->device) / nq_groups;
+    if (n_chunks > ix->n) n_chunks = ix->n;
+    if (n_chunks < 1) n_chunks = 1;
+    const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+    n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+    const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
+    hipLaunchKernelGGL((maxsim_scan_f8_direct_kernel<QW, true>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                       ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
+    return launch_check("maxsim_scan_f8_direct_kernel");
+  }
+  switch (ix->ld) {
+    case 256: return launch_f8_long<256>(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
+    case 512: return launch_f8_long<512>(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
+    case 1024: return launch_f8_long<1024>(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
+    default:
+      return fail(CBV2_EUNSUPPORTED, "index ld %d not built", (int)ix->ld);
+  }
+}
+
 int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
             float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, int shape = 0, int* ctr_ws = nullptr,
             FusedTopk* ft = nullptr) {
   if (ix->n == 0) return CBV2_OK;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+  if (ix->ld != kLd) {   // long documents: automatic shape only (B <= 8 direct, else 8 waves x 8 queries)
+    if (ft != nullptr || shape != 0) return fail(CBV2_EUNSUPPORTED, "long-doc index: automatic scan only");
+    return scan_f8_long(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
+  }
   if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
     return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st, dyn_frac,
                                                                       task_docs, ctr_ws, ft);
@@ -3626,7 +3686,8 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
   // at most 1024 workgroups per row (4096 waves: a lone fallback row still
   // streams at full rate), grid-stride beyond; rows that skip exit at once
   gx = gx < 1024 ? gx : 1024;
-  hipLaunchKernelGGL(rescore_x3_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, st, ix->tokens, ix->resid,
+  hipLaunchKernelGGL(ix->ld != kLd ? rescore_x3_kernel<true> : rescore_x3_kernel<false>, dim3((unsigned)gx, (unsigned)B),
+                     dim3(256), 0, st, ix->tokens, ix->resid,
                      ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out,
                      only_neg, (int)ix->ld);
   return launch_check("rescore_x3_kernel");
@@ -3672,8 +3733,9 @@ int cbv2_index_create_mxfp8(int device, const void* tokens, const void* scales, 
   *out = nullptr;
   CBV2_REQUIRE(n >= 0 && n <= 0x7fffffffLL, "n out of range (%lld)", (long long)n);
   CBV2_REQUIRE(id_base >= 0 && id_base + n <= 0x7fffffffLL, "global ids must fit int32");
-  if (ld != kLd || d != kDim)
-    return fail(CBV2_EUNSUPPORTED, "index geometry ld=%d d=%d not built (ld=128, d=128)", ld, d);
+  if ((ld != 128 && ld != 256 && ld != 512 && ld != 1024) || d != kDim)
+    return fail(CBV2_EUNSUPPORTED, "index geometry ld=%d d=%d not built (ld = 128, 256, 512 or 1024; d = 128)", ld,
+                d);
   if (n > 0) {
     CBV2_REQUIRE(tokens != nullptr && scales != nullptr && doclens != nullptr, "null tokens/scales/doclens");
     CBV2_REQUIRE(aligned16(tokens), "tokens must be 16-byte aligned");
@@ -3873,11 +3935,11 @@ int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int3
                                    (int)dyn));
       hipLaunchKernelGGL(rerank_f8_kernel<true>, dim3((unsigned)B), dim3(kRrWaves * 64), dyn, st, ix->tokens,
                          ix->scales, ix->doclens, ix->n, ix->id_base, Qb, Qs, lq, cand, C, k, out_scores, out_ids,
-                         out_pos);
+                         out_pos, (int)ix->ld);
     } else {
       hipLaunchKernelGGL(rerank_f8_kernel<false>, dim3((unsigned)B), dim3(kRrWaves * 64), 0, st, ix->tokens,
                          ix->scales, ix->doclens, ix->n, ix->id_base, Qb, Qs, lq, cand, C, k, out_scores, out_ids,
-                         out_pos);
+                         out_pos, (int)ix->ld);
     }
     return launch_check("rerank_f8_kernel");
   }
@@ -4018,14 +4080,10 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
                        ix->id_base, ix->n, w.dcnt, w.doff, w.pair_b, w.pair_c);
     if ((rc = launch_check("band_scatter_kernel"))) return rc;
     const unsigned gr = (unsigned)(2 * cu_count(ix->device) * 4);   // 4 waves each; grid-stride over docs
-    if (ix->band_doc_major == 2)
-      hipLaunchKernelGGL(rescore_docs_kernel<true>, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
-                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap,
-                         (int)ix->ld);
-    else
-      hipLaunchKernelGGL(rescore_docs_kernel<false>, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
-                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap,
-                         (int)ix->ld);
+    auto kern = ix->band_doc_major == 2 ? (ix->ld != kLd ? rescore_docs_kernel<true, true> : rescore_docs_kernel<true>)
+                                        : (ix->ld != kLd ? rescore_docs_kernel<false, true> : rescore_docs_kernel<false>);
+    hipLaunchKernelGGL(kern, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, w.qhi, w.qlo, B, lq,
+                       w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap, (int)ix->ld);
     if ((rc = launch_check("rescore_docs_kernel"))) return rc;
   } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) {
     return rc;

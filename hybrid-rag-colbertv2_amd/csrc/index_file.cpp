@@ -11,8 +11,8 @@
 //   tokens_off         [n][ld][d] bf16 (2 B) or e4m3 (1 B)         4 KiB-aligned
 //   scales_off         [n][ld][2] E8M0 bytes (MXFP8 only)            4 KiB-aligned
 //
-// ld = 128 token slots per doc, or 256 / 512 / 1024 for long documents (bf16:
-// the layouts the kernels scan).
+// ld = 128 token slots per doc, or 256 / 512 / 1024 for long documents (the
+// layouts the kernels scan).
 //
 // A rank loads docs [begin, end) of the file: three contiguous byte ranges.
 // Reads go through two pinned staging buffers: a reader thread fills one with
@@ -46,7 +46,7 @@ struct cbv2_file_header {
   uint32_t version;    // 1
   int32_t dtype;       // CBV2_DTYPE_BF16 or CBV2_DTYPE_MXFP8
   int64_t n;           // docs in the file
-  int32_t ld, d;       // token slots per doc (128, or 256 / 512 / 1024 for bf16), 128
+  int32_t ld, d;       // token slots per doc (128, or 256 / 512 / 1024), 128
   int64_t id_base;     // global id of the file's doc 0
   uint64_t doclens_off, tokens_off, scales_off;  // scales_off 0 for bf16
   uint64_t file_bytes;
@@ -72,8 +72,8 @@ size_t scale_bytes(const cbv2_file_header& h) { return h.scales_off ? (size_t)h.
 int layout(int32_t dtype, int64_t n, int32_t ld, int64_t id_base, cbv2_file_header& h) {
   if (dtype != CBV2_DTYPE_BF16 && dtype != CBV2_DTYPE_MXFP8) return err(CBV2_EINVAL, "dtype %d not storable", dtype);
   if (n < 0 || id_base < 0) return err(CBV2_EINVAL, "bad n / id_base");
-  if (ld != 128 && (dtype != CBV2_DTYPE_BF16 || (ld != 256 && ld != 512 && ld != 1024)))
-    return err(CBV2_EINVAL, "ld %d not storable (128; bf16 also 256 / 512 / 1024)", ld);
+  if (ld != 128 && ld != 256 && ld != 512 && ld != 1024)
+    return err(CBV2_EINVAL, "ld %d not storable (128, 256, 512 or 1024)", ld);
   memset(&h, 0, sizeof(h));
   memcpy(h.magic, kMagic, 8);
   h.version = 1;

@@ -7,7 +7,7 @@ is a contiguous id range ``[id_base, id_base + n)`` of the corpus laid out for
 the MI355X scan kernel:
 
     tokens   bf16 [n, ld, 128]   (ld = 128 token slots: 32 KiB per doc; long
-                                  documents: ld = 256 / 512 / 1024, bf16 only;
+                                  documents: ld = 256 / 512 / 1024;
                                   rows >= doclen are padding)
     doclens  int32 [n]
     means    f32  [n, 128]       (optional: literal-reference scorer only)
@@ -28,7 +28,7 @@ import torch
 from . import _lib
 
 LD = 128
-LONG_LDS = (128, 256, 512, 1024)   # token slots per doc a bf16 index can hold (long documents: bf16 MaxSim)
+LONG_LDS = (128, 256, 512, 1024)   # token slots per doc an index can hold (long documents)
 DIM = 128
 LQ_MAX = 32
 BAND_CAP = 16384   # fp32-faithful search: largest band rescored per query
@@ -115,8 +115,8 @@ class ColbertIndex:
     """One shard of the corpus resident in HBM, with a C handle borrowing it.
 
     bf16 tokens (default; [n, ld, 128] with ld = 128, or 256 / 512 / 1024 for
-    long documents), or MXFP8 (``tokens`` uint8 e4m3 [n, 128, 128] plus
-    ``scales`` uint8 E8M0 [n, 128, 2]; see ``ColbertIndex.mxfp8``)."""
+    long documents), or MXFP8 (``tokens`` uint8 e4m3 [n, ld, 128] plus
+    ``scales`` uint8 E8M0 [n, ld, 2]; see ``ColbertIndex.mxfp8``)."""
 
     def __init__(self, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0,
                  scales: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
@@ -125,16 +125,15 @@ class ColbertIndex:
         _require_cuda(doclens, "doclens")
         self.fp8 = tokens.dtype == torch.uint8
         want = torch.uint8 if self.fp8 else torch.bfloat16
-        lds = (LD,) if self.fp8 else LONG_LDS
-        if tokens.dtype != want or tokens.dim() != 3 or tokens.shape[2] != DIM or tokens.shape[1] not in lds:
-            raise ValueError(f"tokens must be bf16 [n, ld, {DIM}] (ld in {LONG_LDS}) or MXFP8 uint8 "
-                             f"[n, {LD}, {DIM}] (got {tokens.dtype} {tuple(tokens.shape)})")
+        if tokens.dtype != want or tokens.dim() != 3 or tokens.shape[2] != DIM or tokens.shape[1] not in LONG_LDS:
+            raise ValueError(f"tokens must be bf16 or MXFP8 uint8 [n, ld, {DIM}] (ld in {LONG_LDS}) "
+                             f"(got {tokens.dtype} {tuple(tokens.shape)})")
         self.ld = int(tokens.shape[1])
         if doclens.dtype != torch.int32 or doclens.shape != (tokens.shape[0],):
             raise ValueError("doclens must be int32 [n]")
         if self.fp8 and (scales is None or scales.dtype != torch.uint8
-                         or tuple(scales.shape) != (tokens.shape[0], LD, 2)):
-            raise ValueError("an MXFP8 index needs uint8 scales [n, 128, 2]")
+                         or tuple(scales.shape) != (tokens.shape[0], tokens.shape[1], 2)):
+            raise ValueError("an MXFP8 index needs uint8 scales [n, ld, 2]")
         self.tokens = tokens.contiguous()
         self.scales = scales.contiguous() if self.fp8 else None
         self.doclens = doclens.contiguous()
@@ -147,7 +146,7 @@ class ColbertIndex:
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         if self.fp8:
             _lib.check(_lib.lib().cbv2_index_create_mxfp8(
-                dev, self.tokens.data_ptr(), self.scales.data_ptr(), self.n, LD, DIM, self.doclens.data_ptr(),
+                dev, self.tokens.data_ptr(), self.scales.data_ptr(), self.n, self.ld, DIM, self.doclens.data_ptr(),
                 self.id_base, ctypes.byref(h)))
         else:
             _lib.check(_lib.lib().cbv2_index_create(
@@ -203,7 +202,7 @@ class ColbertIndex:
 
     @classmethod
     def mxfp8(cls, tokens: torch.Tensor, doclens: torch.Tensor, id_base: int = 0) -> "ColbertIndex":
-        """Quantize bf16/f32 [n, 128, 128] device tokens to MXFP8 (HIP kernel) and index them."""
+        """Quantize bf16/f32 [n, ld, 128] device tokens to MXFP8 (HIP kernel) and index them."""
         q, sc = quantize_mxfp8(tokens)
         return cls(q, doclens, id_base=id_base, scales=sc)
 
@@ -215,8 +214,8 @@ class ColbertIndex:
         device = torch.device(device)
         if dtype not in ("bf16", "fp8", "fp32"):
             raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
-        # bf16 and fp32-faithful indexes take long documents (ld = 256 / 512 / 1024); MXFP8 holds 128 slots
-        tokens, doclens = pack_tokens(embs, device, ld=LD if dtype == "fp8" else None,
+        # long documents: the smallest ld of 256 / 512 / 1024 that holds the longest doc
+        tokens, doclens = pack_tokens(embs, device, ld=None,
                                       dtype=torch.float32 if dtype == "fp32" else torch.bfloat16)
         if dtype == "fp32":
             ix = cls.faithful_f32(tokens, doclens, id_base=id_base)
@@ -522,25 +521,24 @@ class IndexBuilder:
     into bf16 hi/lo by cbv2_split_f32 (fp32-faithful; the residual bounds
     accumulate over the batches).  ``finish()`` returns the ColbertIndex.
 
-    Long documents (bf16 and fp32-faithful): with ``ld=None`` the slot count
-    starts at 128 and grows to 256 / 512 / 1024 when a batch holds a longer
-    doc (the docs so far are re-laid on the GPU); a fixed ``ld`` rejects
-    longer docs.  MXFP8 holds 128 slots."""
+    Long documents: with ``ld=None`` the slot count starts at 128 and grows to
+    256 / 512 / 1024 when a batch holds a longer doc (the docs so far are
+    re-laid on the GPU); a fixed ``ld`` rejects longer docs."""
 
     def __init__(self, n: int, device="cuda", dtype: str = "bf16", id_base: int = 0, ld: Optional[int] = None):
         if dtype not in ("bf16", "fp8", "fp32"):
             raise ValueError(f"index dtype must be bf16, fp8 or fp32 (got {dtype!r})")
-        if ld is not None and (ld not in LONG_LDS or (dtype == "fp8" and ld != LD)):
-            raise ValueError(f"ld must be one of {LONG_LDS} ({LD} for fp8; got {ld})")
+        if ld is not None and ld not in LONG_LDS:
+            raise ValueError(f"ld must be one of {LONG_LDS} (got {ld})")
         self.n, self.dtype, self.id_base = int(n), dtype, int(id_base)
-        self.grow = ld is None and dtype != "fp8"
+        self.grow = ld is None
         self.ld = LD if ld is None else int(ld)
         self.device = torch.device(device)
         self.pos = 0
         self.doclens = torch.zeros((self.n,), dtype=torch.int32, device=self.device)
-        if dtype == "fp8":
-            self.tokens = torch.empty((self.n, LD, DIM), dtype=torch.uint8, device=self.device)
-            self.scales = torch.empty((self.n, LD, 2), dtype=torch.uint8, device=self.device)
+        if dtype == "fp8":     # padding rows: e4m3 zeros, scale 2^0 (never scored)
+            self.tokens = torch.zeros((self.n, self.ld, DIM), dtype=torch.uint8, device=self.device)
+            self.scales = torch.full((self.n, self.ld, 2), 127, dtype=torch.uint8, device=self.device)
         else:
             self.tokens = torch.zeros((self.n, self.ld, DIM), dtype=torch.bfloat16, device=self.device)
             self.scales = None
@@ -550,13 +548,15 @@ class IndexBuilder:
 
     def _relayout(self, ld: int) -> None:
         """Grow every doc to ld token slots (padding rows zero, never scored)."""
-        def grown(x):
-            y = torch.zeros((self.n, ld, DIM), dtype=x.dtype, device=self.device)
+        def grown(x, fill=0):
+            y = torch.full((self.n, ld, x.shape[2]), fill, dtype=x.dtype, device=self.device)
             y[: self.pos, : self.ld] = x[: self.pos]
             return y
         self.tokens = grown(self.tokens)
         if self.dtype == "fp32":
             self.residual = grown(self.residual)
+        if self.dtype == "fp8":
+            self.scales = grown(self.scales, 127)
         self.ld = ld
 
     def append(self, embs) -> int:
@@ -605,14 +605,14 @@ class IndexWriter:
     (MXFP8, HIP) on the GPU and written through two 64 MiB pinned buffers, so
     host memory does not grow with the corpus.  The file is valid only after
     ``close()`` with every declared doc written.  ``ld``: token slots per doc
-    (fixed up front, as the file's layout depends on it; bf16 long documents
-    256 / 512 / 1024)."""
+    (fixed up front, as the file's layout depends on it; long documents 256 /
+    512 / 1024)."""
 
     def __init__(self, path: str, n: int, dtype: str = "bf16", id_base: int = 0, device="cuda", ld: int = LD):
         if dtype not in ("bf16", "fp8"):
             raise ValueError("the native file holds bf16 or MXFP8 tokens")
-        if ld not in LONG_LDS or (dtype == "fp8" and ld != LD):
-            raise ValueError(f"ld must be one of {LONG_LDS} ({LD} for fp8; got {ld})")
+        if ld not in LONG_LDS:
+            raise ValueError(f"ld must be one of {LONG_LDS} (got {ld})")
         self.path, self.n, self.dtype, self.ld = path, int(n), dtype, int(ld)
         self.device = torch.device(device)
         h = ctypes.c_void_p()

@@ -27,9 +27,9 @@
  * Index layout in HBM (see DESIGN.md "Data layout"):
  *    tokens   bf16 [n][ld][d = 128], row-major, 16-byte aligned; ld = 128
  *             token slots (every path), or 256 / 512 / 1024 for long
- *             documents (bf16 MaxSim scan, search and rerank, the
- *             fp32-faithful index and the native file; the MXFP8 index
- *             holds ld = 128);
+ *             documents (bf16 and MXFP8 MaxSim scan, search and rerank, the
+ *             fp32-faithful index and the native file; scales of an MXFP8
+ *             index are [n][ld][2]);
  *             rows t >= doclens[i] of doc i are padding and never score.
  *    doclens  int32 [n], 0 <= doclens[i] <= ld.
  *    Local doc i has global id  id_base + i  (contiguous shard of the corpus).

@@ -103,8 +103,38 @@ def test_from_embeddings_picks_long_ld(dev):
         docs[i, : e.shape[0]] = e.bfloat16().float()
     ref = orc.maxsim(Q.bfloat16().float().numpy(), docs.numpy(), np.array([5, 130, 300, 64]))
     np.testing.assert_allclose(ix.score(Q.to(dev)).cpu().numpy(), ref, atol=ATOL, rtol=0)
-    with pytest.raises(ValueError):
-        ColbertIndex.from_embeddings(embs, device=dev, dtype="fp8")   # MXFP8 holds 128 slots
+    fx = ColbertIndex.from_embeddings(embs, device=dev, dtype="fp8")
+    assert fx.fp8 and fx.ld == 512 and tuple(fx.scales.shape) == (4, 512, 2)
+
+
+@pytest.mark.parametrize("ld,N", [(256, 2500), (1024, 400)])
+@pytest.mark.parametrize("B", [1, 5, 40])
+def test_mxfp8_long_docs(dev, ld, N, B):
+    """MXFP8 index of long documents: every scan shape (B=1 direct, B=5 the
+    4-wave x 2-query shape, B=40 8 waves x 8 queries) within 2e-3 of the
+    float64 oracle on the dequantised values; search = the oracle's selection
+    of the GPU's own scores; rerank raw scores = the scan's bits; docs of <=
+    128 tokens score as in a 128-slot MXFP8 index."""
+    from hybrid_rag_colbertv2_amd.index import quantize_mxfp8
+    docs, doclens, Q = make_case(ld * 7 + B, N, ld, B)
+    ix = ColbertIndex.mxfp8(docs.to(dev), doclens.to(dev), id_base=3)
+    assert ix.fp8 and ix.ld == ld
+    qq, qs = quantize_mxfp8(Q.to(dev))
+    Qd = orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy())
+    Dd = orc.mxfp8_dequant(ix.tokens.cpu().numpy(), ix.scales.cpu().numpy())
+    ref = orc.maxsim(Qd, Dd, doclens.numpy())
+    got = ix.score(Q.to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(got[fin], ref[fin], atol=2e-3, rtol=0)
+    s, i = ix.search(Q.to(dev), 50)
+    assert_selection_exact(i.cpu().numpy(), s.cpu().numpy(), got, 50, id_base=3)
+    cand = np.random.default_rng(ld + B).integers(0, N, size=(B, 60)).astype(np.int32) + 3
+    raw = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), 0).cpu().numpy()
+    np.testing.assert_array_equal(raw, got[np.arange(B)[:, None], cand - 3])
+    short = (doclens <= 128).nonzero().flatten()[:300]
+    sx = ColbertIndex.mxfp8(docs[short, :128].contiguous().to(dev), doclens[short].contiguous().to(dev))
+    assert np.array_equal(sx.score(Q.to(dev)).cpu().numpy(), got[:, short.numpy()])
 
 
 def make_f32_case(seed, N, ld, B):
@@ -158,7 +188,7 @@ def test_faithful_long_docs(dev, ld, N):
     assert_ids_match_separated(ci.cpu().numpy(), ei, es, 1e-4)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32", "fp8"])
 def test_long_docs_native_file_and_builder(dev, tmp_path, dtype):
     """A long-document index (bf16, or fp32-faithful: hi + residual files)
     through the native file (whole and by doc range) scores bit-identically;

@@ -36,7 +36,8 @@ def test_validation_errors_without_gpu(L):
     assert L.cbv2_index_create(0, None, 1, 10, 64, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
     assert L.cbv2_index_create(0, None, 1, 10, 200, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED  # long docs: 256/512/1024
     assert L.cbv2_index_create(0, None, 1, 10, 2048, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
-    assert L.cbv2_index_create_mxfp8(0, None, None, 10, 256, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
+    assert L.cbv2_index_create_mxfp8(0, None, None, 10, 384, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED
+    assert L.cbv2_index_create_mxfp8(0, None, None, 10, 256, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EINVAL  # null
     assert L.cbv2_index_create(0, None, 1, -1, 128, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EINVAL
     assert L.cbv2_index_create(0, None, 1, 10, 128, 128, None, 0, None) == _lib.ERR_EINVAL
     assert L.cbv2_topk_rows(None, 1, 10, 10, 5, 0, None, 0, None, None, None) == _lib.ERR_EINVAL

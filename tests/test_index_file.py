@@ -132,7 +132,8 @@ def test_streaming_writer_incomplete_file_is_invalid(tmp_path):
 def test_long_document_file(tmp_path, ld):
     """bf16 long-document files (ld = 256 / 512 / 1024 token slots, the layout
     of a long-document index): the header records ld, ranges read back exactly,
-    the streaming writer gives the same bytes; MXFP8 and other ld are refused."""
+    the streaming writer gives the same bytes; other ld are refused (MXFP8
+    long files: tests/test_gpu_long_docs.py)."""
     import ctypes
     L = _lib()
     from hybrid_rag_colbertv2_amd.index import index_file_info, index_file_layout
@@ -158,7 +159,7 @@ def test_long_document_file(tmp_path, ld):
         L.check(L.lib().cbv2_index_writer_append(h, b - a, t.ctypes.data, None, d.ctypes.data, 0, None))
     L.check(L.lib().cbv2_index_writer_close(h))
     assert open(path, "rb").read() == open(streamed, "rb").read()
-    for dt, bad_ld in [(L.DTYPE_MXFP8, ld), (L.DTYPE_BF16, 384), (L.DTYPE_BF16, 64)]:
+    for dt, bad_ld in [(L.DTYPE_MXFP8, 384), (L.DTYPE_BF16, 384), (L.DTYPE_BF16, 64)]:
         with pytest.raises(ValueError):
             L.check(L.lib().cbv2_index_file_write_host_ld(os.fsencode(str(tmp_path / "x.cbv2")), dt, n, bad_ld,
                                                           tokens.ctypes.data, tokens.ctypes.data,
