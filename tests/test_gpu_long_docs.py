@@ -215,3 +215,67 @@ def test_long_docs_native_file_and_builder(dev, tmp_path, dtype):
     part = ColbertIndex.load(path, device=dev, begin=290, end=310)
     assert part.id_base == 390 and part.faithful == (dtype == "fp32")
     assert torch.equal(part.score(Qs), ref[:, 290:310])
+
+
+class _LongChunkEncoder:
+    """Docs: one unit vector per word, no padding (chunks of 20-600 words, as
+    the reference's 256-1024-token chunks, LRC:63-64); queries: 32 rows
+    (words, then [PAD]<i> vectors) like Jina-ColBERT's query augmentation."""
+
+    def __init__(self):
+        from hybrid_rag_colbertv2_amd.encoder import FakeEncoder
+        self.fe = FakeEncoder(maxlen=32)
+
+    def encode(self, texts, convert_to_tensor=True, is_query=True, **_):
+        if is_query:
+            return self.fe.encode(texts, convert_to_tensor=True)
+        one = isinstance(texts, str)
+        out = [torch.from_numpy(np.stack([self.fe._vec(w) for w in t.lower().split()]))
+               for t in ([texts] if one else texts)]
+        return out[0] if one else out
+
+
+def test_long_chunks_end_to_end_default_config(dev, tmp_path):
+    """JinaColBERTRetriever with the DEFAULT config (fp32-faithful index) on
+    chunks of up to 600 tokens, ingested in batches (the builder grows to 1024
+    slots): search ids/scores vs the float64 oracle of the fp32 values (1e-4),
+    the text rerank API, and index.pt persistence reloading bit-identically."""
+    from hybrid_rag_colbertv2_amd import RAGConfig, JinaColBERTRetriever
+    rng = np.random.default_rng(5)
+    vocab = [f"w{i}" for i in range(400)]
+    lens = rng.integers(20, 200, size=60)
+    lens[[7, 33, 50]] = [600, 450, 300]
+    corpus = [" ".join(rng.choice(vocab, size=int(L))) for L in lens]
+    cfg = RAGConfig(colbert_index_path=str(tmp_path / "colbert"))
+    assert cfg.index_dtype == "fp32"
+    enc = _LongChunkEncoder()
+    r = JinaColBERTRetriever(cfg, encoder=enc)
+    r.index(corpus, batch_size=16)
+    ix = r.corpus_embeddings
+    assert ix.faithful and ix.ld == 1024 and ix.doclens.cpu().tolist() == [int(x) for x in lens]
+    docs = np.zeros((60, 1024, 128), np.float32)
+    for i, e in enumerate(enc.encode(corpus, is_query=False)):
+        docs[i, : e.shape[0]] = e.numpy()
+    queries = [" ".join(rng.choice(vocab, size=6)) for _ in range(4)] + [corpus[7][:60]]
+    for q in queries:
+        qe = enc.encode(q).numpy()[None]
+        s = orc.maxsim(qe, docs, lens)
+        es, ei = orc.topk(s, 10)
+        got = r.search(q, k=10)
+        np.testing.assert_allclose([g["score"] for g in got], es[0], atol=1e-4, rtol=0)
+        sep = np.abs(np.diff(es[0])) > 1e-4
+        for j, g in enumerate(got):
+            if (j == 0 or sep[j - 1]) and (j == 9 or sep[j]):
+                assert g["document_id"] == int(ei[0, j]), (q, j)
+        assert got[0]["text"] == corpus[got[0]["document_id"]]
+    cand = [3, 7, 50, 12]
+    rr = r.rerank(queries[-1], [corpus[i] for i in cand], k=4)
+    s_c = orc.maxsim(enc.encode(queries[-1]).numpy()[None], docs[cand], lens[cand])[0]
+    np.testing.assert_allclose([x["score"] for x in rr], np.sort(s_c)[::-1], atol=1e-4, rtol=0)
+    assert [x["rank"] for x in rr] == [1, 2, 3, 4]
+    assert rr[0]["result_index"] == int(np.argmax(s_c))
+    ref = r.corpus_embeddings.score(torch.from_numpy(enc.encode(queries[0]).numpy()).to(dev))
+    r2 = JinaColBERTRetriever(cfg, encoder=enc)
+    r2.load()
+    assert r2.corpus_embeddings.ld == 1024
+    assert torch.equal(r2.corpus_embeddings.score(torch.from_numpy(enc.encode(queries[0]).numpy()).to(dev)), ref)
