@@ -4,7 +4,7 @@ stream it into the native index file (or into HBM), never holding the corpus's
 embeddings on the host.
 
     python tools/ingest.py --docs 1000000 --out /path/index.cbv2 [--dtype bf16|fp8] [--batch 4096]
-    python tools/ingest.py --docs 1000000 --hbm            # build the HBM index only
+    python tools/ingest.py --docs 1000000 --hbm [--dtype fp32]   # build the HBM index only
 
 The encoder is the synthetic corpus's (synth.SyntheticDocEncoder: the bench's
 1M-chunk corpus); with a real model, pass any object with encode(texts).
@@ -30,10 +30,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=1_000_000)
     ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16")
+    ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
+                    help="fp32: the fp32-faithful index (hi + residual), --hbm only")
     ap.add_argument("--out", default=None, help="native index file to write")
     ap.add_argument("--hbm", action="store_true", help="build the HBM index instead of a file")
     a = ap.parse_args()
+    if a.dtype == "fp32" and not a.hbm:
+        ap.error("the fp32-faithful index is built in HBM (--hbm); its file form is ColbertIndex.save")
     dev = torch.device("cuda:0")
     B = 64
     Qf = synth.make_queries(B, 32, seed=1)
@@ -53,7 +56,7 @@ def main():
     dt = time.time() - t0
     if ix is None:
         ix = ColbertIndex.load(a.out, device=dev)
-    _, ids = ix.search(Qf.to(dev, torch.bfloat16), 100)
+    _, ids = ix.search(Qf.to(dev, torch.float32 if ix.faithful else torch.bfloat16), 100)
     ids = ids.cpu().numpy()
     ok = float(sum(set(ids[b, :10]) == set(planted[b]) for b in range(B)) / B)
     print(json.dumps({"docs": a.docs, "dtype": a.dtype, "sink": "hbm" if a.hbm else "file", "seconds": round(dt, 2),
