@@ -1289,6 +1289,54 @@ __device__ __forceinline__ void tile_f8(const i32x8& a, int as, const i32x8 (&qa
   }
 }
 
+// Query scale bytes of the doc-interleaved f8 scan: one VGPR per (query,
+// column tile) (PQS = false), or four packed per VGPR with the MFMA's op_sel
+// picking the byte (PQS = true: 12 fewer VGPRs at 8 queries per wave).  i =
+// 2 * query + column tile; a compile-time constant once the loops unroll.
+template <int QW, bool PQS>
+constexpr int kQsRegs = PQS ? (2 * QW + 3) / 4 : 2 * QW;
+
+template <bool PQS>
+__device__ __forceinline__ f32x4 mfma_f8q(const i32x8& a, int as, const i32x8& b, const int* qsv, int i,
+                                          const f32x4& c) {
+  if constexpr (!PQS) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, as, 0, qsv[i]);
+  } else {
+    const int v = qsv[i >> 2];
+    switch (i & 3) {
+      case 0: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, as, 0, v);
+      case 1: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, as, 1, v);
+      case 2: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, as, 2, v);
+      default: return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, as, 3, v);
+    }
+  }
+}
+
+template <int QW, bool PQS>
+__device__ __forceinline__ void pack_qscales(const int (&qs)[QW][2], int (&qsv)[kQsRegs<QW, PQS>]) {
+#pragma unroll
+  for (int r = 0; r < kQsRegs<QW, PQS>; ++r) qsv[r] = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * QW; ++i) {
+    const int v = qs[i >> 1][i & 1];
+    if constexpr (PQS) qsv[i >> 2] |= (v & 0xff) << (8 * (i & 3));
+    else qsv[i] = v;
+  }
+}
+
+template <int QW, bool PQS>
+__device__ __forceinline__ void tile_f8q(const i32x8& a, int as, const i32x8 (&qa)[QW][2], const int* qsv,
+                                         const f32x4& init, float (&m)[QW][2]) {
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const f32x4 acc = mfma_f8q<PQS>(a, as, qa[q][ct], qsv, 2 * q + ct, init);
+      m[q][ct] = fmaxf(fmaxf(m[q][ct], fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
+    }
+  }
+}
+
 // Whole (query, doc) pass of the f8 tiling; FRAG(rt, a, as) loads row tile rt.
 template <int QW, typename Frag>
 __device__ __forceinline__ void doc_f8(Frag frag, const i32x8 (&qa)[QW][2], const int (&qs)[QW][2], int dl, int lane,
@@ -1431,9 +1479,9 @@ __device__ __forceinline__ void lds_afrag_f8x4(const uint8_t* buf, int t, int la
 // wait for them (hipcc waits lgkmcnt(0) there), and the fold of chain k-D is
 // fenced after MFMA k (hipcc otherwise hoists the fold above it and pads the
 // MFMA -> VALU hazard with s_nop).
-template <int QW, int D, int TPI = 32, bool PF = false>
+template <int QW, int D, int TPI = 32, bool PF = false, bool PQS = false>
 __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, const i32x8 (&qa)[QW][2],
-                                               const int (&qs)[QW][2], float (&m)[QW][2]) {
+                                               const int* qsv, float (&m)[QW][2]) {
   constexpr int NC = 2 * QW;
   static_assert(D >= 1 && NC % (D + 1) == 0, "ring slot of chain k must be k % (D+1) across tiles");
   constexpr int NT = TPI / 4;
@@ -1453,8 +1501,7 @@ __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, con
     for (int cc = 0; cc < NC; ++cc) {
       const int k = t * NC + cc;
       if (!PF && cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
-      acc[k % (D + 1)] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-          a[t & 1], qa[cc >> 1][cc & 1], f32x4{}, 0, 0, 0, as[t & 1], 0, qs[cc >> 1][cc & 1]);
+      acc[k % (D + 1)] = mfma_f8q<PQS>(a[t & 1], as[t & 1], qa[cc >> 1][cc & 1], qsv, cc, f32x4{});
       if constexpr (PF) {
         __builtin_amdgcn_sched_barrier(0);
         if (cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
@@ -1467,10 +1514,9 @@ __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, con
   for (int k = NT * NC - D; k < NT * NC; ++k) fold(k);
 }
 
-template <int QW, int TPI = 32>
+template <int QW, int TPI = 32, bool PQS = false>
 __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, int j, int dl_g, int dl_max,
-                                                 const i32x8 (&qa)[QW][2], const int (&qs)[QW][2],
-                                                 float (&m)[QW][2]) {
+                                                 const i32x8 (&qa)[QW][2], const int* qsv, float (&m)[QW][2]) {
   const int nt = min(TPI / 4, (dl_max - TPI * j + 3) >> 2);
 #pragma unroll 1
   for (int t = 0; t < nt; ++t) {
@@ -1481,12 +1527,12 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
     f32x4 init;
 #pragma unroll
     for (int r = 0; r < 4; ++r) init[r] = (tok0 + r < dl_g) ? 0.0f : neg_inf();
-    tile_f8<QW>(a, as, qa, qs, init, m);
+    tile_f8q<QW, PQS>(a, as, qa, qsv, init, m);
   }
 }
 
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
-          int FK = 0, int LD = kLd>
+          int FK = 0, int LD = kLd, bool PQS = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1526,9 +1572,13 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   const int64_t chunk = lin / nq_groups;
 
   i32x8 qa[QW][2];
-  int qs[QW][2];
+  int qsv[kQsRegs<QW, PQS>];
+  {
+    int qs[QW][2];
 #pragma unroll
-  for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, qg * QPB + wave * QW + q, B, lq, lane, qa[q], qs[q]);
+    for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, qg * QPB + wave * QW + q, B, lq, lane, qa[q], qs[q]);
+    pack_qscales<QW, PQS>(qs, qsv);
+  }
 
   // piece p = image rows 8p..8p+7 (128 B each) = doc 8p / TPI (uniform per
   // piece), tokens TPI*j + 8p % TPI + 0..7.  Offsets are recomputed per issue
@@ -1606,9 +1656,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     }
     if (TPI * j + TPI <= dl_min)
-      iter_f8x4_full<QW, D, TPI, PF>(buf, lane, qa, qs, m);
+      iter_f8x4_full<QW, D, TPI, PF, PQS>(buf, lane, qa, qsv, m);
     else if (TPI * j < dl_max)
-      iter_f8x4_ragged<QW, TPI>(buf, lane, j, dl_g, dl_max, qa, qs, m);
+      iter_f8x4_ragged<QW, TPI, PQS>(buf, lane, j, dl_g, dl_max, qa, qsv, m);
     if (j == IPG - 1) {
 #pragma unroll
       for (int q = 0; q < QW; ++q) {
@@ -3342,11 +3392,19 @@ constexpr int kF8SmallMaxB = 8;
 // (lab r02ad), B=80 35.1 -> 26.2 (r02af).
 constexpr ShapeCost kF8Shapes[] = {{8, 3.0f, 9}, {16, 5.2f, 7}, {32, 9.5f, 8}, {64, 18.2f, 5}};
 constexpr int kF8Waves = 8, kF8QW = 8;
+// Fold distance of the doc-interleaved f8 scans: a chain's row max is folded
+// 3 MFMAs after it issues (no MFMA -> VALU hazard pads: 122 -> 36 s_nop per
+// 128 MFMAs), with the query scale bytes packed four per VGPR (PQS) to pay
+// for the two extra accumulators (254 VGPRs, no spill; was 256 + 2 spilled).
+// Lab A/B, 1M docs, bit-identical (profiles/r02s3_lab_f8*.log): B=256 72.44
+// -> 70.98 ms, B=64 19.19 -> 18.77, B=32 10.26 -> 10.17, B=16 5.73 -> 5.71,
+// B=8 3.73 -> 3.65.
+constexpr int kF8D = 3;
 
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
-          int FK = 0, int LD = kLd>
+          int FK = 0, int LD = kLd, int D = 1, bool PQS = false>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -3359,7 +3417,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, 1, NBUF, TPI, PF, OCC, FK, LD>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3375,10 +3433,10 @@ template <int LD>
 int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                    hipStream_t st, int* ctr_ws) {
   if (B <= kF8SmallMaxB)
-    return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, LD>(ix, Qb, Qs, B, lq, out, ld_out, st, kScanDynFrac,
-                                                       kScanTaskDocs, ctr_ws);
-  return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, LD>(ix, Qb, Qs, B, lq, out, ld_out, st, kScanDynFrac,
-                                                                kScanTaskDocs, ctr_ws);
+    return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, LD, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, kScanDynFrac,
+                                                                   kScanTaskDocs, ctr_ws);
+  return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, LD, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                            kScanDynFrac, kScanTaskDocs, ctr_ws);
 }
 
 int scan_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
@@ -3443,19 +3501,27 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    case 5: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 5: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out,
+                                                                                      st, dyn_frac, task_docs, ctr_ws);
     case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
     // 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave, three
     // workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two per CU
     // (2 waves per SIMD from independent barrier domains); 9 = 2 queries per
     // wave, two per CU
-    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac,
+                                                                            task_docs, ctr_ws);
+    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac,
+                                                                            task_docs, ctr_ws);
+    case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac,
+                                                                            task_docs, ctr_ws);
 #ifdef CBV2_LAB
     case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    // 11 = shape 5 as it was before the packed scales and D = 3 (round 2)
+    case 11: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, 1, false>(ix, Qb, Qs, B, lq, out, ld_out,
+                                                                                     st, dyn_frac, task_docs, ctr_ws);
 #endif
-    default: return launch_f8x4<32, 3, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    default: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out,
+                                                                                         st, dyn_frac, task_docs, ctr_ws);
   }
 }
 
