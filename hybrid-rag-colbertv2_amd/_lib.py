@@ -88,6 +88,8 @@ _SIGS = {
     "cbv2_f32_workspace_bytes": (_sz, [_p, _i32, _i32, _i32, _i32]),
     "cbv2_score_f32": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _sz, _p, _i64, _p]),
     "cbv2_search_f32": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
+    "cbv2_search_f32_begin": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p, _p, _p]),
+    "cbv2_search_f32_finish": (ctypes.c_int, [_p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p, _p, _p]),
     "cbv2_rerank_f32": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
 }
 

@@ -3610,6 +3610,11 @@ int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t
   return scan_meanpool(ix, (const float*)Q, B, lq, out, ld_out, st);
 }
 
+__global__ void fill_neg_inf_kernel(float* x, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = neg_inf();
+}
+
 __global__ void fill_empty_kernel(float* out_s, int32_t* out_i, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < total) {
@@ -4085,44 +4090,50 @@ int cbv2_score_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, void* 
   return launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, out, ld_out, st);
 }
 
-int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
-                    size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_status, void* stream) {
-  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
-  // k beyond any band: every row takes the full faithful scan (status -1)
-  const bool full = k > kBandCapMax;
-  CBV2_REQUIRE(full || (cap >= k && cap <= kBandCapMax), "cap must be in [k, %d] (got %d)", kBandCapMax, cap);
-  F32Ws w;
-  int rc = check_f32(ix, CBV2_F32_SEARCH, Q, B, lq, cap, ws, wsb, &w);
-  if (rc) return rc;
-  CBV2_REQUIRE(out_scores && out_ids && out_status, "null outputs");
-  DeviceGuard dg(ix->device);
-  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
-  hipStream_t st = (hipStream_t)stream;
+namespace {
+// Faithful search, phase 1: split the queries, bf16 scan of hi (T), its top-k
+// (out), and -- with the two-pass band -- the exact lower bound lb of each
+// row's k-th faithful score (the minimum faithful score of the bf16 top-k)
+// into lb_out; fk_out (nullable): those k faithful scores themselves, [B][k].
+// Returns 1 when the whole search is already done (k beyond any band: the
+// full faithful scan ran, status -1 everywhere).
+int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w,
+                      float* out_scores, int32_t* out_ids, int32_t* out_status, float* lb_out, hipStream_t st,
+                      float* fk_out = nullptr) {
+  int rc;
   if (ix->n == 0) {
     CBV2_HIP(hipMemsetAsync(out_status, 0, (size_t)B * sizeof(int32_t), st));
-    return topk_impl_empty(B, k, out_scores, out_ids, st);
+    if ((rc = topk_impl_empty(B, k, out_scores, out_ids, st))) return rc;
+    return 1;
   }
   if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
-  if (full) {
+  if (k > kBandCapMax) {   // no band can hold k: every row takes the full faithful scan (status -1)
     CBV2_HIP(hipMemsetAsync(out_status, 0xff, (size_t)B * sizeof(int32_t), st));
     if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st))) return rc;
-    return topk_multi(w.T, B, ix->n, ix->n, k, ix->id_base, nullptr, 0, out_scores, out_ids, nullptr, st);
+    if ((rc = topk_multi(w.T, B, ix->n, ix->n, k, ix->id_base, nullptr, 0, out_scores, out_ids, nullptr, st)))
+      return rc;
+    return 1;
   }
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
   if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr))) return rc;
   if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
     return rc;
-  // 2. the band: every doc with T >= lb - beta, lb = an exact lower bound of
-  //    the k-th faithful score (the bf16 top-k's own faithful scores: the
-  //    minimum of k of them), or T_k - 2 beta without that pass (A/B);
-  // 3. faithful rescoring of the band, 4. exact top-k of the band
-  const float* lb = nullptr;
-  if (ix->band_lower_bound) {
+  if (fk_out != nullptr)     // the bf16 top-k's own faithful scores, for the caller's cross-shard bound
+    return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, fk_out, k, st);
+  if (lb_out != nullptr) {   // the bf16 top-k's own faithful scores: k docs score at least their minimum
     if ((rc = launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, w.F, cap, st))) return rc;
-    hipLaunchKernelGGL(band_lb_kernel, dim3((unsigned)B), dim3(64), 0, st, w.F, cap, k, w.lb);
+    hipLaunchKernelGGL(band_lb_kernel, dim3((unsigned)B), dim3(64), 0, st, w.F, cap, k, lb_out);
     if ((rc = launch_check("band_lb_kernel"))) return rc;
-    lb = w.lb;
   }
+  return CBV2_OK;
+}
+
+// Phase 2: the band (every doc with T >= lb - beta; lb == nullptr: T_k - 2
+// beta, the one-pass band), its faithful rescoring, the exact top-k of the
+// band, and the full faithful scan for rows whose band overflowed cap.
+int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w, const float* lb,
+                      float* out_scores, int32_t* out_ids, int32_t* out_status, hipStream_t st) {
+  int rc;
   CBV2_HIP(hipMemsetAsync(w.count, 0, (size_t)B * sizeof(int32_t), st));
   int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
   const int64_t max_splits = (ix->n + 8191) / 8192;
@@ -4157,14 +4168,78 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
                      ix->id_base, out_scores, out_ids, out_status);
   if ((rc = launch_check("band_select_kernel"))) return rc;
-  // 5. rows whose band overflowed cap (status -1): the full faithful scan over
-  //    every doc and an exact top-k, on the device (other rows exit at once)
+  // rows whose band overflowed cap (status -1): the full faithful scan over
+  // every doc and an exact top-k, on the device (other rows exit at once)
   if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st, out_status))) return rc;
   if (k > kTopkMax)
     return topk_multi(w.T, B, ix->n, ix->n, k, ix->id_base, nullptr, 0, out_scores, out_ids, nullptr, st, out_status);
   hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.T, ix->n, ix->n, k, ix->id_base,
                      out_scores, out_ids, out_status);
   return launch_check("topk_rows_kernel");
+}
+
+int check_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
+                     size_t wsb, F32Ws* w) {
+  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
+  CBV2_REQUIRE(k > kBandCapMax || (cap >= k && cap <= kBandCapMax), "cap must be in [k, %d] (got %d)", kBandCapMax,
+               cap);
+  return check_f32(ix, CBV2_F32_SEARCH, Q, B, lq, cap, ws, wsb, w);
+}
+}  // namespace
+
+int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
+                    size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_status, void* stream) {
+  F32Ws w;
+  int rc = check_search_f32(ix, Q, B, lq, k, cap, ws, wsb, &w);
+  if (rc) return rc;
+  CBV2_REQUIRE(out_scores && out_ids && out_status, "null outputs");
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipStream_t st = (hipStream_t)stream;
+  // 2. the band: every doc with T >= lb - beta, lb = an exact lower bound of
+  //    the k-th faithful score (the bf16 top-k's own faithful scores: the
+  //    minimum of k of them), or T_k - 2 beta without that pass (A/B);
+  // 3. faithful rescoring of the band, 4. exact top-k of the band
+  float* lb = ix->band_lower_bound ? w.lb : nullptr;
+  rc = search_f32_phase1(ix, Q, B, lq, k, cap, w, out_scores, out_ids, out_status, lb, st);
+  if (rc) return rc < 0 ? rc : CBV2_OK;
+  return search_f32_phase2(ix, B, lq, k, cap, w, lb, out_scores, out_ids, out_status, st);
+}
+
+int cbv2_search_f32_begin(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
+                          size_t wsb, float* fk, float* out_scores, int32_t* out_ids, int32_t* out_status,
+                          void* stream) {
+  F32Ws w;
+  int rc = check_search_f32(ix, Q, B, lq, k, cap, ws, wsb, &w);
+  if (rc) return rc;
+  CBV2_REQUIRE(fk && out_scores && out_ids && out_status, "null outputs");
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  hipStream_t st = (hipStream_t)stream;
+  // fk = -inf unless phase 1 writes it (an empty shard, k beyond any band)
+  hipLaunchKernelGGL(fill_neg_inf_kernel, dim3((unsigned)(((int64_t)B * k + 255) / 256)), dim3(256), 0, st, fk,
+                     (int64_t)B * k);
+  if ((rc = launch_check("fill_neg_inf_kernel"))) return rc;
+  rc = search_f32_phase1(ix, Q, B, lq, k, cap, w, out_scores, out_ids, out_status, nullptr, st, fk);
+  return rc < 0 ? rc : CBV2_OK;
+}
+
+int cbv2_search_f32_finish(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws, size_t wsb,
+                           const float* lb, float* out_scores, int32_t* out_ids, int32_t* out_status, void* stream) {
+  F32Ws w;
+  CBV2_REQUIRE(ix != nullptr, "null index");
+  CBV2_REQUIRE(B >= 1 && B <= 65535 && lq >= 1 && lq <= kLqMax, "bad B / lq");
+  CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
+  CBV2_REQUIRE(k > kBandCapMax || (cap >= k && cap <= kBandCapMax), "cap must be in [k, %d] (got %d)", kBandCapMax,
+               cap);
+  const size_t need = f32_ws_layout(ix, CBV2_F32_SEARCH, B, lq, cap, nullptr, &w);
+  CBV2_REQUIRE(ws != nullptr && wsb >= need && aligned16(ws), "workspace too small or misaligned");
+  f32_ws_layout(ix, CBV2_F32_SEARCH, B, lq, cap, (uint8_t*)ws, &w);
+  CBV2_REQUIRE(lb && out_scores && out_ids && out_status, "null inputs/outputs");
+  if (ix->n == 0 || k > kBandCapMax) return CBV2_OK;   // phase 1 already finished these
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  return search_f32_phase2(ix, B, lq, k, cap, w, lb, out_scores, out_ids, out_status, (hipStream_t)stream);
 }
 
 int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C,

@@ -257,10 +257,29 @@ class ShardedSearcher:
             dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
         return out
 
+    def _local_search(self, Q: torch.Tensor, k: int):
+        """This rank's top-k.  An fp32-faithful shard bounds its band by the
+        GLOBAL k-th score: every rank's exact faithful scores of its bf16 top-k
+        ([B, k] f32, one all-gather) give k docs per rank whose scores are
+        known, and the k-th largest of all of them is a lower bound of the
+        global k-th score; each rank then rescores only the docs that can reach
+        the global top-k rather than its own (cbv2_search_f32_begin / _finish).
+        The merge of the per-rank lists is the exact global top-k."""
+        if self.world > 1 and getattr(self.local, "faithful", False):
+            return self.local.search(Q, k, lb_reduce=lambda fk: self._global_kth(fk, k))
+        return self.local.search(Q, k)
+
+    def _global_kth(self, fk: torch.Tensor, k: int) -> torch.Tensor:
+        allf = self._all_gather(fk)                                                  # [G, B, k]
+        B = fk.shape[0]
+        union = allf.permute(1, 0, 2).reshape(B, self.world * k).contiguous()        # [B, G*k]
+        s, _, _ = self.ops.select(union, k, None)                                    # HIP select, desc
+        return s[:, k - 1].contiguous()
+
     def search(self, Q: torch.Tensor, k: int):
         if self._nx is not None:
             return self._nx.search(Q, k)[:2]
-        s, i = self.local.search(Q, k)
+        s, i = self._local_search(Q, k)
         if self.world == 1:
             return s, i
         return self.search_exchange(s, i, k)
@@ -278,7 +297,7 @@ class ShardedSearcher:
         """
         if self._nx is not None:
             return self._nx.search(Q, k, lexical)
-        s, i = self.local.search(Q, k)
+        s, i = self._local_search(Q, k)
         if lexical is None:
             if self.world == 1:
                 return s, i, None

@@ -426,13 +426,24 @@ class ColbertIndex:
                                          out.shape[1], _stream_ptr(self.device)))
         return out[:, : self.n]
 
-    def search(self, Q: torch.Tensor, k: int, scorer: str = "maxsim") -> Tuple[torch.Tensor, torch.Tensor]:
-        """Top-k over the shard: (f32 [B, k] scores, int32 [B, k] global ids), -inf/-1 padded."""
+    def search(self, Q: torch.Tensor, k: int, scorer: str = "maxsim",
+               lb_reduce=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Top-k over the shard: (f32 [B, k] scores, int32 [B, k] global ids), -inf/-1 padded.
+
+        ``lb_reduce`` (fp32-faithful index, sharded corpus): called with the
+        exact faithful scores of this shard's bf16 top-k (device f32 [B, k]);
+        returns a per-row lower bound of the GLOBAL k-th faithful score (device
+        f32 [B]: the k-th largest of every shard's lists).  The shard then
+        rescores only the docs that can reach the global top-k and returns its
+        part of it, which the merge completes (cbv2_search_f32_begin /
+        _finish)."""
         if self._query_blocks(Q, scorer) is not None:   # long queries: summed block scores + radix top-k
             return topk_rows(self.score(Q, scorer), int(k), id_base=self.id_base)
         sid = self._scorer(scorer)
         _keep, qptr, qdt, B, lq = self._prep_query(Q, scorer)
         if self.faithful and scorer == "maxsim":
+            if lb_reduce is not None:
+                return self._search_f32_global(_keep, B, lq, k, lb_reduce)
             return self._search_f32(_keep, B, lq, k)
         L = _lib.lib()
         need = int(L.cbv2_search_workspace_size(self._h, B, int(k), sid))
@@ -457,6 +468,28 @@ class ColbertIndex:
         _lib.check(_lib.lib().cbv2_search_f32(self._h, Qd.data_ptr(), B, lq, int(k), cap, ws.data_ptr(),
                                               ws.numel() * 4, out_s.data_ptr(), out_i.data_ptr(),
                                               status.data_ptr(), _stream_ptr(self.device)))
+        self.last_band = status
+        return out_s, out_i
+
+    def _search_f32_global(self, Qd: torch.Tensor, B: int, lq: int, k: int, lb_reduce, cap: int = BAND_CAP):
+        """Faithful search of one shard against the global k-th bound (see
+        ``search``): begin -> lb = lb_reduce(fk) -> finish, asynchronous."""
+        cap = max(int(cap), int(k))
+        ws = self._f32_ws(_lib.F32_SEARCH, B, lq, cap)
+        out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
+        out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
+        status = torch.empty((B,), dtype=torch.int32, device=self.device)
+        fk = torch.empty((B, k), dtype=torch.float32, device=self.device)
+        L = _lib.lib()
+        _lib.check(L.cbv2_search_f32_begin(self._h, Qd.data_ptr(), B, lq, int(k), cap, ws.data_ptr(),
+                                           ws.numel() * 4, fk.data_ptr(), out_s.data_ptr(), out_i.data_ptr(),
+                                           status.data_ptr(), _stream_ptr(self.device)))
+        lb = lb_reduce(fk).to(device=self.device, dtype=torch.float32).contiguous()
+        if tuple(lb.shape) != (B,):
+            raise ValueError(f"lb_reduce must return f32 [{B}] (got {tuple(lb.shape)})")
+        _lib.check(L.cbv2_search_f32_finish(self._h, B, lq, int(k), cap, ws.data_ptr(), ws.numel() * 4,
+                                            lb.data_ptr(), out_s.data_ptr(), out_i.data_ptr(), status.data_ptr(),
+                                            _stream_ptr(self.device)))
         self.last_band = status
         return out_s, out_i
 

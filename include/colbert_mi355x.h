@@ -216,6 +216,17 @@ int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const i
  *    k > 16384 (no band can hold it): every row takes the full scan (-1).
  *    Either way the result is the faithful top-k of the whole corpus; the
  *    call stays asynchronous (no host round trip).
+ *  - cbv2_search_f32_begin / _finish: the same search in two calls, for a
+ *    sharded corpus.  begin runs the scan and top-k and writes fk (DEVICE f32
+ *    [B][k]): the exact faithful scores of the shard's bf16 top-k (-inf
+ *    padded; all -inf for an empty shard).  The caller derives lb (DEVICE f32
+ *    [B]) from them: the k-th largest of the fk of ALL shards (one all-gather)
+ *    -- k docs of the corpus score at least that, so it is <= the global k-th
+ *    faithful score; any such lower bound keeps the result exact (one shard:
+ *    the minimum of its fk).  finish rescores only the docs with T >= lb -
+ *    beta(q) and returns this shard's part of the global top-k (-inf / -1
+ *    padded where fewer of its docs can reach it), which the cross-shard merge
+ *    completes.  Same workspace between the two calls.
  *  - cbv2_rerank_f32: cbv2_rerank with faithful scores.                      */
 #define CBV2_F32_SCORE 0
 #define CBV2_F32_SEARCH 1
@@ -229,6 +240,12 @@ int cbv2_score_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, voi
 int cbv2_search_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap,
                     void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids,
                     int32_t* out_status, void* stream);
+int cbv2_search_f32_begin(cbv2_index* index, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap,
+                          void* workspace, size_t workspace_bytes, float* fk, float* out_scores, int32_t* out_ids,
+                          int32_t* out_status, void* stream);
+int cbv2_search_f32_finish(cbv2_index* index, int32_t B, int32_t lq, int32_t k, int32_t cap, void* workspace,
+                           size_t workspace_bytes, const float* lb, float* out_scores, int32_t* out_ids,
+                           int32_t* out_status, void* stream);
 int cbv2_rerank_f32(cbv2_index* index, const float* Q, int32_t B, int32_t lq, const int32_t* cand,
                     int32_t C, int32_t k, void* workspace, size_t workspace_bytes, float* out_scores,
                     int32_t* out_ids, int32_t* out_pos, void* stream);

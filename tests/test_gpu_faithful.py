@@ -184,3 +184,38 @@ def test_band_lower_bound_equals_plain_band(dev, N, k):
     rs, _ = orc.topk(exact, k, id_base=11)
     fin = np.isfinite(rs)
     np.testing.assert_allclose(s1.cpu().numpy()[fin], rs[fin], atol=ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("N,k,parts", [(12000, 100, (0, 3000, 7000, 12000)), (3000, 10, (0, 1500, 3000)),
+                                       (600, 100, (0, 550, 600))])
+def test_sharded_global_lower_bound_equals_unsharded(dev, N, k, parts):
+    """cbv2_search_f32_begin / _finish as ShardedSearcher uses them: the
+    shards' faithful scores of their bf16 top-k, gathered, give the k-th
+    largest as a bound of the GLOBAL k-th score for every shard's band; the
+    merge of the per-shard lists equals the unsharded faithful search bit for
+    bit, and no shard's band is wider than with its own bound (the minimum of
+    its own list; shard 550..600 has < k docs)."""
+    from hybrid_rag_colbertv2_amd.index import merge_topk
+    docs, doclens, Q = make_case(N + k, N, 6, 32)
+    Qd = Q.to(dev)
+    fs, fi = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev)).search(Qd, k)
+    shards = [ColbertIndex.faithful_f32(docs[a:b].to(dev), doclens[a:b].to(dev), id_base=a)
+              for a, b in zip(parts[:-1], parts[1:])]
+    fks, own_band = [], []
+
+    def own(fk):                                      # pass 1: every shard alone (its lists are the gather's inputs)
+        fks.append(fk.clone())
+        return fk.min(dim=1).values
+    for sh in shards:
+        sh.search(Qd, k, lb_reduce=own)
+        own_band.append(sh.last_band.clone())
+    glob = torch.cat(fks, dim=1).topk(k, dim=1).values[:, k - 1]
+    lists, bands = [], []
+    for sh in shards:                                 # pass 2: what each rank does after the all-gather
+        lists.append(sh.search(Qd, k, lb_reduce=lambda fk: glob))
+        bands.append(sh.last_band.clone())
+    ms, mi = merge_topk(torch.stack([x[0] for x in lists]), torch.stack([x[1] for x in lists]), k)
+    assert torch.equal(mi, fi) and torch.equal(ms, fs)
+    for own, b in zip(own_band, bands):
+        assert ((b >= 0) & (b <= own)).all(), (own, b)
+    assert sum(int(b.sum()) for b in bands) < sum(int(b.sum()) for b in own_band)
