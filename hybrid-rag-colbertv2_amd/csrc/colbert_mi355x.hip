@@ -4228,6 +4228,7 @@ int cbv2_search_f32_finish(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
                            const float* lb, float* out_scores, int32_t* out_ids, int32_t* out_status, void* stream) {
   F32Ws w;
   CBV2_REQUIRE(ix != nullptr, "null index");
+  if (ix->resid == nullptr) return fail(CBV2_ESTATE, "index has no fp32 residual (cbv2_index_attach_residual)");
   CBV2_REQUIRE(B >= 1 && B <= 65535 && lq >= 1 && lq <= kLqMax, "bad B / lq");
   CBV2_REQUIRE(k >= 1, "k must be >= 1 (got %d)", k);
   CBV2_REQUIRE(k > kBandCapMax || (cap >= k && cap <= kBandCapMax), "cap must be in [k, %d] (got %d)", kBandCapMax,
