@@ -129,6 +129,15 @@ def test_f32_abi_validation(dev):
                             None) == _lib.ERR_EINVAL
     assert L.cbv2_score_f32(ix._h, q.data_ptr(), 1, 32, ws.data_ptr(), 16, out.data_ptr(), 10,
                             None) == _lib.ERR_EINVAL
+    fk = torch.empty((1, 10), device=dev)
+    oi = torch.empty((1, 10), dtype=torch.int32, device=dev)
+    stt = torch.empty((1,), dtype=torch.int32, device=dev)
+    assert L.cbv2_search_f32_finish(bx._h, 1, 32, 10, 64, ws.data_ptr(), ws.numel(), fk.data_ptr(), out.data_ptr(),
+                                    oi.data_ptr(), stt.data_ptr(), None) == _lib.ERR_ESTATE
+    assert L.cbv2_search_f32_begin(ix._h, q.data_ptr(), 1, 32, 10, 5, ws.data_ptr(), ws.numel(), fk.data_ptr(),
+                                   out.data_ptr(), oi.data_ptr(), stt.data_ptr(), None) == _lib.ERR_EINVAL  # cap < k
+    assert L.cbv2_search_f32_begin(ix._h, q.data_ptr(), 1, 32, 10, 64, ws.data_ptr(), ws.numel(), None,
+                                   out.data_ptr(), oi.data_ptr(), stt.data_ptr(), None) == _lib.ERR_EINVAL  # null fk
 
 
 def test_faithful_shards_merge_equal_unsharded(dev):
