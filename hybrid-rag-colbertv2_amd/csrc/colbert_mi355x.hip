@@ -1834,6 +1834,26 @@ __device__ void bitonic_desc(uint64_t* keys, int P) {
   __syncthreads();
 }
 
+// LDS histogram add with wave aggregation: lanes whose bins agree add once
+// (up to 4 rounds, led by the lowest remaining lane's bin), the rest by plain
+// atomics.  Score keys of similar magnitude share their top digit, so in a
+// radix select's first pass one bin takes most of a wave: 64 serialised LDS
+// atomics on one address become one add.
+__device__ __forceinline__ void hist_add(uint32_t* hist, uint32_t bin, bool take) {
+  const int lane = threadIdx.x & 63;
+  uint64_t rem = __ballot(take);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (rem == 0) break;   // wave-uniform
+    const int leader = __ffsll((unsigned long long)rem) - 1;
+    const uint32_t lb = __shfl(bin, leader);
+    const uint64_t same = rem & __ballot(take && bin == lb);
+    if (lane == leader) atomicAdd(&hist[lb], (uint32_t)__popcll(same));
+    rem &= ~same;
+  }
+  if ((rem >> lane) & 1ull) atomicAdd(&hist[bin], 1u);
+}
+
 // Exact selection of the kk largest keys of row x into sel[0..kk) (unordered).
 // Radix select on the 32-bit score key (11/11/10-bit digits); if the kk-th
 // score is tied, a second radix select over ~index keeps the lowest indices.
@@ -1861,7 +1881,7 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
     for (int64_t i = tid; i < n; i += nth) {
       const float v = x[i];
       const uint32_t u = f2u(v);
-      if ((u & mask) == prefix && live(v, i)) atomicAdd(&hist[(u >> shifts[p]) & (nb - 1)], 1u);
+      hist_add(hist, (u >> shifts[p]) & (nb - 1), (u & mask) == prefix && live(v, i));
     }
     __syncthreads();
     if (wave == 0) find_bin(hist, nb, kleft, s_bin, s_above, s_bincount);
@@ -1883,8 +1903,7 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
       for (int64_t i = tid; i < n; i += nth) {
         const uint32_t key2 = ~(uint32_t)i;
         const float v = x[i];
-        if (f2u(v) == ustar && (key2 & imask) == iprefix && live(v, i))
-          atomicAdd(&hist[(key2 >> shifts[p]) & (nb - 1)], 1u);
+        hist_add(hist, (key2 >> shifts[p]) & (nb - 1), f2u(v) == ustar && (key2 & imask) == iprefix && live(v, i));
       }
       __syncthreads();
       if (wave == 0) find_bin(hist, nb, kl2, s_bin, s_above, s_bincount);
@@ -2028,7 +2047,15 @@ __global__ __launch_bounds__(256) void topk_filter_kernel(const float* __restric
   const int row = blockIdx.y;
   const float* x = scores + (size_t)row * ld;
   const int64_t stride = n / kSampleN;
-  for (int j = tid; j < kSampleN; j += 256) skeys[j] = f2u(x[(int64_t)j * stride]);
+  {   // all 32 strided sample loads of a thread in flight at once (a load-store
+      // loop kept ~1 in flight: the sample, not the stream, set the B=1 time)
+    constexpr int SPT = kSampleN / 256;
+    float sv[SPT];
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) sv[u] = x[(int64_t)(tid + 256 * u) * stride];
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) skeys[tid + 256 * u] = f2u(sv[u]);
+  }
   int64_t m64 = (8LL * k * kSampleN + n - 1) / n;
   const uint32_t m = (uint32_t)(m64 < 1 ? 1 : (m64 > kSampleN ? kSampleN : m64));
   uint32_t prefix = 0, mask = 0, kleft = m;
@@ -2038,7 +2065,7 @@ __global__ __launch_bounds__(256) void topk_filter_kernel(const float* __restric
     __syncthreads();
     for (int j = tid; j < kSampleN; j += 256) {
       const uint32_t u = skeys[j];
-      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);   // (wave-aggregated adds: slower here)
     }
     __syncthreads();
     if (tid < 64) find_bin(hist, 256, kleft, &s_bin, &s_above, &s_bincount);
@@ -2049,7 +2076,10 @@ __global__ __launch_bounds__(256) void topk_filter_kernel(const float* __restric
     __syncthreads();
   }
   const uint32_t t = prefix;
-  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  // slices of a multiple of 4 scores, so a row that starts 16-B aligned
+  // (aligned base, ld % 4 == 0) streams as float4: 16 scores per thread in flight (4 KiB
+  // per workgroup with scalar loads left the B=256 filter at 2.1 TB/s)
+  const int64_t per = ((n + gridDim.x - 1) / gridDim.x + 3) & ~3LL;
   const int64_t a = (int64_t)blockIdx.x * per;
   const int64_t b = (a + per < n) ? a + per : n;
   uint64_t* crow = cand + (size_t)row * kCandCap;
@@ -2059,23 +2089,49 @@ __global__ __launch_bounds__(256) void topk_filter_kernel(const float* __restric
   uint64_t* stage = reinterpret_cast<uint64_t*>(skeys);
   if (tid == 0) s_above = 0;   // reused: the workgroup's survivor count
   __syncthreads();
-  for (int64_t i = a + tid; i < b; i += 4 * 256) {
-    float v[4];
+  auto offer = [&](int64_t i, float v) {
+    const uint32_t key = f2u(v);
+    if (key >= t) {
+      const uint64_t kv = ((uint64_t)key << 32) | (uint32_t)(~(uint32_t)i);
+      const uint32_t lp = atomicAdd(&s_above, 1u);
+      if (lp < kStage) {
+        stage[lp] = kv;
+      } else {
+        const uint32_t pos = atomicAdd(&cnt[row], 1u);
+        if (pos < (uint32_t)kCandCap) crow[pos] = kv;
+      }
+    }
+  };
+  if ((ld & 3) == 0 && ((uintptr_t)scores & 15) == 0) {
+    constexpr int U = 4;
+    for (int64_t i = a + 4 * tid; i < b; i += 4 * 256 * U) {
+      f32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = (i + u * 256 < b) ? x[i + u * 256] : neg_inf();
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t key = f2u(v[u]);
-      if (i + u * 256 < b && key >= t) {
-        const uint64_t kv = ((uint64_t)key << 32) | (uint32_t)(~(uint32_t)(i + u * 256));
-        const uint32_t lp = atomicAdd(&s_above, 1u);
-        if (lp < kStage) {
-          stage[lp] = kv;
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = i + (int64_t)u * 1024;
+        if (j + 3 < b) {
+          v[u] = *reinterpret_cast<const f32x4*>(x + j);
         } else {
-          const uint32_t pos = atomicAdd(&cnt[row], 1u);
-          if (pos < (uint32_t)kCandCap) crow[pos] = kv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[u][e] = (j + e < b) ? x[j + e] : neg_inf();
         }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t j = i + (int64_t)u * 1024 + e;
+          if (j < b) offer(j, v[u][e]);
+        }
+    }
+  } else {
+    for (int64_t i = a + tid; i < b; i += 4 * 256) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (i + u * 256 < b) ? x[i + u * 256] : neg_inf();
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + u * 256 < b) offer(i + u * 256, v[u]);
     }
   }
   __syncthreads();
@@ -2138,7 +2194,7 @@ __global__ __launch_bounds__(kTkThreads) void select_keys_kernel(const uint64_t*
     __syncthreads();
     for (int64_t i = tid; i < M; i += kTkThreads) {
       const uint64_t u = x[i];
-      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);
+      hist_add(hist, (u >> shift) & 255, (u & mask) == prefix);
     }
     __syncthreads();
     if (wave == 0) find_bin(hist, 256, kleft, &s_bin, &s_above, &s_bincount);

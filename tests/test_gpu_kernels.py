@@ -282,9 +282,11 @@ def test_small_batch_scan_bit_identical_to_batched(dev):
 
 
 @pytest.mark.parametrize("dist", ["normal", "ints", "const", "spike", "neg"])
-@pytest.mark.parametrize("n,k", [(65536, 100), (300000, 100), (1000000, 10), (200000, 1024)])
+@pytest.mark.parametrize("n,k", [(65536, 100), (300000, 100), (1000000, 10), (200000, 1024), (262147, 100),
+                                 (65540, 50)])
 def test_sampled_topk_equals_exact(dev, dist, n, k):
-    """The threshold-filter top-k path (long rows) == exact radix select == oracle."""
+    """The threshold-filter top-k path (long rows) == exact radix select == oracle
+    (n % 4 != 0: the filter's scalar stream; otherwise float4 slices)."""
     g = torch.Generator(device=dev).manual_seed(n + k)
     B = 3
     if dist == "normal":
