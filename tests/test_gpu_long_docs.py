@@ -274,6 +274,12 @@ def test_long_chunks_end_to_end_default_config(dev, tmp_path):
     np.testing.assert_allclose([x["score"] for x in rr], np.sort(s_c)[::-1], atol=1e-4, rtol=0)
     assert [x["rank"] for x in rr] == [1, 2, 3, 4]
     assert rr[0]["result_index"] == int(np.argmax(s_c))
+    # stage 3 of HybridRetriever (_colbert_rerank -> rerank_ids): candidate tiles gathered by id
+    qe = torch.from_numpy(enc.encode(queries[1]).numpy()).to(dev)[None]
+    cand_ids = torch.tensor([[50, 7, 33, 0, 12, 59]], dtype=torch.int32, device=dev)
+    rs, ri, rp = r.rerank_ids(qe, cand_ids, 4)
+    s_ref = orc.maxsim(qe.cpu().numpy(), docs[[50, 7, 33, 0, 12, 59]], lens[[50, 7, 33, 0, 12, 59]])[0]
+    np.testing.assert_allclose(rs[0].cpu().numpy(), np.sort(s_ref)[::-1][:4], atol=1e-4, rtol=0)
     ref = r.corpus_embeddings.score(torch.from_numpy(enc.encode(queries[0]).numpy()).to(dev))
     r2 = JinaColBERTRetriever(cfg, encoder=enc)
     r2.load()
