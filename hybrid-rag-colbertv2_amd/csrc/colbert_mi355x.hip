@@ -3234,6 +3234,13 @@ constexpr int kScanTaskDocs = -16;     // guided: tasks shrink to 16 docs at the
 // 1.439 ms" was noise: the tail only switched on from 262,144 docs at B <= 16
 // then; it now switches on whenever each static chunk keeps >= 64 docs.)
 constexpr float kScanDynFracSmallB = 0.30f;
+// The 4-wave x 4-query shape (B = 9-16) on the ticket tail (round 2, session
+// 3; the 0.5 / 1.0 losses above were the CAS tail): lab, same process, 8
+// interleaved rounds (profiles/r02s3_lab_dynfrac_b16.log): 1M docs B=16 10.64
+// (0.3) -> 10.48 (0.45) -> 10.32 (0.6) -> 10.37 ms (0.75); 100k 1.080 ->
+// 1.064 / 1.069 / 1.129 ms.  The 4 x 2 shape (B = 3-8) stays at 0.3 (0.45 and
+// 0.6 are flat or slower at B = 4 / 8, profiles/r02s3_lab_dynfrac_b8.log).
+constexpr float kScanDynFracB16 = 0.60f;
 constexpr int64_t kMinChunkDocs = 64;
 
 // Fused top-k output of one scan launch: part [B][max_slots][k] keys; the
@@ -3424,7 +3431,7 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac,
                                                                           kScanTaskDocs, nullptr, ctr_ws);
     case kScan16x4W4:
-      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs,
                                                    nullptr, ctr_ws);
     case kScan16x4W4Q2:   // 8 queries per workgroup (2 per wave)
       return launch_scan16x4<4, 2, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
