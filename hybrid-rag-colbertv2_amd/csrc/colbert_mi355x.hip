@@ -3463,6 +3463,15 @@ constexpr int kF8Waves = 8, kF8QW = 8;
 // -> 70.98 ms, B=64 19.19 -> 18.77, B=32 10.26 -> 10.17, B=16 5.73 -> 5.71,
 // B=8 3.73 -> 3.65.
 constexpr int kF8D = 3;
+// Dynamic share of the MXFP8 scans (dyn_frac = kF8DynAuto picks it per shape):
+// the 4-wave shapes hand more of the corpus to the ticket tail.  Lab, same
+// process, 1M docs (profiles/r02s3_lab_dynfrac_f8.log): B=16 (4 x 4, three
+// per CU) 5.99 / 5.61 / 5.55 ms at 0.1 / 0.3 / 0.6; B=32 (4 x 8) 10.39 /
+// 10.20 / 9.96; B=8 (4 x 2) 3.80 / 3.68 / 3.70; the 8 x 8 shape is flat (B=64
+// 19.28-19.32, B=256 73.35-73.44, 1.25M B=256 91.67-91.81) and keeps 0.1.
+constexpr float kF8DynAuto = -1.0f;
+constexpr float kF8DynSmall = 0.6f;   // shapes 7 and 8
+constexpr float kF8DynB8 = 0.3f;      // shape 9
 
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
@@ -3527,17 +3536,19 @@ int scan_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, in
 }
 
 int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
-            float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, int shape = 0, int* ctr_ws = nullptr,
+            float dyn_frac = kF8DynAuto, int task_docs = kScanTaskDocs, int shape = 0, int* ctr_ws = nullptr,
             FusedTopk* ft = nullptr) {
   if (ix->n == 0) return CBV2_OK;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+  const bool auto_frac = dyn_frac < 0.0f;
+  auto frac = [&](float d) { return auto_frac ? d : dyn_frac; };
   if (ix->ld != kLd) {   // long documents: automatic shape only (B <= 8 direct, else 8 waves x 8 queries)
     if (ft != nullptr || shape != 0) return fail(CBV2_EUNSUPPORTED, "long-doc index: automatic scan only");
     return scan_f8_long(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
   }
   if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
-    return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st, dyn_frac,
-                                                                      task_docs, ctr_ws, ft);
+    return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st,
+                                                                      frac(kScanDynFrac), task_docs, ctr_ws, ft);
   if (B > kF8DirectMaxB && shape == 0) shape = pick_shape(kF8Shapes, B);
   if (B <= kF8DirectMaxB && shape == 0) {
     constexpr int QW = 2;
@@ -3560,31 +3571,31 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   // 2-deep (2-4 spill at 8 queries per wave), 6 = 2 with PF, 10 = 9 with
   // three workgroups per CU.
   switch (shape) {
-    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
-    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     case 5: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out,
-                                                                                      st, dyn_frac, task_docs, ctr_ws);
-    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+                                                                                      st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave, three
     // workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two per CU
     // (2 waves per SIMD from independent barrier domains); 9 = 2 queries per
     // wave, two per CU
-    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac,
-                                                                            task_docs, ctr_ws);
-    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac,
-                                                                            task_docs, ctr_ws);
-    case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac,
-                                                                            task_docs, ctr_ws);
+    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                            frac(kF8DynSmall), task_docs, ctr_ws);
+    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                            frac(kF8DynSmall), task_docs, ctr_ws);
+    case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                            frac(kF8DynB8), task_docs, ctr_ws);
 #ifdef CBV2_LAB
-    case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, dyn_frac, task_docs, ctr_ws);
+    case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 11 = shape 5 as it was before the packed scales and D = 3 (round 2)
     case 11: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, 1, false>(ix, Qb, Qs, B, lq, out, ld_out,
-                                                                                     st, dyn_frac, task_docs, ctr_ws);
+                                                                                     st, frac(kScanDynFrac), task_docs, ctr_ws);
 #endif
     default: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out,
-                                                                                         st, dyn_frac, task_docs, ctr_ws);
+                                                                                         st, frac(kScanDynFrac), task_docs, ctr_ws);
   }
 }
 
@@ -3660,7 +3671,7 @@ int scan_maxsim_timed(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, floa
   const bool timed = scan_event_pair(ix, &e0, &e1);
   if (timed && hipEventRecord(e0, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
   const int rc = ix->dtype == CBV2_DTYPE_MXFP8
-                     ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st, kScanDynFrac, kScanTaskDocs, 0, ctr_ws, ft)
+                     ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st, kF8DynAuto, kScanTaskDocs, 0, ctr_ws, ft)
                      : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st, kDefaultScan, ctr_ws, ft);
   // the stop event is recorded even after a failed launch, so the reserved pair stays readable
   if (timed && hipEventRecord(e1, st) != hipSuccess && rc == CBV2_OK) return fail(CBV2_EHIP, "hipEventRecord failed");

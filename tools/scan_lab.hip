@@ -440,6 +440,9 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
   const uint8_t* Qb = (const uint8_t*)Qbuf;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   hipStream_t st = (hipStream_t)stream;
+  // variant 100 * j + shape (j = 1, 2, 3): that shape with a dynamic share of 0.3 j
+  if (variant >= 100) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.3f * (float)(variant / 100), kScanTaskDocs,
+                                     variant % 100);
   if (variant == 1 || (B <= kF8SmallMaxB && variant < 10)) return scan_f8(ix, Qb, B, lq, out, ld, st);
   if (variant == 2) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.0f);  // doc-interleaved, static split only
   if (variant >= 10 && variant <= 30) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
