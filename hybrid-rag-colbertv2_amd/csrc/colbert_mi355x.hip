@@ -3505,7 +3505,7 @@ template <int LD>
 int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                    hipStream_t st, int* ctr_ws) {
   if (B <= kF8SmallMaxB)
-    return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, LD, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, kScanDynFrac,
+    return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, LD, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st, kF8DynB8,
                                                                    kScanTaskDocs, ctr_ws);
   return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, LD, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
                                                                             kScanDynFrac, kScanTaskDocs, ctr_ws);
