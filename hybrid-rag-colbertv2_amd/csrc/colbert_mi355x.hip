@@ -3348,10 +3348,18 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
   return finish_split(ix, sp, st);
 }
 
+// Direct scans (B <= 2): chunks for kDirectOversub x the resident waves (2
+// per SIMD), so workgroups that start late balance the XCDs' clock
+// differences; lab, same process (profiles/r02s3_lab_direct_oversub.log), B=1:
+// 1M docs 5.229 (1x) -> 5.128 (2x) / 5.111 (4x) / 5.169 ms (16x); 100k 0.531
+// -> 0.526 (2x) / 0.535 (4x).  The MXFP8 direct scan stays at 1x (1.25M docs
+// B=1 3.289 vs 3.314 ms at 2x; B=2 2.636 vs 2.672).
+constexpr int kDirectOversub = 2;
+
 template <int QW>
 int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
   const int nq_groups = (B + QW - 1) / QW;
-  const int64_t target_waves = 8LL * cu_count(ix->device);  // 2 waves per SIMD
+  const int64_t target_waves = 8LL * cu_count(ix->device) * kDirectOversub;  // 2 waves per SIMD, oversubscribed
   int64_t n_chunks = target_waves / nq_groups;
   if (n_chunks > ix->n) n_chunks = ix->n;
   if (n_chunks < 1) n_chunks = 1;

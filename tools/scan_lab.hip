@@ -409,8 +409,30 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   return launch_scan16x4<8, 4, 1, 2, 2, false, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr);
 }
 
+// The B <= 2 direct scan with mult x the production chunk count (smaller
+// per-wave chunks: the dispatcher balances late workgroups over the XCDs).
+namespace {
+template <int QW>
+int lab_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
+               int mult) {
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t target_waves = 8LL * cu_count(ix->device) * mult;
+  int64_t n_chunks = target_waves / nq_groups;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  if (n_chunks < 1) n_chunks = 1;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
+  hipLaunchKernelGGL((maxsim_scan_direct_kernel<QW, false>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, kLd);
+  return launch_check("maxsim_scan_direct_kernel");
+}
+}  // namespace
+
 extern "C" int lab_scan(cbv2_index* ix, int variant, const void* Q, int B, int lq, float* out, int64_t ld,
                         void* stream) {
+  if (variant >= 200 && variant < 300)   // 200 + mult: the direct scan (one query per wave) oversubscribed
+    return lab_direct<1>(ix, (const uint16_t*)Q, B, lq, out, ld, (hipStream_t)stream, variant - 200);
   const uint16_t* q = (const uint16_t*)Q;
   hipStream_t st = (hipStream_t)stream;
   switch (variant) {
@@ -440,6 +462,19 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
   const uint8_t* Qb = (const uint8_t*)Qbuf;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   hipStream_t st = (hipStream_t)stream;
+  if (variant >= 200 && variant < 300) {   // 200 + mult: the f8 direct scan (QW = 2) with mult x the resident waves
+    constexpr int QW = 2;
+    const int nq_groups = (B + QW - 1) / QW;
+    int64_t n_chunks = 8LL * cu_count(ix->device) * (variant - 200) / nq_groups;
+    if (n_chunks > ix->n) n_chunks = ix->n;
+    if (n_chunks < 1) n_chunks = 1;
+    const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+    n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+    const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
+    hipLaunchKernelGGL(maxsim_scan_f8_direct_kernel<QW>, dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                       ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld, chunk_docs);
+    return launch_check("maxsim_scan_f8_direct_kernel");
+  }
   // variant 100 * j + shape (j = 1, 2, 3): that shape with a dynamic share of 0.3 j
   if (variant >= 100) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.3f * (float)(variant / 100), kScanTaskDocs,
                                      variant % 100);
