@@ -73,6 +73,7 @@ _SIGS = {
     "cbv2_index_writer_count": (_i64, [_p]),
     "cbv2_index_writer_close": (ctypes.c_int, [_p]),
     "cbv2_comm_init": (ctypes.c_int, [_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbv2_comm_loopback_init": (ctypes.c_int, [_i32, ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_comm_size": (ctypes.c_int, [_p]),
     "cbv2_comm_rank": (ctypes.c_int, [_p]),
     "cbv2_comm_destroy": (ctypes.c_int, [_p]),

@@ -4390,3 +4390,29 @@ int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32
 }
 
 }  // extern "C"
+
+// Test-only (sharded.cpp's loopback communicator): out[i] = max over g of srcs[g][i].
+struct LoopbackSrcs {
+  const float* p[64];
+};
+__global__ void __launch_bounds__(256) loopback_max_kernel(LoopbackSrcs s, int32_t G, int64_t n, float* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float m = s.p[0][i];
+    for (int32_t g = 1; g < G; ++g) m = fmaxf(m, s.p[g][i]);
+    out[i] = m;
+  }
+}
+
+extern "C" int cbv2_loopback_max(const float* const* srcs, int32_t G, int64_t n, float* out, void* stream) {
+  CBV2_REQUIRE(srcs && out, "null pointer");
+  CBV2_REQUIRE(G >= 1 && G <= 64, "G must be in [1, 64]");
+  CBV2_REQUIRE(n >= 1, "n must be >= 1");
+  LoopbackSrcs s{};
+  for (int32_t g = 0; g < G; ++g) {
+    CBV2_REQUIRE(srcs[g], "null source %d", g);
+    s.p[g] = srcs[g];
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(loopback_max_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, G, n, out);
+  return launch_check("loopback_max_kernel");
+}

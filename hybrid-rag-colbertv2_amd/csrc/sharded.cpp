@@ -18,9 +18,13 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
+#include <vector>
 
 #include "colbert_mi355x.h"
 
@@ -56,18 +60,154 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
 struct cbv2_comm {
-  void* nccl = nullptr;  // borrowed ncclComm_t
+  void* nccl = nullptr;  // borrowed ncclComm_t (loopback: this comm's LoopRank)
   void* lib = nullptr;
   AllGatherFn all_gather = nullptr;
   AllReduceFn all_reduce = nullptr;
   ErrStrFn err_str = nullptr;
   int nranks = 0, rank = 0;
+  bool loopback = false;
 };
 
 namespace {
 int nccl_check(const cbv2_comm* c, int rc, const char* what) {
   if (rc == 0) return CBV2_OK;
   return err(CBV2_EHIP, "%s failed (%d): %s", what, rc, c->err_str ? c->err_str(rc) : "rccl error");
+}
+
+// ---------------------------------------------------------------------------
+// Test-only loopback communicator (cbv2_comm_loopback_init): G "ranks" in ONE
+// process and on ONE device, each driven by its own host thread and stream,
+// with collectives that have RCCL's semantics -- every rank must call, the
+// call returns once every rank has enqueued, and no rank's stream runs past
+// the collective before every peer's data is in.  all-gather = G device
+// copies; all-reduce(MAX) = one max kernel over the G send buffers into a
+// scratch, then a copy into the (possibly in-place) receive buffer.  It lets
+// one GPU run cbv2_search_sharded_* / cbv2_rerank_sharded at G = 2..64 on real
+// per-shard data; production code never creates one.
+constexpr int kLoopRcTimeout = 1001, kLoopRcType = 1002, kLoopRcHip = 1003;
+const char* loop_err_str(int rc) {
+  switch (rc) {
+    case kLoopRcTimeout: return "loopback: a peer rank did not reach the collective within 60 s";
+    case kLoopRcType: return "loopback: unsupported datatype / reduction";
+    case kLoopRcHip: return "loopback: HIP call failed";
+    default: return "loopback error";
+  }
+}
+
+struct LoopGroup {
+  int G = 0, refs = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const void*> send;
+  std::vector<hipEvent_t> ready, done;
+  bool broken = false;
+
+  // generation barrier; false on timeout (the group is then broken for good,
+  // so peers fail fast instead of waiting out the timeout one by one)
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const uint64_t gen = generation;
+    if (++arrived == G) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+      return true;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return generation != gen || broken; }) || broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
+
+struct LoopRank {
+  LoopGroup* g = nullptr;
+  int rank = 0;
+  float* scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+
+extern "C" int cbv2_loopback_max(const float* const* srcs, int32_t G, int64_t n, float* out, void* stream);
+
+#define LOOP_HIP(call)                      \
+  do {                                      \
+    if ((call) != hipSuccess) return kLoopRcHip; \
+  } while (0)
+
+// phase 1 (every rank): this rank's send buffer is ready on its stream
+int loop_enter(LoopRank* r, const void* send, hipStream_t st) {
+  LoopGroup* g = r->g;
+  LOOP_HIP(hipEventRecord(g->ready[r->rank], st));
+  g->send[r->rank] = send;
+  return g->barrier() ? 0 : kLoopRcTimeout;
+}
+
+// phase 2 (every rank): this rank's reads of the peers are enqueued; no stream
+// passes the collective until every rank's reads are done (so no rank can
+// overwrite a send buffer a peer is still reading)
+int loop_leave(LoopRank* r, hipStream_t st) {
+  LoopGroup* g = r->g;
+  LOOP_HIP(hipEventRecord(g->done[r->rank], st));
+  if (!g->barrier()) return kLoopRcTimeout;
+  for (int p = 0; p < g->G; ++p) LOOP_HIP(hipStreamWaitEvent(st, g->done[p], 0));
+  return 0;
+}
+
+int loop_all_gather(const void* send, void* recv, size_t count, int dtype, void* comm, hipStream_t st) {
+  auto* r = (LoopRank*)comm;
+  if (dtype != kNcclInt32 && dtype != kNcclFloat32) return kLoopRcType;
+  if (int rc = loop_enter(r, send, st)) return rc;
+  for (int p = 0; p < r->g->G; ++p) {
+    LOOP_HIP(hipStreamWaitEvent(st, r->g->ready[p], 0));
+    LOOP_HIP(hipMemcpyAsync((uint8_t*)recv + (size_t)p * count * 4, r->g->send[p], count * 4,
+                            hipMemcpyDeviceToDevice, st));
+  }
+  return loop_leave(r, st);
+}
+
+int loop_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm, hipStream_t st) {
+  auto* r = (LoopRank*)comm;
+  if (dtype != kNcclFloat32 || op != kNcclMax) return kLoopRcType;
+  if (count * 4 > r->scratch_bytes) {  // test-only code: allocation outside the collective is fine
+    LOOP_HIP(hipStreamSynchronize(st));
+    if (r->scratch) LOOP_HIP(hipFree(r->scratch));
+    r->scratch = nullptr;
+    r->scratch_bytes = 0;
+    LOOP_HIP(hipMalloc(&r->scratch, count * 4));
+    r->scratch_bytes = count * 4;
+  }
+  if (int rc = loop_enter(r, send, st)) return rc;
+  std::vector<const float*> srcs(r->g->G);
+  for (int p = 0; p < r->g->G; ++p) {
+    LOOP_HIP(hipStreamWaitEvent(st, r->g->ready[p], 0));
+    srcs[p] = (const float*)r->g->send[p];
+  }
+  if (cbv2_loopback_max(srcs.data(), r->g->G, (int64_t)count, r->scratch, st)) return kLoopRcHip;
+  if (int rc = loop_leave(r, st)) return rc;
+  LOOP_HIP(hipMemcpyAsync(recv, r->scratch, count * 4, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+void loop_release(LoopRank* r) {
+  LoopGroup* g = r->g;
+  if (r->scratch) (void)hipFree(r->scratch);
+  delete r;
+  bool last;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    last = --g->refs == 0;
+  }
+  if (last) {
+    for (auto e : g->ready) (void)hipEventDestroy(e);
+    for (auto e : g->done) (void)hipEventDestroy(e);
+    delete g;
+  }
 }
 }  // namespace
 
@@ -105,11 +245,48 @@ int cbv2_comm_init(void* nccl_comm, const char* rccl_library, cbv2_comm** out) {
   return CBV2_OK;
 }
 
+int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out) {
+  if (!out) return err(CBV2_EINVAL, "null output array");
+  if (nranks < 1 || nranks > 64) return err(CBV2_EINVAL, "nranks must be in [1, 64] (got %d)", nranks);
+  for (int r = 0; r < nranks; ++r) out[r] = nullptr;
+  auto* g = new LoopGroup;
+  g->G = nranks;
+  g->refs = nranks;
+  g->send.assign(nranks, nullptr);
+  g->ready.assign(nranks, nullptr);
+  g->done.assign(nranks, nullptr);
+  for (int r = 0; r < nranks; ++r) {
+    if (hipEventCreateWithFlags(&g->ready[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming) != hipSuccess) {
+      for (auto e : g->ready) if (e) (void)hipEventDestroy(e);
+      for (auto e : g->done) if (e) (void)hipEventDestroy(e);
+      delete g;
+      return err(CBV2_EHIP, "hipEventCreate failed");
+    }
+  }
+  for (int r = 0; r < nranks; ++r) {
+    auto* lr = new LoopRank;
+    lr->g = g;
+    lr->rank = r;
+    auto* c = new cbv2_comm;
+    c->nccl = lr;
+    c->all_gather = loop_all_gather;
+    c->all_reduce = loop_all_reduce;
+    c->err_str = loop_err_str;
+    c->nranks = nranks;
+    c->rank = r;
+    c->loopback = true;
+    out[r] = c;
+  }
+  return CBV2_OK;
+}
+
 int cbv2_comm_size(const cbv2_comm* c) { return c ? c->nranks : -1; }
 int cbv2_comm_rank(const cbv2_comm* c) { return c ? c->rank : -1; }
 
 int cbv2_comm_destroy(cbv2_comm* c) {
   if (c) {
+    if (c->loopback) loop_release((LoopRank*)c->nccl);
     if (c->lib) dlclose(c->lib);
     delete c;  // the ncclComm_t is borrowed: its owner destroys it
   }

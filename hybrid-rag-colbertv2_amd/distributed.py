@@ -29,6 +29,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .encoder import encode
+
 
 def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
     """Contiguous [begin, end) of global ids owned by ``rank`` (sizes differ by <= 1)."""
@@ -55,10 +57,7 @@ def encode_queries_sharded(encoder, queries, device=None, dtype=torch.bfloat16,
     B = len(queries)
 
     def enc(rows):
-        try:
-            out = encoder.encode(rows, convert_to_tensor=True, is_query=True)
-        except TypeError:                       # encoders without the is_query keyword (FakeEncoder-like)
-            out = encoder.encode(rows, convert_to_tensor=True)
+        out = encode(encoder, rows, is_query=True)
         out = out if isinstance(out, torch.Tensor) else torch.as_tensor(np.asarray(out))
         return out.to(device=device, dtype=dtype) if device is not None else out.to(dtype)
 
@@ -141,6 +140,20 @@ class _PinnedStage:
         return out
 
 
+def loopback_comms(G: int):
+    """TEST-ONLY: ``G`` ``cbv2_comm*`` handles forming one in-process loopback
+    group on the current device (include/colbert_mi355x.h
+    cbv2_comm_loopback_init).  Drive rank r from its own thread and stream
+    (``NativeExchange(shard_r, comm=handles[r])``); the handle is freed by the
+    NativeExchange that adopts it."""
+    import ctypes
+
+    from . import _lib
+    arr = (ctypes.c_void_p * G)()
+    _lib.check(_lib.lib().cbv2_comm_loopback_init(G, arr))
+    return [ctypes.c_void_p(arr[r]) for r in range(G)]
+
+
 class NativeExchange:
     """The exchange inside libcolbert_mi355x.so (include/colbert_mi355x.h:
     cbv2_search_sharded_local/_exchange, cbv2_rerank_sharded) over the RCCL
@@ -148,7 +161,9 @@ class NativeExchange:
     all-gather and merges are all enqueued by C++ on the current stream, with
     no Python between them."""
 
-    def __init__(self, index, group: Optional[dist.ProcessGroup] = None, lexical_k: int = 100):
+    def __init__(self, index, group: Optional[dist.ProcessGroup] = None, lexical_k: int = 100, comm=None):
+        """``comm``: an existing ``cbv2_comm*`` handle to adopt (e.g. one rank of
+        ``loopback_comms``, test-only); default: wrap torch's RCCL communicator."""
         import ctypes
         import os
 
@@ -157,18 +172,22 @@ class NativeExchange:
             raise ValueError("the native exchange scans bf16/MXFP8 shards; an fp32-faithful shard uses the "
                              "torch.distributed exchange (ShardedSearcher(native=False))")
         self.index, self.dev, self.lexical_k = index, index.device, int(lexical_k)
-        pg = group if group is not None else dist.distributed_c10d._get_default_group()
-        if dist.get_backend(pg) != "nccl":
-            raise RuntimeError("the native exchange needs the RCCL ('nccl') backend")
-        warm = torch.zeros(1, device=self.dev)
-        dist.all_reduce(warm, group=group)                 # the communicator exists after one collective
-        torch.cuda.synchronize(self.dev)
-        comm_ptr = pg._get_backend(self.dev)._comm_ptr()
-        rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        h = ctypes.c_void_p()
-        _lib.check(_lib.lib().cbv2_comm_init(comm_ptr, rccl.encode() if os.path.exists(rccl) else None,
-                                             ctypes.byref(h)))
-        self._h, self._lib = h, _lib
+        self._lib = _lib
+        if comm is not None:
+            h = comm
+        else:
+            pg = group if group is not None else dist.distributed_c10d._get_default_group()
+            if dist.get_backend(pg) != "nccl":
+                raise RuntimeError("the native exchange needs the RCCL ('nccl') backend")
+            warm = torch.zeros(1, device=self.dev)
+            dist.all_reduce(warm, group=group)                 # the communicator exists after one collective
+            torch.cuda.synchronize(self.dev)
+            comm_ptr = pg._get_backend(self.dev)._comm_ptr()
+            rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+            h = ctypes.c_void_p()
+            _lib.check(_lib.lib().cbv2_comm_init(comm_ptr, rccl.encode() if os.path.exists(rccl) else None,
+                                                 ctypes.byref(h)))
+        self._h = h
         self._stage = _PinnedStage(slots=4)               # ids + scores per call
         self.world = int(_lib.lib().cbv2_comm_size(h))
         self.rank = int(_lib.lib().cbv2_comm_rank(h))

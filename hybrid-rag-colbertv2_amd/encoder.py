@@ -74,6 +74,26 @@ class FakeEncoder:
         return torch.from_numpy(out) if convert_to_tensor else out
 
 
+def _accepts_keyword(fn, name: str) -> bool:
+    """True when ``fn`` takes ``name`` as a keyword (explicitly or via **kwargs)."""
+    import inspect
+    try:
+        params = inspect.signature(fn).parameters.values()
+    except (TypeError, ValueError):          # builtins / C callables without a signature
+        return False
+    return any(p.kind is p.VAR_KEYWORD or (p.name == name and p.kind is not p.POSITIONAL_ONLY) for p in params)
+
+
+def encode(model, texts, is_query: bool, **kw):
+    """``model.encode(texts, convert_to_tensor=True, **kw)`` as the reference calls it
+    (LRC:735, 758-761, 782-783), adding ``is_query`` only when the encoder's
+    ``encode`` accepts it (jina-colbert's remote code and this package's encoders
+    do; sentence-transformers 2.x's ``encode`` has no ``**kwargs`` and would raise)."""
+    if _accepts_keyword(model.encode, "is_query"):
+        kw["is_query"] = is_query
+    return model.encode(texts, convert_to_tensor=True, **kw)
+
+
 def load_local_encoder(path: str, device: str = "cuda"):
     """The Jina-ColBERT encoder from a LOCAL directory on PyTorch-ROCm.
 

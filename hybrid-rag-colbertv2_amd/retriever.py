@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Sequence, Union
 import torch
 
 from .config import RAGConfig
-from .encoder import load_local_encoder
+from .encoder import encode, load_local_encoder
 from .index import ColbertIndex, IndexBuilder, select_topk
 
 
@@ -53,10 +53,7 @@ class JinaColBERTRetriever:
                                             dtype=getattr(self.config, "index_dtype", "fp32"))
 
     def _encode_docs(self, texts: List[str]):
-        try:
-            return self.model.encode(texts, show_progress_bar=False, convert_to_tensor=True, is_query=False)
-        except TypeError:                         # encoders without the is_query keyword
-            return self.model.encode(texts, show_progress_bar=False, convert_to_tensor=True)
+        return encode(self.model, texts, is_query=False, show_progress_bar=False)
 
     def index(self, corpus: List[str], batch_size: Optional[int] = None) -> None:
         """LRC:728-746: encode the corpus, keep it in HBM, persist it.
@@ -146,7 +143,7 @@ class JinaColBERTRetriever:
 
     # ------------------------------------------------------------ encoding
     def _encode_query(self, query: Union[str, torch.Tensor]) -> torch.Tensor:
-        q = query if isinstance(query, torch.Tensor) else self.model.encode(query, convert_to_tensor=True, is_query=True)
+        q = query if isinstance(query, torch.Tensor) else encode(self.model, query, is_query=True)
         if q.dim() == 1:
             q = q.unsqueeze(0)
         return q
@@ -176,7 +173,7 @@ class JinaColBERTRetriever:
         if not documents:
             return []
         q = self._encode_query(query)
-        d = self.model.encode(documents, convert_to_tensor=True, is_query=False)
+        d = encode(self.model, documents, is_query=False)
         tmp = self._build(d)
         kk = min(k, len(documents))
         if self.scorer == "maxsim":

@@ -421,6 +421,18 @@ int cbv2_rerank_sharded(cbv2_index* index, cbv2_comm* comm, const void* Q, int32
                         const int32_t* cand, int32_t C, int32_t k, void* workspace, size_t workspace_bytes,
                         float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
 
+/* TEST-ONLY -- not for production use.  cbv2_comm_loopback_init writes
+ * `nranks` (1..64) communicator handles out[0..nranks) that form ONE group
+ * inside this process, on the current device: rank r is driven by its own
+ * host thread and stream, and the collectives the calls above use keep RCCL's
+ * semantics (every rank calls; a call returns once every rank has enqueued;
+ * no rank's stream passes the collective before all peers' data is in):
+ * all-gather = device copies of the G send blocks, all-reduce(MAX) = a max
+ * kernel over them.  It exercises the sharded exchange at G > 1 on one GPU.
+ * A rank that does not reach a collective within 60 s fails the group.
+ * Free each handle with cbv2_comm_destroy.                                  */
+int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
+
 #ifdef __cplusplus
 }
 #endif

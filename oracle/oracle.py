@@ -20,6 +20,10 @@ reference line it follows (LRC = /root/reference/local_rag_complete.py):
   split_f32 /       the fp32-faithful index (LRC:735-746 keeps fp32 embeddings):
   band_beta         hi/lo split and the bound |T - S| <= beta(q) the faithful
                     search's band rests on
+  codebook_*        maxsim + topk for corpora whose tokens are rows of a small
+                    codebook: max_t <q, d_t> is the max over the doc's code SET,
+                    so a 1M-doc corpus is scored exactly in seconds (checked
+                    against maxsim itself in tests/test_oracle_golden.py)
 
 Pinning: meanpool_cosine, rrf and the search/rerank
 dict pipeline are checked against golden vectors produced by the reference's
@@ -312,6 +316,10 @@ def c_lib():
         L.oracle_maxsim_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
         L.oracle_topk.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_codebook_topk.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]
         _CLIB = L
     return _CLIB
 
@@ -336,3 +344,60 @@ def c_topk(scores_row: np.ndarray, k: int) -> np.ndarray:
     vals = np.empty(k, np.float64)
     c_lib().oracle_topk(s.ctypes.data, len(s), k, vals.ctypes.data, ids.ctypes.data)
     return ids
+
+
+# ------------------------------------------------------------------ codebook corpora (exact 1M-doc parity)
+def codebook_masks(codes: np.ndarray, doclens: np.ndarray, chunk: int = 65536) -> np.ndarray:
+    """codes uint8 [n, L] (codebook row of every token slot), doclens [n] -> uint32 [n]:
+    bit c set when code c fills one of doc n's scoring rows (t < doclens[n])."""
+    codes = np.asarray(codes)
+    doclens = np.asarray(doclens)
+    n, L = codes.shape
+    out = np.empty(n, np.uint32)
+    t = np.arange(L)[None, :]
+    for a in range(0, n, chunk):
+        c = codes[a:a + chunk].astype(np.uint32)
+        bits = np.where(t < doclens[a:a + chunk, None], np.left_shift(np.uint32(1), c), np.uint32(0))
+        out[a:a + chunk] = np.bitwise_or.reduce(bits, axis=1)
+    return out
+
+
+def codebook_table(Q: np.ndarray, codebook: np.ndarray) -> np.ndarray:
+    """T[b, q, c] = <Q[b, q], code_c> in float64: [B, lq, K]."""
+    return np.einsum("bqd,cd->bqc", np.asarray(Q, np.float64), np.asarray(codebook, np.float64))
+
+
+def codebook_maxsim(T: np.ndarray, masks: np.ndarray) -> np.ndarray:
+    """maxsim() for codebook docs given by their code sets: [B, n] float64
+    (sum over q of the max over the doc's codes; an empty set scores -inf)."""
+    T = np.asarray(T, np.float64)
+    K = T.shape[2]
+    bits = ((np.asarray(masks, np.uint64)[:, None] >> np.arange(K, dtype=np.uint64)) & 1).astype(bool)   # [n, K]
+    v = np.where(bits[None, None], T[:, :, None, :], -np.inf).max(axis=3)                               # [B, lq, n]
+    return v.sum(axis=1)
+
+
+def codebook_topk(T: np.ndarray, masks: np.ndarray, k: int, over_ids=None, over_scores=None):
+    """Top-k (score desc, id asc) of maxsim over a codebook corpus of n = len(masks)
+    docs (C: oracle_codebook_topk).  over_ids [P] / over_scores [B, P]: docs whose
+    scores the caller computed itself (planted docs with non-codebook tokens).
+    -> (scores float64 [B, k], ids int64 [B, k])."""
+    T = np.ascontiguousarray(T, np.float64)
+    B, lq, K = T.shape
+    assert K <= 32
+    umask, inv = np.unique(np.asarray(masks, np.uint32), return_inverse=True)
+    umask = np.ascontiguousarray(umask, np.uint32)
+    inv = np.ascontiguousarray(inv.reshape(-1), np.int32)
+    n = len(inv)
+    over_idx = np.full(n, -1, np.int32)
+    if over_ids is not None and len(over_ids):
+        over_idx[np.asarray(over_ids, np.int64)] = np.arange(len(over_ids), dtype=np.int32)
+        over = np.ascontiguousarray(over_scores, np.float64).reshape(B, len(over_ids))
+    else:
+        over = np.zeros((B, 1), np.float64)
+    vals = np.empty((B, k), np.float64)
+    ids = np.empty((B, k), np.int64)
+    c_lib().oracle_codebook_topk(T.ctypes.data, B, lq, K, umask.ctypes.data, len(umask), inv.ctypes.data,
+                                 over_idx.ctypes.data, over.ctypes.data, over.shape[1], n, int(k),
+                                 vals.ctypes.data, ids.ctypes.data)
+    return vals, ids

@@ -66,6 +66,35 @@ def test_c1_literal_search_rerank_retrieve_match_reference(dev, tmp_path):
             assert abs(f["score"] - x["score"]) < 1e-5
 
 
+class StrictEncoder:
+    """sentence-transformers 2.x ``encode`` signature: no ``is_query``, no ``**kwargs``."""
+
+    def __init__(self, **kw):
+        self.fe = FakeEncoder(**kw)
+
+    def encode(self, sentences, batch_size=32, show_progress_bar=None, output_value="sentence_embedding",
+               convert_to_numpy=True, convert_to_tensor=False, device=None, normalize_embeddings=False):
+        return self.fe.encode(sentences, convert_to_tensor=convert_to_tensor)
+
+
+@pytest.mark.parametrize("scorer", ["maxsim", "ref_meanpool_cosine"])
+def test_strict_signature_encoder_through_search_rerank_retrieve(dev, tmp_path, scorer):
+    """LRC:758-761 / 782-783 call ``encode(x, convert_to_tensor=True)`` only: an
+    encoder without ``is_query`` / ``**kwargs`` must work in index, search,
+    rerank and retrieve, with results equal to the keyword-tolerant encoder's."""
+    cfg, ind, hyb = _system(tmp_path / "a", scorer)
+    cfg2 = RAGConfig(scorer=scorer, colbert_index_path=str(tmp_path / "b"), index_dtype="bf16")
+    ind2 = DualIndexer(cfg2, encoder=StrictEncoder(**TOY["encoder"]))
+    ind2.colbert_retriever.index(TOY["corpus"])
+    ind2.bm25_retriever = RecordedBM25()
+    hyb2 = HybridRetriever(cfg2, ind2, hyb.db_session, verbose=False)
+    for q in TOY["queries"]:
+        assert ind2.colbert_retriever.search(q, k=10) == ind.colbert_retriever.search(q, k=10)
+        docs = TOY["corpus"][1:40:4]
+        assert ind2.colbert_retriever.rerank(q, docs, k=5) == ind.colbert_retriever.rerank(q, docs, k=5)
+        assert hyb2.retrieve(q) == hyb.retrieve(q)
+
+
 def test_literal_maxsim_score_shapes_match_reference(dev, tmp_path):
     cfg = RAGConfig(scorer="ref_meanpool_cosine")
     from hybrid_rag_colbertv2_amd.retriever import JinaColBERTRetriever

