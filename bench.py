@@ -62,6 +62,7 @@ PEAK_FP8_TFLOPS = 5000.0                   # MI355X dense fp8 (block-scaled MFMA
 FLOP_PER_PAIR = 2 * LQ * LD * DIM          # 1,048,576 algorithmic FLOP per (query, doc)
 PEAK_BF16_TFLOPS = 2500.0                  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+JSON_FD = 1                                # set in main(): the real stdout, for the JSON line only
 SCAN_KERNEL = "maxsim_scan16x4_kernel"    # the B=256 scan (auto dispatch: doc-interleaved tiles, 32 queries / workgroup)
 
 
@@ -154,11 +155,14 @@ def cpu_baseline(Q: torch.Tensor, tokens: torch.Tensor, n_total: int, budget_s: 
             "omp_num_threads": info["omp_num_threads"], "rows": rows}
 
 
-def timed_steps(run_steps, K, W, world):
+def timed_steps(run_steps, K, W, world, on_start=None):
     """W untimed warmup steps, then EXACTLY K steps bracketed by barrier + sync on
-    both sides; returns (outputs, max-over-ranks elapsed seconds)."""
+    both sides; returns (outputs, max-over-ranks elapsed seconds).  on_start()
+    runs after the warmup, before the timed region (arms measurement records)."""
     if W:
         run_steps(W)
+    if on_start is not None:
+        on_start()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -174,6 +178,16 @@ def timed_steps(run_steps, K, W, world):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     return outs, elapsed
+
+
+def gather_floats(vals, world, dev, backend):
+    """Every rank's list of floats (same length on every rank) -> [rank][i] on all ranks."""
+    if world == 1:
+        return [list(vals)]
+    t = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
 
 
 def spot_check(fs, fi_h, Qd, docs_fn, begin, end, queries, tol, world, dev):
@@ -219,6 +233,11 @@ def main():
                     help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
                          "(bf16 hi scanned + residual-certified band, DESIGN 3.12)")
     args = ap.parse_args()
+    # stdout carries exactly the ONE JSON line: everything else any layer prints
+    # to fd 1 (Python, RCCL / gloo C++ logging) is sent to stderr from here on
+    global JSON_FD
+    JSON_FD = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -287,7 +306,9 @@ def main():
         return lambda K: pipe.run([(Qb, bm_all)] * K)
 
     ix.time_scans(True)      # HIP events around each scan launch, on its own stream (C ABI)
-    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world)
+    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world,
+                                on_start=lambda: searcher.time_collectives(True))
+    coll = searcher.collective_times()                  # the K timed steps' all-gathers / all-reduces
     scan_ms = ix.scan_times()                           # the warmup + K scans; keep the K of the timed region
     scan_ms = scan_ms[-args.steps:] if len(scan_ms) >= args.steps else scan_ms
     qps = B * args.steps / elapsed
@@ -334,7 +355,7 @@ def main():
     fused_topk = ix.fused_topk_slots(B, args.k) > 0
     # HBM bytes per launch from the committed PMC passes of the same kernel and
     # shape (tools/profile_round.sh -> tools/pmc_summary.py); null otherwise
-    traffic = clock = None
+    traffic = clock = traffic_src = None
     pmc = os.path.join(ROOT, "profiles", "pmc_scan.json")
     want = "maxsim_scan_f8x4_kernel" if args.dtype == "fp8" else SCAN_KERNEL
     variant = "fused" if fused_topk else "unfused"
@@ -345,6 +366,22 @@ def main():
             if (d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == want
                     and d.get("variant", "unfused") == variant):
                 traffic, clock = d.get("hbm_bytes_per_launch"), d.get("clock_ghz")
+                traffic_src = (f"committed PMC pass profiles/pmc_scan.json ({want}, {variant}, batch {B}, "
+                               f"{n_local} docs/GPU, one MI355X), not this run")
+    # every rank's scan time and collective time per step (max-over-ranks view of N > 1)
+    names = ("all_gather", "all_reduce_max")
+    mine = [scan_avg] + [coll.get(k, {}).get(f, 0.0) / args.steps for k in names for f in ("device_ms", "host_ms")] \
+        + [coll.get(k, {}).get("calls", 0) / args.steps for k in names]
+    per_rank = gather_floats(mine, world, dev, backend)
+    collectives = None
+    if world > 1:
+        collectives = {k: {"calls_per_step": per_rank[0][5 + j],
+                           "device_ms_per_step_max": round(max(r[1 + 2 * j] for r in per_rank), 4),
+                           "host_ms_per_step_max": round(max(r[2 + 2 * j] for r in per_rank), 4),
+                           "device_ms_per_step_by_rank": [round(r[1 + 2 * j], 4) for r in per_rank]}
+                       for j, k in enumerate(names)}
+        collectives["timing"] = ("HIP events on the issuing stream (device_ms; RCCL) and host wall time of "
+                                 "the call (host_ms; gloo blocks the host), summed per step over the K timed steps")
 
     # ---- spot parity: oracle MaxSim of the final candidates, on the owning rank
     check_rows = list(range(min(args.check_queries, B)))
@@ -453,7 +490,11 @@ def main():
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
             "roofline": {"bound": "mfma", "kernel": want, "variant": variant, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "traffic": traffic, "avg_ms": round(scan_avg, 3), "launches_timed": len(scan_ms),
+                         "traffic": traffic, "traffic_source": traffic_src, "avg_ms": round(scan_avg, 3),
+                         "launches_timed": len(scan_ms),
+                         "avg_ms_by_rank": [round(r[0], 3) for r in per_rank],
+                         "avg_ms_min_max": [round(min(r[0] for r in per_rank), 3),
+                                            round(max(r[0] for r in per_rank), 3)],
                          "clock_ghz_under_load": round(clock, 3) if clock else None},
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad,
@@ -465,7 +506,9 @@ def main():
             line["faithful"] = fleg
         if native is not None:
             line["native_exchange"] = native
-        print(json.dumps(line), flush=True)
+        if collectives is not None:
+            line["collectives"] = collectives
+        os.write(JSON_FD, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

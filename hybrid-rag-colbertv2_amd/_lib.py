@@ -28,6 +28,7 @@ _p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_
 _SIGS = {
     "cbv2_abi_version": (ctypes.c_int, []),
     "cbv2_last_error": (ctypes.c_char_p, []),
+    "cbv2_build_stamp": (ctypes.c_char_p, []),
     "cbv2_index_create": (ctypes.c_int, [ctypes.c_int, _p, _i32, _i64, _i32, _i32, _p, _i64,
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_index_destroy": (ctypes.c_int, [_p]),
@@ -106,8 +107,13 @@ def header_symbols(path: str = HEADER):
 def lib():
     global _lib
     if _lib is None:
+        from . import _build
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        want, have = _build.source_stamp(), _build.library_stamp(LIB_PATH)
+        if have != want:     # never run a library built from other sources than the tree's
+            raise RuntimeError(f"{LIB_PATH} was built from other sources (stamp {have}, sources {want}): "
+                               "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)

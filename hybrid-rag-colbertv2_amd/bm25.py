@@ -285,19 +285,33 @@ class HostBM25:
         return ids.astype(np.int64), sc
 
     # ---------------------------------------------------------------- persistence
+    FORMAT = 2     # 2: vocabulary of stemmed tokens (bm25s' stopwords + Snowball English)
+
     def save(self, path: str) -> None:
         os.makedirs(path, exist_ok=True)
         np.savez(os.path.join(path, "bm25_corpus.npz"), terms=self._corpus[0], offsets=self._corpus[1])
         with open(os.path.join(path, "bm25.json"), "w") as f:
-            json.dump({"vocab": self.vocab, "n_docs": self.n_docs, "k1": self.k1, "b": self.b,
+            json.dump({"format": self.FORMAT, "vocab": self.vocab, "n_docs": self.n_docs, "k1": self.k1, "b": self.b,
                        "stopwords": self.stopwords if isinstance(self.stopwords, (str, bool)) or self.stopwords is None
-                       else list(self.stopwords), "stemmer": "english"}, f)
+                       else list(self.stopwords), "stemmer": getattr(self.stemmer, "algorithm", "custom")}, f)
 
     @classmethod
-    def load(cls, path: str) -> "HostBM25":
+    def load(cls, path: str, stemmer: Optional[Stemmer] = None) -> "HostBM25":
+        """Reads what ``save`` wrote.  The query tokens must be stemmed as the
+        vocabulary was, so a file without the format/stemmer record (written by
+        an older, unstemmed tokenizer) is refused rather than silently matching
+        nothing; a "custom" stemmer must be passed in again."""
         with open(os.path.join(path, "bm25.json")) as f:
             meta = json.load(f)
-        self = cls(meta["k1"], meta["b"], stopwords=meta.get("stopwords", "en"))
+        if meta.get("format") != cls.FORMAT or "stemmer" not in meta:
+            raise ValueError(f"{path}/bm25.json has format {meta.get('format')!r} (need {cls.FORMAT}, with its "
+                             "stemmer recorded): rebuild the BM25 index")
+        if meta["stemmer"] == "custom":
+            if stemmer is None:
+                raise ValueError(f"{path}/bm25.json was built with a custom stemmer: pass it to load()")
+        elif stemmer is None:
+            stemmer = Stemmer(meta["stemmer"])
+        self = cls(meta["k1"], meta["b"], stemmer=stemmer, stopwords=meta.get("stopwords", "en"))
         self.vocab, self.n_docs = meta["vocab"], meta["n_docs"]
         z = np.load(os.path.join(path, "bm25_corpus.npz"))
         self._corpus = (z["terms"], z["offsets"])

@@ -3854,6 +3854,13 @@ int cbv2_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 int cbv2_abi_version(void) { return CBV2_ABI_VERSION; }
 
+// _build.py passes -DCBV2_BUILD_STAMP="<sha256 prefix of the sources + flags>"; the
+// prefix makes the stamp findable in the .so's bytes without loading it.
+#ifndef CBV2_BUILD_STAMP
+#define CBV2_BUILD_STAMP "unstamped"
+#endif
+const char* cbv2_build_stamp(void) { return "cbv2-build-stamp:" CBV2_BUILD_STAMP; }
+
 const char* cbv2_last_error(void) { return g_err; }
 
 int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, int32_t ld, int32_t d,

@@ -455,11 +455,12 @@ int cbv2_index_writer_close(cbv2_index_writer* w) {
   int rc = CBV2_OK;
   if (w->fd >= 0) {
     if (w->written != w->h.n)
-      rc = err(CBV2_EINVAL, "%s: closed after %lld of %lld docs (left without a header)", w->path,
+      rc = err(CBV2_EINVAL, "%s: closed after %lld of %lld docs (partial file removed)", w->path,
                (long long)w->written, (long long)w->h.n);
     else if (pwrite_full(w->fd, &w->h, sizeof(w->h), 0) || fsync(w->fd) != 0)
-      rc = err(CBV2_EINVAL, "%s: header write failed", w->path);
+      rc = err(CBV2_EINVAL, "%s: header write failed (file removed)", w->path);
     close(w->fd);
+    if (rc != CBV2_OK) unlink(w->path);  // never leave a full-size file without a valid header behind
   }
   delete w;
   return rc;

@@ -267,13 +267,53 @@ class ShardedSearcher:
         self.world = world
         # native=True: the whole exchange runs inside the C ABI (NativeExchange)
         self._nx = NativeExchange(local, group, lexical_k) if native else None
+        self._coll = None          # collective timing record (time_collectives)
+
+    # ------------------------------------------------------------ measurement
+    def time_collectives(self, enable: bool) -> None:
+        """Record every collective this searcher issues from now on: HIP events on
+        the current stream around it (device time, for RCCL) and the host wall
+        time of the call (for gloo, whose collectives block the host)."""
+        self._coll = [] if enable else None
+
+    def collective_times(self) -> dict:
+        """{name: {"calls", "device_ms", "host_ms"}} summed over the recorded calls
+        (synchronises); the record is cleared."""
+        rec, self._coll = self._coll or [], None
+        out = {}
+        for name, e0, e1, host_ms in rec:
+            e1.synchronize()
+            d = out.setdefault(name, {"calls": 0, "device_ms": 0.0, "host_ms": 0.0})
+            d["calls"] += 1
+            d["device_ms"] += e0.elapsed_time(e1) if e0 is not None else 0.0
+            d["host_ms"] += host_ms
+        return out
+
+    def _collective(self, name: str, fn, device):
+        if self._coll is None:
+            return fn()
+        import time
+        cuda = torch.device(device).type == "cuda"
+        e0 = e1 = None
+        if cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        t0 = time.perf_counter()
+        r = fn()
+        host_ms = (time.perf_counter() - t0) * 1e3
+        if cuda:
+            e1.record()
+        self._coll.append((name, e0, e1, host_ms))
+        return r
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            self._collective("all_gather", lambda: dist.all_gather_into_tensor(out, t.contiguous(), group=self.group),
+                             t.device)
         else:
-            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=self.group)
+            self._collective("all_gather", lambda: dist.all_gather(list(out.unbind(0)), t.contiguous(),
+                                                                   group=self.group), t.device)
         return out
 
     def _local_search(self, Q: torch.Tensor, k: int):
@@ -347,5 +387,6 @@ class ShardedSearcher:
         if self.world == 1:
             return self.local.rerank(Q, cand, k)                                           # fused select
         raw = self.local.rerank(Q, cand, 0)                                                # [B, C]
-        dist.all_reduce(raw, op=dist.ReduceOp.MAX, group=self.group)
+        self._collective("all_reduce_max", lambda: dist.all_reduce(raw, op=dist.ReduceOp.MAX, group=self.group),
+                         raw.device)
         return self.ops.select(raw, k, ids=cand)

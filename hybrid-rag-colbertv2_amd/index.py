@@ -247,6 +247,9 @@ class ColbertIndex:
         their ld (the file header records it)."""
         dt = _lib.DTYPE_MXFP8 if self.fp8 else _lib.DTYPE_BF16
         torch.cuda.current_stream(self.device).synchronize()
+        for side in (path + ".bounds.json", path + ".resid"):   # sidecars of an earlier save at this path
+            if os.path.exists(side):
+                os.unlink(side)
         _lib.check(_lib.lib().cbv2_index_file_write_ld(
             os.fsencode(path), dt, self.n, self.ld, self.tokens.data_ptr(),
             self.scales.data_ptr() if self.fp8 else None, self.doclens.data_ptr(), self.id_base,
@@ -255,8 +258,10 @@ class ColbertIndex:
             _lib.check(_lib.lib().cbv2_index_file_write_ld(
                 os.fsencode(path + ".resid"), _lib.DTYPE_BF16, self.n, self.ld, self.residual.data_ptr(), None,
                 self.doclens.data_ptr(), self.id_base, _stream_ptr(self.device)))
+            # written last: the bounds name the exact hi / residual files they belong to
             with open(path + ".bounds.json", "w") as f:
-                json.dump({"resid_max": self.bounds[0], "norm_max": self.bounds[1]}, f)
+                json.dump({"resid_max": self.bounds[0], "norm_max": self.bounds[1],
+                           "hi": file_fingerprint(path), "resid": file_fingerprint(path + ".resid")}, f)
 
     @classmethod
     def load(cls, path: str, device="cuda", begin: int = 0, end: Optional[int] = None) -> "ColbertIndex":
@@ -280,16 +285,17 @@ class ColbertIndex:
                 _stream_ptr(device)))
         if not fp8 and os.path.exists(path + ".resid") and os.path.exists(path + ".bounds.json"):
             # fp32-faithful: the residual file's same doc range, and the split's bounds
-            if index_file_layout(path + ".resid")[1:] != (n, id_base, ld):
-                raise ValueError(f"{path}.resid does not match {path}")
+            with open(path + ".bounds.json") as f:
+                b = json.load(f)
+            if index_file_layout(path + ".resid")[1:] != (n, id_base, ld) or \
+                    b.get("hi") != file_fingerprint(path) or b.get("resid") != file_fingerprint(path + ".resid"):
+                raise ValueError(f"{path}.resid / .bounds.json were not written with {path}")
             resid = torch.empty((m, ld, DIM), dtype=torch.bfloat16, device=device)
             dl2 = torch.empty((m,), dtype=torch.int32, device=device)
             with torch.cuda.device(device):
                 _lib.check(_lib.lib().cbv2_index_file_read(
                     os.fsencode(path + ".resid"), begin, end, resid.data_ptr() if m else None, None,
                     dl2.data_ptr() if m else None, _stream_ptr(device)))
-            with open(path + ".bounds.json") as f:
-                b = json.load(f)
             if not torch.equal(dl2, doclens):
                 raise ValueError(f"{path}.resid does not match {path}")
             return cls(tokens, doclens, id_base=id_base + begin, residual=resid,
@@ -689,6 +695,22 @@ class IndexWriter:
 
 
 # --------------------------------------------------------------------- free functions
+def file_fingerprint(path: str, span: int = 4 << 20) -> str:
+    """Identity of a native index file as written: its size and a CRC-32 of its
+    first and last ``span`` bytes (the header, the doclens and the edge docs'
+    tokens).  An fp32-faithful save records the hi and residual files'
+    fingerprints in ``.bounds.json``, so a load never pairs a residual with
+    another save's tokens."""
+    import zlib
+    size = os.path.getsize(path)
+    with open(path, "rb") as f:
+        crc = zlib.crc32(f.read(span))
+        if size > span:
+            f.seek(max(span, size - span))
+            crc = zlib.crc32(f.read(span), crc)
+    return f"{size}:{crc:08x}"
+
+
 def index_file_info(path: str):
     """(ABI dtype, doc count, id_base) of a native index file."""
     dt, n, base = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()

@@ -63,14 +63,18 @@ class JinaColBERTRetriever:
         128 tokens).  Here the corpus is encoded ``config.ingest_batch`` docs at a
         time and each batch goes straight into the HBM index (cast / quantised
         / split on the GPU: ``IndexBuilder``), so host memory stays bounded.
-        Persistence: a corpus of at most ``config.index_pt_max_docs`` docs is
-        also saved as the reference's ``index.pt`` (its fp32 embeddings, kept
+        Persistence: a corpus of at most ``config.index_pt_max_docs`` docs (and
+        any corpus of the literal scorer, whose means need the fp32 embeddings)
+        is also saved as the reference's ``index.pt`` (its fp32 embeddings, kept
         per batch on the host); a larger one as the native ``index.cbv2``
-        (streamed from HBM through pinned buffers) + ``index.corpus.json``."""
+        (streamed from HBM through pinned buffers) + ``index.corpus.json``.
+        Writing one format deletes the other's files from the directory, so
+        ``load()`` always serves the latest ``index()``."""
         self.corpus = corpus
         n = len(corpus)
         bs = int(batch_size or getattr(self.config, "ingest_batch", 256))
-        keep_pt = n <= int(getattr(self.config, "index_pt_max_docs", 50_000))
+        # the literal scorer needs the fp32 embeddings back at load(); only index.pt holds them
+        keep_pt = n <= int(getattr(self.config, "index_pt_max_docs", 50_000)) or self.scorer == "ref_meanpool_cosine"
         dtype = getattr(self.config, "index_dtype", "fp32")
         print(f"  Encoding {n} documents...")
         if self.scorer == "ref_meanpool_cosine" or n == 0:
@@ -97,8 +101,19 @@ class JinaColBERTRetriever:
                 saved = [e for h in host for e in (h if isinstance(h, list) else list(h.unbind(0)))]
             torch.save({"embeddings": saved, "corpus": corpus},
                        os.path.join(self.config.colbert_index_path, "index.pt"))
+            self._remove_native()
         else:
             self.save_native()
+            pt = os.path.join(self.config.colbert_index_path, "index.pt")
+            if os.path.exists(pt):      # an earlier, smaller corpus: load() must not serve it
+                os.unlink(pt)
+
+    def _remove_native(self) -> None:
+        """Delete the native index files an earlier index() left in the index directory."""
+        path = self._native_path()
+        for f in (path, path + ".resid", path + ".bounds.json", os.path.splitext(path)[0] + ".corpus.json"):
+            if os.path.exists(f):
+                os.unlink(f)
 
     def load(self) -> None:
         """LRC:748-753 (reads the reference's own index.pt format; never unpickles code).

@@ -67,6 +67,10 @@ typedef struct cbv2_index cbv2_index;
 /* Library / error reporting ------------------------------------------------ */
 int cbv2_abi_version(void);
 const char* cbv2_last_error(void);
+/* "cbv2-build-stamp:<hex>": a content hash of the sources and compiler flags
+ * the library was built from (build provenance; the Python loader refuses a
+ * library whose stamp differs from the tree's sources).                     */
+const char* cbv2_build_stamp(void);
 
 /* Index handle --------------------------------------------------------------
  * Replaces the tensor the reference keeps in `self.corpus_embeddings`
@@ -365,7 +369,9 @@ int cbv2_index_file_read_host(const char* path, int64_t begin, int64_t end, void
  * doc count, append contiguous batches (DEVICE pointers with on_device = 1 --
  * D2H through 64 MiB pinned buffers on `stream` -- or HOST pointers), close.
  * The header is written by close() only when every declared doc was
- * appended, so an interrupted ingest never leaves a file that reads as valid.
+ * appended; close() after an incomplete ingest (or a failed header write)
+ * deletes the file and returns CBV2_EINVAL, so an interrupted ingest never
+ * leaves a file behind, valid-looking or not.
  * Host memory is two staging buffers whatever the corpus size.             */
 typedef struct cbv2_index_writer cbv2_index_writer;
 int cbv2_index_writer_open(const char* path, int32_t dtype, int64_t n, int64_t id_base, cbv2_index_writer** out);

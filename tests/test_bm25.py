@@ -129,8 +129,25 @@ def test_hostbm25_text_roundtrip(tmp_path):
     assert ids[0][0] == 2
     bm.save(str(tmp_path))
     bm2 = HostBM25.load(str(tmp_path))
+    assert bm2.stemmer.algorithm == "english"
     ids2, sc2 = bm2.retrieve(bm2.tokenize("quick dog"), k=5)
     assert np.array_equal(ids, ids2) and np.array_equal(sc, sc2)
+    # a bm25.json of the earlier, unstemmed tokenizer (no format / stemmer record) is refused
+    import json
+    meta = json.load(open(tmp_path / "bm25.json"))
+    for drop in ("format", "stemmer"):
+        old = {k: v for k, v in meta.items() if k != drop}
+        json.dump(old, open(tmp_path / "bm25.json", "w"))
+        with pytest.raises(ValueError, match="rebuild the BM25 index"):
+            HostBM25.load(str(tmp_path))
+    # a custom stemmer is recorded as such and must be passed back in
+    bm3 = HostBM25(stemmer=type("S", (), {"stemWords": lambda self, w: [x[:4] for x in w]})())
+    bm3.index(bm3.tokenize(corpus))
+    bm3.save(str(tmp_path / "c"))
+    with pytest.raises(ValueError, match="custom stemmer"):
+        HostBM25.load(str(tmp_path / "c"))
+    bm4 = HostBM25.load(str(tmp_path / "c"), stemmer=bm3.stemmer)
+    assert np.array_equal(bm4.retrieve(bm4.tokenize("quick dog"), 3)[0], bm3.retrieve(bm3.tokenize("quick dog"), 3)[0])
 
 
 def test_native_bm25_repeated_query_terms():

@@ -106,3 +106,55 @@ def test_1m_ingest_bounded_host_memory(dev):
     # the same tokens as the one-shot generator, on a slice
     ref, _ = synth.make_shard(123_456, 123_456 + 3000, Qf, planted, dev)
     assert torch.equal(ix.tokens[123_456:126_456], ref)
+
+
+def test_reindex_same_directory_serves_latest_format(dev, tmp_path):
+    """index() writes ONE persistence format and deletes the other's
+    files, so load() after re-indexing never serves an earlier corpus."""
+    small = [f"small doc {i} topic {i % 5}" for i in range(40)]
+    large = [f"large doc {i} topic {i % 9}" for i in range(300)]
+    cfg = RAGConfig(colbert_index_path=str(tmp_path / "ix"), index_pt_max_docs=100, index_dtype="bf16")
+    d = tmp_path / "ix"
+    for corpus, fmt in ((small, "pt"), (large, "cbv2"), (small, "pt")):
+        r = JinaColBERTRetriever(cfg, encoder=FakeEncoder())
+        r.index(corpus)
+        assert (d / "index.pt").exists() == (fmt == "pt")
+        assert (d / "index.cbv2").exists() == (fmt == "cbv2")
+        assert (d / "index.corpus.json").exists() == (fmt == "cbv2")
+        want = r.search("doc 7 topic 2", k=5)
+        r2 = JinaColBERTRetriever(cfg, encoder=FakeEncoder())
+        r2.load()
+        assert r2.corpus == corpus and r2.search("doc 7 topic 2", k=5) == want
+    # the literal scorer always keeps index.pt (its means need the fp32 embeddings)
+    lit = RAGConfig(colbert_index_path=str(tmp_path / "lit"), index_pt_max_docs=100, scorer="ref_meanpool_cosine")
+    r = JinaColBERTRetriever(lit, encoder=FakeEncoder())
+    r.index(large)
+    assert (tmp_path / "lit" / "index.pt").exists() and not (tmp_path / "lit" / "index.cbv2").exists()
+    r2 = JinaColBERTRetriever(lit, encoder=FakeEncoder())
+    r2.load()
+    assert r2.search("doc 7 topic 2", k=5) == r.search("doc 7 topic 2", k=5)
+
+
+def test_faithful_sidecars_never_pair_with_other_tokens(dev, tmp_path):
+    """a bf16 save over a faithful file removes its .resid /
+    .bounds.json; sidecars copied from another save are refused on load."""
+    import shutil
+    a = ColbertIndex.from_embeddings(_embs(11, 50, ragged=False), device=dev, dtype="fp32")
+    b = ColbertIndex.from_embeddings(_embs(12, 50, ragged=False), device=dev, dtype="fp32")
+    p = str(tmp_path / "f.cbv2")
+    a.save(p)
+    assert ColbertIndex.load(p, device=dev).faithful
+    shutil.copy(p + ".resid", tmp_path / "a.resid")
+    shutil.copy(p + ".bounds.json", tmp_path / "a.bounds.json")
+    b.save(p)
+    back = ColbertIndex.load(p, device=dev)
+    assert back.faithful and torch.equal(back.residual, b.residual)
+    shutil.copy(tmp_path / "a.resid", p + ".resid")
+    shutil.copy(tmp_path / "a.bounds.json", p + ".bounds.json")
+    with pytest.raises(ValueError, match="not written with"):
+        ColbertIndex.load(p, device=dev)
+    bf = ColbertIndex.from_embeddings(_embs(13, 50, ragged=False), device=dev, dtype="bf16")
+    bf.save(p)
+    import os
+    assert not os.path.exists(p + ".resid") and not os.path.exists(p + ".bounds.json")
+    assert not ColbertIndex.load(p, device=dev).faithful

@@ -29,6 +29,19 @@ def test_library_exports_every_header_symbol(L):
     assert L.cbv2_abi_version() == 1
 
 
+def test_library_stamp_is_the_sources_content_hash(L, tmp_path):
+    """Build provenance: the loaded library was compiled from exactly the tree's
+    sources and flags; a library with another stamp is refused by the loader."""
+    from hybrid_rag_colbertv2_amd import _build
+    stamp = _build.source_stamp()
+    assert L.cbv2_build_stamp().decode() == f"cbv2-build-stamp:{stamp}"
+    assert _build.library_stamp(_lib.LIB_PATH) == stamp
+    fake = tmp_path / "lib.so"
+    fake.write_bytes(b"\0ELF... cbv2-build-stamp:0123456789abcdef ...")
+    assert _build.library_stamp(str(fake)) == "0123456789abcdef" != stamp
+    assert _build.library_stamp(str(tmp_path / "missing.so")) is None
+
+
 def test_validation_errors_without_gpu(L):
     h = ctypes.c_void_p()
     assert L.cbv2_index_create(0, None, 7, 10, 128, 128, None, 0, ctypes.byref(h)) == _lib.ERR_EUNSUPPORTED

@@ -121,8 +121,9 @@ def test_streaming_writer_incomplete_file_is_invalid(tmp_path):
     h = ctypes.c_void_p()
     L.check(L.lib().cbv2_index_writer_open(os.fsencode(path), L.DTYPE_BF16, 10, 0, ctypes.byref(h)))
     L.check(L.lib().cbv2_index_writer_append(h, 3, tokens.ctypes.data, None, doclens.ctypes.data, 0, None))
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError, match="partial file removed"):
         L.check(L.lib().cbv2_index_writer_close(h))
+    assert not os.path.exists(path)                  # no full-size headerless file left behind
     from hybrid_rag_colbertv2_amd.index import index_file_info
     with pytest.raises(ValueError):
         index_file_info(path)
