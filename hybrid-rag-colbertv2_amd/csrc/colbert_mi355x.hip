@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 #include <stdio.h>
@@ -2170,6 +2171,167 @@ __global__ __launch_bounds__(kTkThreads) void topk_select_kernel(const float* __
 }
 
 // ---------------------------------------------------------------------------
+// Block-max top-k for long rows (kSampledMinN <= n <= 64 * kBmMaxBlocks), two
+// launches (replaces the sampled filter + select):
+//  1. block_max_kernel: bm[row][j] = max key of docs [64j, 64j + 64), one wave
+//     per block, the whole chip streaming the score matrix once.
+//  2. topk_bmax_kernel, one workgroup per row: t = the kk-th largest block key
+//     rounded down to its top 22 bits (two 11-bit radix passes in LDS).  At
+//     least kk blocks have a max >= t, so the kk-th largest score is >= t:
+//     every doc of the top-kk is >= t and lies in a block whose max is >= t.
+//     Only those blocks (about kk) are read; their docs >= t are gathered as
+//     ranking keys (score desc, index asc) and ranked by counting (<= 512
+//     keys) or a bitonic sort.  Fewer than kk or more than kBmCand gathered
+//     (ties at t), or more than kBmQual qualifying blocks: the row falls back
+//     to the exact full-row radix select.  The result equals topk_rows_kernel's
+//     in every case, and the correctness argument never depends on bm being
+//     tight -- only on every entry being >= its block's true max.
+// ---------------------------------------------------------------------------
+constexpr int kBmCand = 4096;          // gathered ranking keys (32 KiB)
+constexpr int kBmQual = 2048;          // qualifying blocks
+constexpr int kBmMaxBlocks = 24576;    // block keys in LDS (96 KiB): rows of n <= 1,572,864
+constexpr int kBmRankMax = 512;        // gathered keys ranked by counting (else bitonic)
+constexpr size_t kBmFixedLds = kBmCand * 8 + 2048 * 4 + kBmQual * 4 + 64;
+inline int64_t bm_blocks(int64_t n) { return (n + 63) >> 6; }   // 64-doc blocks of a row
+
+// 16 lanes per 64-doc block (a float4 each), 4 blocks per wave-load, 4 loads
+// in flight per lane: a wave covers 16 blocks, a workgroup 64.  Rows that do
+// not start 16-B aligned (n % 4 != 0) load their floats one by one.
+constexpr int kBmBlocksPerWg = 64;
+__global__ __launch_bounds__(256) void block_max_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
+                                                        uint32_t* __restrict__ bm, int64_t bm_ld) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.y;
+  const int64_t nb = (n + 63) >> 6;
+  const int c = lane & 15, r = lane >> 4;
+  const int64_t b0 = (int64_t)blockIdx.x * kBmBlocksPerWg + wave * 16;
+  const float* x = scores + (size_t)row * ld;
+  const bool vec = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(scores) & 15) == 0);
+  uint32_t key[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {   // block b0 + 4u + r, docs 64 * blk + 4c .. + 3
+    const int64_t blk = b0 + 4 * u + r;
+    const int64_t i = blk * 64 + 4 * c;
+    uint32_t m = 0u;
+    if (blk < nb) {
+      if (vec && i + 3 < n) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+        m = max(max(f2u(v[0]), f2u(v[1])), max(f2u(v[2]), f2u(v[3])));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = (i + e < n) ? max(m, f2u(x[i + e])) : m;
+      }
+    }
+    key[u] = m;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {   // max over each 16-lane row = one block
+    uint32_t v = key[u];
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+    const int64_t blk = b0 + 4 * u + r;
+    if (c == 0 && blk < nb) bm[(size_t)row * bm_ld + blk] = v;
+  }
+}
+
+__global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
+                                                               int k, int64_t id_base, const uint32_t* __restrict__ bm,
+                                                               int64_t bm_ld, float* __restrict__ out_s,
+                                                               int32_t* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
+  uint64_t* const sel = reinterpret_cast<uint64_t*>(bm_dyn);   // [kBmCand]
+  uint32_t* const hist = reinterpret_cast<uint32_t*>(sel + kBmCand);   // [2048]
+  uint32_t* const qual = hist + 2048;                              // [kBmQual]
+  uint32_t* const misc = qual + kBmQual;                           // [16]
+  uint32_t* const keys = misc + 16;                                // [nb]
+  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6;
+  const int row = blockIdx.x;
+  const int nb = (int)((n + 63) >> 6);
+  const float* x = scores + (size_t)row * ld;
+  const uint32_t* brow = bm + (size_t)row * bm_ld;
+  const int kk = (int)((int64_t)k < n ? k : n);
+  for (int i = tid; i < nb; i += nth) keys[i] = brow[i];
+  if (tid < 16) misc[tid] = 0;
+  __syncthreads();
+  // 1. t = the kk-th largest block key, to its top 22 bits (two 11-bit digits)
+  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < nb ? kk : nb);
+  for (int p = 0; p < 2; ++p) {
+    const int shift = 21 - 11 * p;
+    for (int b = tid; b < 2048; b += nth) hist[b] = 0;
+    __syncthreads();
+    for (int i = tid; i < nb; i += nth) {
+      const uint32_t u = keys[i];
+      hist_add(hist, (u >> shift) & 2047u, (u & mask) == prefix);
+    }
+    __syncthreads();
+    if (wave == 0) find_bin(hist, 2048, kleft, &misc[4], &misc[5], &misc[6]);
+    __syncthreads();
+    kleft -= misc[5];
+    prefix |= misc[4] << shift;
+    mask |= 2047u << shift;
+    __syncthreads();
+  }
+  const uint32_t t = prefix;
+  // 2. the blocks whose max reaches t, then their docs >= t
+  for (int i = tid; i < nb; i += nth)
+    if (keys[i] >= t) {
+      const uint32_t pos = atomicAdd(&misc[0], 1u);
+      if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)i;
+    }
+  __syncthreads();
+  const uint32_t nqual = misc[0];
+  if (nqual <= (uint32_t)kBmQual) {
+    constexpr int U = 4;   // one score per thread per block row, U loads in flight
+    const uint32_t total = nqual * 64;
+    for (uint32_t w0 = tid; w0 < total; w0 += (uint32_t)nth * U) {
+      float v[U];
+      int64_t idx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t w = w0 + (uint32_t)(u * nth);
+        idx[u] = w < total ? (int64_t)qual[w >> 6] * 64 + (w & 63) : n;
+        v[u] = idx[u] < n ? x[idx[u]] : neg_inf();
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (idx[u] < n && f2u(v[u]) >= t) {
+          const uint32_t pos = atomicAdd(&misc[1], 1u);
+          if (pos < (uint32_t)kBmCand) sel[pos] = rank_key(v[u], (uint32_t)idx[u]);
+        }
+    }
+  }
+  __syncthreads();
+  const uint32_t ncand = misc[1];
+  int m = (int)ncand;
+  if (nqual > (uint32_t)kBmQual || ncand < (uint32_t)kk || ncand > (uint32_t)kBmCand) {
+    __syncthreads();
+    topk_exact_row(x, n, kk, sel, hist, &misc[4], &misc[5], &misc[6], &misc[7]);
+    m = kk;
+  }
+  float* os = out_s + (size_t)row * k;
+  int32_t* oi = out_i + (size_t)row * k;
+  if (m <= kBmRankMax) {   // rank by counting: keys are unique, rank = #greater
+    for (int i = tid; i < m; i += nth) {
+      const uint64_t key = sel[i];
+      int r = 0;
+      for (int j = 0; j < m; ++j) r += sel[j] > key ? 1 : 0;
+      if (r < k) {
+        os[r] = u2f((uint32_t)(key >> 32));
+        oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+      }
+    }
+    for (int j = m + tid; j < k; j += nth) {
+      os[j] = neg_inf();
+      oi[j] = -1;
+    }
+  } else {
+    sort_and_write(sel, m, k, id_base, os, oi);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Top-k of the fused scan's per-workgroup lists: row b holds M = slots * k
 // unique 64-bit ranking keys (0 = padding).  Exact radix select of the
 // kk = min(k, M)-th largest key (8 passes of 8-bit digits over the keys in
@@ -3053,6 +3215,7 @@ struct cbv2_index {
   bool fused_topk = false;   // CBV2_OPT_FUSED_TOPK != 0
   int fused_topk_mode = 0;   // its value (2: also the MXFP8 scan, A/B only)
   int dynamic_tail = 1;      // CBV2_OPT_DYNAMIC_TAIL (1: XCD-sliced tail, 2: one shared tail, 0: off)
+  int topk_bmax = 1;         // CBV2_OPT_TOPK_BMAX (1: block-max top-k where eligible, 0: sampled filter + select)
   int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
   bool band_lower_bound = true;  // CBV2_OPT_BAND_LOWER_BOUND
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
@@ -3569,7 +3732,7 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
     const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
     hipLaunchKernelGGL(maxsim_scan_f8_direct_kernel<QW>, dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
-                       ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs);
+                       ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, kLd);
     return launch_check("maxsim_scan_f8_direct_kernel");
   }
   // shape: 0 = auto (above); 5 = 8 waves x 8 queries, 32-token iterations /
@@ -3623,6 +3786,33 @@ int64_t fused_slots(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) 
   }
   if (B <= kSmallLdsMaxB) return 0;
   return scan_chunks(ix, (B + 31) / 32, cu_count(ix->device));
+}
+
+// Block-max top-k eligibility of a search (topk_bmax_kernel): the unfused
+// MaxSim scan of a 128-slot index, rows long enough for the sampled path
+// (shorter ones take the exact row select) and block keys that fit its LDS.
+bool bmax_eligible(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) {
+  return ix->topk_bmax != 0 && scorer == CBV2_SCORER_MAXSIM && ix->ld == kLd && ix->n >= kSampledMinN &&
+         bm_blocks(ix->n) <= kBmMaxBlocks && k <= kTopkMax && B <= 65535 && fused_slots(ix, scorer, B, k) == 0;
+}
+size_t bm_ws_bytes(int32_t B, int64_t n) { return ((size_t)B * (size_t)bm_blocks(n) * 4 + 255) & ~(size_t)255; }
+
+int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, uint32_t* bm,
+              float* out_s, int32_t* out_i, hipStream_t st, int dev) {
+  static std::atomic<bool> attr_set[64] = {};
+  if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
+    CBV2_HIP(hipFuncSetAttribute((const void*)topk_bmax_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)(kBmFixedLds + (size_t)kBmMaxBlocks * 4)));
+    if (dev >= 0 && dev < 64) attr_set[dev].store(true, std::memory_order_relaxed);
+  }
+  const int64_t nb = bm_blocks(n);
+  hipLaunchKernelGGL(block_max_kernel, dim3((unsigned)((nb + kBmBlocksPerWg - 1) / kBmBlocksPerWg), (unsigned)B),
+                     dim3(256), 0, st, scores, n, ld, bm, nb);
+  if (int rc = launch_check("block_max_kernel")) return rc;
+  const size_t lds = kBmFixedLds + (size_t)nb * 4;
+  hipLaunchKernelGGL(topk_bmax_kernel, dim3((unsigned)B), dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm,
+                     bm_blocks(n), out_s, out_i);
+  return launch_check("topk_bmax_kernel");
 }
 
 int scan_meanpool(cbv2_index* ix, const float* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
@@ -4001,12 +4191,14 @@ size_t cbv2_search_workspace_size(const cbv2_index* ix, int32_t B, int32_t k, in
   if (!ix || B < 1 || k < 1) return 0;
   const int64_t slots = fused_slots(ix, scorer, B, k);
   if (slots > 0) return kCtrBytes + (size_t)B * slots * k * sizeof(uint64_t);
-  return kCtrBytes + topk_ws_bytes(B, ix->n) + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
+  const size_t sel = bmax_eligible(ix, scorer, B, k) ? bm_ws_bytes(B, ix->n) : topk_ws_bytes(B, ix->n);
+  return kCtrBytes + sel + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
 }
 
 size_t cbv2_search_workspace_bytes(const cbv2_index* ix, int32_t B) {
-  if (!ix || B < 1) return 0;   // enough for any k and scorer (the unfused layout is the larger)
-  return kCtrBytes + topk_ws_bytes(B, ix->n) + (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
+  if (!ix || B < 1) return 0;   // enough for any k and scorer (the unfused layouts are the larger)
+  return kCtrBytes + std::max(topk_ws_bytes(B, ix->n), bm_ws_bytes(B, ix->n)) +
+         (size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float);
 }
 
 int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
@@ -4033,6 +4225,12 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
                        slots * k, k, ix->id_base, out_scores, out_ids);
     return launch_check("select_keys_kernel");
   }
+  if (bmax_eligible(ix, scorer, B, k)) {   // block maxima, then one select reading only the blocks that can win
+    uint32_t* bm = (uint32_t*)rest;
+    float* sc = (float*)(rest + bm_ws_bytes(B, ix->n));
+    if ((rc = scan_maxsim_timed(ix, Q, B, lq, sc, ix->n, st, ctr))) return rc;
+    return topk_bmax(sc, B, ix->n, ix->n, k, ix->id_base, bm, out_scores, out_ids, st, ix->device);
+  }
   const size_t tk = topk_ws_bytes(B, ix->n);
   float* sc = (float*)(rest + tk);
   rc = score_impl(ix, scorer, Q, B, lq, sc, ix->n, st, ctr);
@@ -4055,6 +4253,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
       return CBV2_OK;
     case CBV2_OPT_BAND_LOWER_BOUND:
       ix->band_lower_bound = value != 0;
+      return CBV2_OK;
+    case CBV2_OPT_TOPK_BMAX:
+      ix->topk_bmax = (int)value;
       return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);

@@ -108,6 +108,11 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        top-k, whose minimum faithful score lb bounds the
  *                        k-th from below, and bands T >= lb - beta (0: the
  *                        wider T >= T_k - 2 beta).  Identical results.
+ *  CBV2_OPT_TOPK_BMAX    1: cbv2_search's unfused MaxSim scan (rows of >= 65,536
+ *                        and <= 1,572,864 docs, k <= 1024) also folds the max of
+ *                        every 64-doc block, and ONE select launch reads only
+ *                        the blocks that can reach the top-k (0: the sampled
+ *                        filter + select).  Identical results.
  * cbv2_index_last_scan_plan: the work split of this handle's latest scan
  * launch: {workgroups, static chunk docs, static docs, dynamic tail 0/1}.
  * Thread safety: one handle may be used from several host threads and
@@ -117,6 +122,7 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_DYNAMIC_TAIL 2
 #define CBV2_OPT_BAND_DOC_MAJOR 3
 #define CBV2_OPT_BAND_LOWER_BOUND 4
+#define CBV2_OPT_TOPK_BMAX 5
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the
