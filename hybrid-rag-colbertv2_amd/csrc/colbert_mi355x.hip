@@ -1532,8 +1532,12 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
   }
 }
 
+// PAIR: two TPI-token iterations per barrier (4 ring slots = 2 pair buffers;
+// pair p+1 is issued right after the barrier that retires pair p-1, so its
+// loads get one pair's compute to land) -- half the barriers and pipeline
+// drains of the 3-deep ring, the same 32-token body (and VGPRs) per step.
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
-          int FK = 0, int LD = kLd, bool PQS = false>
+          int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1552,7 +1556,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   constexpr int kPiecesPerWave = kPieces / WAVES;
   static_assert(TPI == 32 || TPI == 64 || TPI == 128, "32, 64 or 128 tokens per iteration");
   static_assert(kPieces % WAVES == 0 && kScaleDma <= WAVES, "pieces must split evenly over waves");
-  static_assert(NBUF == 2 || NBUF == 3, "2- or 3-deep ring");
+  static_assert(PAIR ? (NBUF == 4 && IPG % 2 == 0 && FK == 0) : (NBUF == 2 || NBUF == 3),
+                "2- or 3-deep ring; PAIR: 4 slots, an even number of iterations per doc group, unfused");
   constexpr int kCandBytes = FK > 0 ? QPB * (FK * 8 + kFusedStateBytes) : 0;   // fused top-k buffers + state
   __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterStage + 256 + 16 + kCandBytes];
   int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterStage + 256);
@@ -1621,27 +1626,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   int dl_g = 0, dl_min = 0, dl_max = 0;
 
   const int nit = IPG * ngr;
-  issue(0, 0);
-  if (NBUF == 3 && nit > 1) issue(1, 1);
-  int cur = 0;
   bool stored = false;
-  for (int it = 0; it < nit; ++it) {
-    if (NBUF == 3 && it + 1 < nit && !stored) {
-      if (loader)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave + 1) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    stored = false;
-    if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
-    if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
-    const uint8_t* buf = smem + cur * kIterStage;
-    cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
-
+  // one TPI-token iteration on the landed slot buf: doc-group start, tiles, epilogue
+  auto step = [&](int it, const uint8_t* buf) {
     const int G = it / IPG, j = it % IPG;
     if (j == 0) {
       int dl4[4];
@@ -1685,6 +1672,43 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
           stored = true;
         }
       }
+    }
+  };
+  if constexpr (PAIR) {
+    issue(0, 0);
+    if (nit > 1) issue(1, 1);
+    for (int it = 0; it < nit; ++it) {
+      const int pb = (it >> 1) & 1;   // this pair's buffer: slots 2pb, 2pb + 1
+      if ((it & 1) == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this pair landed (the next is not issued yet)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (it + 2 < nit) issue(it + 2, 2 * (pb ^ 1));   // into the pair every wave finished before the barrier
+        if (it + 3 < nit) issue(it + 3, 2 * (pb ^ 1) + 1);
+      }
+      step(it, smem + (2 * pb + (it & 1)) * kIterStage);
+    }
+  } else {
+    issue(0, 0);
+    if (NBUF == 3 && nit > 1) issue(1, 1);
+    int cur = 0;
+    for (int it = 0; it < nit; ++it) {
+      if (NBUF == 3 && it + 1 < nit && !stored) {
+        if (loader)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave + 1) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      stored = false;
+      if (NBUF == 2 && it + 1 < nit) issue(it + 1, cur ^ 1);
+      if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+      const uint8_t* buf = smem + cur * kIterStage;
+      cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+      step(it, buf);
     }
   }
   }
@@ -3647,7 +3671,7 @@ constexpr float kF8DynB8 = 0.3f;      // shape 9
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
-          int FK = 0, int LD = kLd, int D = 1, bool PQS = false>
+          int FK = 0, int LD = kLd, int D = 1, bool PQS = false, bool PAIR = false>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -3660,7 +3684,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3735,9 +3759,11 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                        ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, kLd);
     return launch_check("maxsim_scan_f8_direct_kernel");
   }
-  // shape: 0 = auto (above); 5 = 8 waves x 8 queries, 32-token iterations /
-  // 3-deep ring with the prefetch after each tile's first MFMA (PF: 75.7 ->
-  // 73.5 ms at 1M, B=256); 7 / 8 / 9 = the 4-wave shapes of kF8Shapes.  Lab
+  // shape: 0 = auto (above); 5 = 8 waves x 8 queries, 32-token iterations,
+  // two per barrier (PAIR, round 3: lab, same process, bit-identical, 1M docs
+  // B=256 73.95 -> 73.28 ms, 1.25M 92.39 -> 91.75, B=64 19.28 -> 19.20;
+  // profiles/r03g_lab_f8_*), with the prefetch after each tile's first MFMA
+  // (PF: 75.7 -> 73.5 ms at 1M, B=256); 7 / 8 / 9 = the 4-wave shapes of kF8Shapes.  Lab
   // A/B only: 1 = 5 without PF, 2 = 64 / 2-deep, 3 = 64 / 3-deep, 4 = 128 /
   // 2-deep (2-4 spill at 8 queries per wave), 6 = 2 with PF, 10 = 9 with
   // three workgroups per CU.
@@ -3746,8 +3772,8 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
-    case 5: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out,
-                                                                                      st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 5: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave, three
     // workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two per CU
@@ -3759,14 +3785,17 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                                                                             frac(kF8DynSmall), task_docs, ctr_ws);
     case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
                                                                             frac(kF8DynB8), task_docs, ctr_ws);
+    // 12 = shape 5 before PAIR: one 32-token iteration per barrier, 3-deep ring
+    case 12: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
 #ifdef CBV2_LAB
     case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 11 = shape 5 as it was before the packed scales and D = 3 (round 2)
     case 11: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, 1, false>(ix, Qb, Qs, B, lq, out, ld_out,
                                                                                      st, frac(kScanDynFrac), task_docs, ctr_ws);
 #endif
-    default: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out,
-                                                                                         st, frac(kScanDynFrac), task_docs, ctr_ws);
+    default: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
   }
 }
 
