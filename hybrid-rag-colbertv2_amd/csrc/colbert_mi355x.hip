@@ -4013,7 +4013,7 @@ size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8
     w->count = (int32_t*)take((size_t)B * sizeof(int32_t));
     w->cand = (int32_t*)take((size_t)B * cap * sizeof(int32_t));
     w->F = (float*)take((size_t)B * cap * sizeof(float));
-    w->tk_bytes = topk_ws_bytes(B, ix->n);
+    w->tk_bytes = std::max(topk_ws_bytes(B, ix->n), bm_ws_bytes(B, ix->n));   // either top-k of T
     w->tk = take(w->tk_bytes);
     w->T = (float*)take((size_t)B * (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(float));
     const size_t nd = (size_t)(ix->n > 0 ? ix->n : 1) * sizeof(int32_t);
@@ -4435,7 +4435,10 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
   }
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
   if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr))) return rc;
-  if ((rc = topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device)))
+  if ((rc = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k)
+                ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st, ix->device)
+                : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st,
+                            ix->device)))
     return rc;
   if (fk_out != nullptr)     // the bf16 top-k's own faithful scores, for the caller's cross-shard bound
     return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, fk_out, k, st);

@@ -91,3 +91,17 @@ def test_bmax_workspace_and_small_rows(dev):
     any_k = int(L.cbv2_search_workspace_bytes(big._h, 256))
     for k in (1, 100, 1024, 4096):
         assert int(L.cbv2_search_workspace_size(big._h, 256, k, 0)) <= any_k
+
+
+@pytest.mark.parametrize("B", [1, 16])
+def test_bmax_faithful_search(dev, B):
+    """The fp32-faithful search's bf16 phase takes the same block-max top-k."""
+    n, k = 80_000, 100
+    Qf = synth.make_queries(B, 32, seed=40 + B)
+    planted = synth.planted_ids(B, n, 10, seed=41)
+    x, doclens = synth.make_shard(0, n, Qf, planted, dev, seed=42, dtype=torch.float32)
+    ix = ColbertIndex.faithful_f32(x, doclens)
+    Q = Qf.to(dev)
+    (s1, i1), (s0, i0) = _both(ix, Q, k)
+    assert torch.equal(i1, i0) and torch.equal(s1, s0)
+    assert all(set(i1[b, :10].tolist()) == set(planted[b].tolist()) for b in range(B))
