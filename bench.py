@@ -19,7 +19,7 @@ timed region; every stage runs in full inside every timed step.
 The JSON line also carries, measured in the same run:
   faithful         the same K steps on the fp32-faithful index (the reference's
                    fp32 arithmetic within 1e-4: bf16 scan + certified band
-                   rescoring, DESIGN.md §3.12), checked against the float64
+                   rescoring, DESIGN.md §3.7), checked against the float64
                    oracle of the fp32 values at 1e-4;
   native_exchange  (N > 1, RCCL) the same K steps with the exchange inside the
                    C ABI (cbv2_search_sharded_* / cbv2_rerank_sharded);
@@ -231,7 +231,7 @@ def main():
     ap.add_argument("--fused-topk", action="store_true", help="stage 2 with the top-k fused into the scan (A/B)")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
-                         "(bf16 hi scanned + residual-certified band, DESIGN 3.12)")
+                         "(bf16 hi scanned + residual-certified band, DESIGN §3.7)")
     args = ap.parse_args()
     # stdout carries exactly the ONE JSON line: everything else any layer prints
     # to fd 1 (Python, RCCL / gloo C++ logging) is sent to stderr from here on

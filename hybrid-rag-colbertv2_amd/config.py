@@ -17,7 +17,7 @@ Added fields (no reference counterpart):
   * ``index_dtype``    — "fp32" (default: fp32-faithful, the reference's fp32
                           scores within ~1e-5 and their exact top-k, as the
                           north star's 1e-3 contract requires for an encoder
-                          that returns fp32 embeddings; DESIGN.md §3.12),
+                          that returns fp32 embeddings; DESIGN.md §3.7),
                           "bf16" (~3 % more queries/s; scores within ~5e-3 of
                           fp32 on fp32 embeddings, exact on bf16-valued ones)
                           or "fp8" (MXFP8, config 5).

@@ -12,7 +12,7 @@
 //   scales_off         [n][ld][2] E8M0 bytes (MXFP8 only)            4 KiB-aligned
 //
 // ld = 128 token slots per doc, or 256 / 512 / 1024 for long documents (the
-// layouts the kernels scan, DESIGN.md §3.13).
+// layouts the kernels scan, DESIGN.md §3.9).
 //
 // A rank loads docs [begin, end) of the file: three contiguous byte ranges.
 // Reads go through two pinned staging buffers: a reader thread fills one with
