@@ -1536,8 +1536,12 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
 // pair p+1 is issued right after the barrier that retires pair p-1, so its
 // loads get one pair's compute to land) -- half the barriers and pipeline
 // drains of the 3-deep ring, the same 32-token body (and VGPRs) per step.
+// Lab only (round 3, bit-identical, profiles/r03i_lab_f8_spread_*): SPREAD2
+// (with PAIR) issues pair p+1's second iteration after the first iteration of
+// pair p instead of right after the barrier (-0.3 %); SPLIT has only waves
+// 0 .. WAVES/2 - 1 issue the DMA pieces (+0.2 %, within noise, 4 VGPR spills).
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
-          int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false>
+          int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false, bool SPREAD2 = false, bool SPLIT = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1553,9 +1557,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   constexpr size_t kDocStride = (size_t)LD * kDim, kScaleStride = (size_t)LD * 2;
   constexpr int kScaleDma = 4 * TPI * 2 / 256;                // 256-B scale DMAs per iteration
   constexpr int kPieces = kIterBytes / 1024;
-  constexpr int kPiecesPerWave = kPieces / WAVES;
+  constexpr int kLoadWaves = SPLIT ? WAVES / 2 : WAVES;
+  constexpr int kPiecesPerWave = kPieces / kLoadWaves;
   static_assert(TPI == 32 || TPI == 64 || TPI == 128, "32, 64 or 128 tokens per iteration");
-  static_assert(kPieces % WAVES == 0 && kScaleDma <= WAVES, "pieces must split evenly over waves");
+  static_assert(kPieces % kLoadWaves == 0 && kScaleDma <= kLoadWaves, "pieces must split evenly over waves");
+  static_assert(!SPREAD2 || PAIR, "SPREAD2 spreads a PAIR ring's issue");
   static_assert(PAIR ? (NBUF == 4 && IPG % 2 == 0 && FK == 0) : (NBUF == 2 || NBUF == 3),
                 "2- or 3-deep ring; PAIR: 4 slots, an even number of iterations per doc group, unfused");
   constexpr int kCandBytes = FK > 0 ? QPB * (FK * 8 + kFusedStateBytes) : 0;   // fused top-k buffers + state
@@ -1600,6 +1606,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   auto issue = [&](int it, int buf) {
     const int G = it / IPG, j = it % IPG;
     uint8_t* sbuf = smem + buf * kIterStage;
+    if (SPLIT && wave >= kLoadWaves) return;   // the partner waves load nothing (wave-uniform)
 #pragma unroll
     for (int jj = 0; jj < kPiecesPerWave; ++jj) {
       const int piece = wave * kPiecesPerWave + jj;
@@ -1684,7 +1691,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (it + 2 < nit) issue(it + 2, 2 * (pb ^ 1));   // into the pair every wave finished before the barrier
-        if (it + 3 < nit) issue(it + 3, 2 * (pb ^ 1) + 1);
+        if (!SPREAD2 && it + 3 < nit) issue(it + 3, 2 * (pb ^ 1) + 1);
+      } else if (SPREAD2 && it + 2 < nit) {
+        issue(it + 2, 2 * (pb ^ 1) + 1);                   // the same free pair buffer, one iteration later
       }
       step(it, smem + (2 * pb + (it & 1)) * kIterStage);
     }
@@ -3671,7 +3680,8 @@ constexpr float kF8DynB8 = 0.3f;      // shape 9
 // QW queries per wave, PER_CU workgroups per CU in the split, OCC the
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
-          int FK = 0, int LD = kLd, int D = 1, bool PQS = false, bool PAIR = false>
+          int FK = 0, int LD = kLd, int D = 1, bool PQS = false, bool PAIR = false, bool SPREAD2 = false,
+          bool SPLIT = false>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -3684,7 +3694,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3793,6 +3803,13 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     // 11 = shape 5 as it was before the packed scales and D = 3 (round 2)
     case 11: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, 1, false>(ix, Qb, Qs, B, lq, out, ld_out,
                                                                                      st, frac(kScanDynFrac), task_docs, ctr_ws);
+    // 13 / 14 / 15 = shape 5 with SPREAD2 / SPLIT / both
+    case 13: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, true, false>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 14: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, false, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 15: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, true, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
 #endif
     default: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
