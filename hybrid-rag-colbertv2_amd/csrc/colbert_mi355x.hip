@@ -1541,7 +1541,8 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
 // pair p instead of right after the barrier (-0.3 %); SPLIT has only waves
 // 0 .. WAVES/2 - 1 issue the DMA pieces (+0.2 %, within noise, 4 VGPR spills).
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
-          int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false, bool SPREAD2 = false, bool SPLIT = false>
+          int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false, bool SPREAD2 = false, bool SPLIT = false,
+          bool QUAD = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1561,9 +1562,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
   constexpr int kPiecesPerWave = kPieces / kLoadWaves;
   static_assert(TPI == 32 || TPI == 64 || TPI == 128, "32, 64 or 128 tokens per iteration");
   static_assert(kPieces % kLoadWaves == 0 && kScaleDma <= kLoadWaves, "pieces must split evenly over waves");
-  static_assert(!SPREAD2 || PAIR, "SPREAD2 spreads a PAIR ring's issue");
-  static_assert(PAIR ? (NBUF == 4 && IPG % 2 == 0 && FK == 0) : (NBUF == 2 || NBUF == 3),
-                "2- or 3-deep ring; PAIR: 4 slots, an even number of iterations per doc group, unfused");
+  constexpr int kGrp = QUAD ? 4 : 2;   // PAIR: iterations per barrier (QUAD, lab: four)
+  static_assert(!SPREAD2 || (PAIR && !QUAD), "SPREAD2 spreads a PAIR ring's issue");
+  static_assert(!QUAD || PAIR, "QUAD is a PAIR ring of four");
+  static_assert(PAIR ? (NBUF == 2 * kGrp && IPG % kGrp == 0 && FK == 0) : (NBUF == 2 || NBUF == 3),
+                "2- or 3-deep ring; PAIR: 2 x kGrp slots, whole groups per doc group, unfused");
   constexpr int kCandBytes = FK > 0 ? QPB * (FK * 8 + kFusedStateBytes) : 0;   // fused top-k buffers + state
   __shared__ __attribute__((aligned(1024))) uint8_t smem[NBUF * kIterStage + 256 + 16 + kCandBytes];
   int* const task_slot = reinterpret_cast<int*>(smem + NBUF * kIterStage + 256);
@@ -1681,7 +1684,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       }
     }
   };
-  if constexpr (PAIR) {
+  if constexpr (PAIR && !QUAD) {
     issue(0, 0);
     if (nit > 1) issue(1, 1);
     for (int it = 0; it < nit; ++it) {
@@ -1696,6 +1699,22 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
         issue(it + 2, 2 * (pb ^ 1) + 1);                   // the same free pair buffer, one iteration later
       }
       step(it, smem + (2 * pb + (it & 1)) * kIterStage);
+    }
+  } else if constexpr (QUAD) {   // the same with four iterations per barrier (slots 4qb .. 4qb + 3)
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      if (x < nit) issue(x, x);
+    for (int it = 0; it < nit; ++it) {
+      const int qb = (it >> 2) & 1;
+      if ((it & 3) == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+          if (it + 4 + x < nit) issue(it + 4 + x, 4 * (qb ^ 1) + x);
+      }
+      step(it, smem + (4 * qb + (it & 3)) * kIterStage);
     }
   } else {
     issue(0, 0);
@@ -3681,7 +3700,7 @@ constexpr float kF8DynB8 = 0.3f;      // shape 9
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
           int FK = 0, int LD = kLd, int D = 1, bool PQS = false, bool PAIR = false, bool SPREAD2 = false,
-          bool SPLIT = false>
+          bool SPLIT = false, bool QUAD = false>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -3694,7 +3713,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT, QUAD>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3809,6 +3828,9 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     case 14: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, false, true>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     case 15: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, true, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    // 16 = QUAD: four 32-token iterations (a whole 128-token doc group) per barrier, 8 ring slots
+    case 16: return launch_f8x4<32, 8, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, false, false, true>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
 #endif
     default: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true>(
