@@ -46,6 +46,8 @@ _SIGS = {
     "cbv2_index_last_scan_plan": (ctypes.c_int, [_p, _p]),
     "cbv2_search": (ctypes.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _p, _sz, _p, _p, _p]),
     "cbv2_rerank": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _p, _p, _p]),
+    "cbv2_rerank_workspace_bytes": (_sz, [_i32, _i32]),
+    "cbv2_rerank_ws": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
     "cbv2_select_topk": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p]),
     "cbv2_topk_workspace_bytes": (_sz, [_i32, _i64]),
     "cbv2_topk_rows": (ctypes.c_int, [_p, _i32, _i64, _i64, _i32, _i64, _p, _sz, _p, _p, _p]),

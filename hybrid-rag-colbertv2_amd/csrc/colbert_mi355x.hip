@@ -2569,6 +2569,36 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_kernel(
   rerank_finish<BIG>(sc, keys, hist, misc, b, crow, C, k, out_s, out_i, out_p);
 }
 
+__device__ __forceinline__ float rerank_one_f8(const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales,
+                                               const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
+                                               const i32x8 (&qa)[1][2], const int (&qs)[1][2], int lq, int32_t id,
+                                               int lane, int ld) {
+  const int64_t loc = (int64_t)id - id_base;
+  if (id < 0 || loc < 0 || loc >= n) return neg_inf();
+  const int g = lane >> 4;
+  int dl = doclens[loc];
+  dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+  float m[1][2] = {{neg_inf(), neg_inf()}};
+  for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {   // long documents: 128-token blocks
+    const int dlb = dl - kLd * blk;
+    const uint8_t* dbase = tokens + ((size_t)loc * ld + (size_t)kLd * blk) * kDim;
+    const uint8_t* dsc = tscales + ((size_t)loc * ld + (size_t)kLd * blk) * 2;
+    i32x8 af[kLd / 16];
+    int as[kLd / 16];
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt)
+      if (16 * rt < dlb) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
+#pragma unroll
+    for (int rt = 0; rt < kLd / 16; ++rt) {
+      if (16 * rt < dlb) {
+        const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+        tile_f8<1>(af[rt], as[rt], qa, qs, init, m);
+      }
+    }
+  }
+  return reduce16(m[0][0], m[0][1], lane, lq);
+}
+
 template <bool BIG = false>
 __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
@@ -2584,41 +2614,45 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_f8_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.x;
-  const int g = lane >> 4;
   i32x8 qa[1][2];
   int qs[1][2];
   load_qfrag_f8(Qb, Qs, b, b + 1, lq, lane, qa[0], qs[0]);
   const int32_t* crow = cand + (size_t)b * C;
   for (int c = wave; c < C; c += kRrWaves) {
-    const int32_t id = crow[c];
-    const int64_t loc = (int64_t)id - id_base;
-    float v = neg_inf();
-    if (id >= 0 && loc >= 0 && loc < n) {
-      int dl = doclens[loc];
-      dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
-      float m[1][2] = {{neg_inf(), neg_inf()}};
-      for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {   // long documents: 128-token blocks
-        const int dlb = dl - kLd * blk;
-        const uint8_t* dbase = tokens + ((size_t)loc * ld + (size_t)kLd * blk) * kDim;
-        const uint8_t* dsc = tscales + ((size_t)loc * ld + (size_t)kLd * blk) * 2;
-        i32x8 af[kLd / 16];
-        int as[kLd / 16];
-#pragma unroll
-        for (int rt = 0; rt < kLd / 16; ++rt)
-          if (16 * rt < dlb) gbl_afrag_f8(dbase, dsc, rt, lane, af[rt], as[rt]);
-#pragma unroll
-        for (int rt = 0; rt < kLd / 16; ++rt) {
-          if (16 * rt < dlb) {
-            const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
-            tile_f8<1>(af[rt], as[rt], qa, qs, init, m);
-          }
-        }
-      }
-      v = reduce16(m[0][0], m[0][1], lane, lq);
-    }
+    const float v = rerank_one_f8(tokens, tscales, doclens, n, id_base, qa, qs, lq, crow[c], lane, ld);
     if (lane == 0) sc[c] = v;
   }
   rerank_finish<BIG>(sc, keys, hist, misc, b, crow, C, k, out_s, out_i, out_p);
+}
+
+// Candidate-parallel rerank scores (small batches, raw): one wave per (query,
+// candidate), grid (ceil(C / kRrWaves), B).  A B=1 rerank of 50 candidates
+// then spreads over 7 CUs instead of running 7 candidates per wave in
+// sequence on one; the same per-candidate math (rerank_one_*), so the same
+// bits.  The top-k of the raw row is select_small_kernel (= rerank_finish).
+template <bool F8>
+__global__ __launch_bounds__(kRrWaves * 64) void rerank_raw_kernel(
+    const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
+    int64_t n, int64_t id_base, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int lq,
+    const int32_t* __restrict__ cand, int C, float* __restrict__ raw, int ld) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * kRrWaves + wave;
+  if (c >= C) return;   // wave-uniform; no barriers below
+  const int32_t id = cand[(size_t)b * C + c];
+  float v;
+  if constexpr (F8) {
+    i32x8 qa[1][2];
+    int qs[1][2];
+    load_qfrag_f8(Qb, Qs, b, b + 1, lq, lane, qa[0], qs[0]);
+    v = rerank_one_f8(tokens, tscales, doclens, n, id_base, qa, qs, lq, id, lane, ld);
+  } else {
+    bf16x8 qf[1][2][4];
+    load_qfrag16(reinterpret_cast<const uint16_t*>(Qb), b, b + 1, lq, lane, qf[0]);
+    v = rerank_one_bf16(tokens, doclens, n, id_base, qf, lq, id, lane, ld);
+  }
+  if (lane == 0) raw[(size_t)b * C + c] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -4341,8 +4375,19 @@ int cbv2_index_last_scan_plan(const cbv2_index* ix, int64_t* out4) {
   return CBV2_OK;
 }
 
-int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
-                float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+// Batches up to kRrSplitMaxB take the candidate-parallel raw kernel (+ the
+// row select when k > 0, its raw row in the caller's workspace); larger ones
+// one workgroup per query (the batch fills the chip by itself).
+constexpr int kRrSplitMaxB = 32;
+
+size_t cbv2_rerank_workspace_bytes(int32_t B, int32_t C) {
+  if (B < 1 || C < 1) return 0;
+  return ((size_t)B * (size_t)C * sizeof(float) + 255) & ~(size_t)255;
+}
+
+static int rerank_impl(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C,
+                       int32_t k, void* ws, size_t ws_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                       void* stream) {
   const int32_t qdt = ix && ix->dtype == CBV2_DTYPE_MXFP8 ? CBV2_DTYPE_MXFP8 : CBV2_DTYPE_BF16;
   int rc = check_query(ix, CBV2_SCORER_MAXSIM, Q, qdt, B, lq);
   if (rc) return rc;
@@ -4356,9 +4401,26 @@ int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int3
   const hipStream_t st = (hipStream_t)stream;
   const bool big = C > kSmallMax;                 // raw scores in dynamic LDS, multi-pass selection
   const unsigned dyn = big ? (unsigned)C * sizeof(float) : 0u;
-  if (ix->dtype == CBV2_DTYPE_MXFP8) {
-    const uint8_t* Qb = (const uint8_t*)Q;
-    const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
+  const bool f8 = ix->dtype == CBV2_DTYPE_MXFP8;
+  const uint8_t* Qb = (const uint8_t*)Q;
+  const uint8_t* Qs = f8 ? Qb + (size_t)B * lq * kDim : nullptr;
+  const size_t raw_bytes = (size_t)B * (size_t)C * sizeof(float);
+  if (B <= kRrSplitMaxB && (k == 0 || (!big && ws != nullptr && ws_bytes >= raw_bytes))) {
+    float* raw = k == 0 ? out_scores : (float*)ws;
+    const dim3 grid((unsigned)((C + kRrWaves - 1) / kRrWaves), (unsigned)B);
+    if (f8)
+      hipLaunchKernelGGL(rerank_raw_kernel<true>, grid, dim3(kRrWaves * 64), 0, st, ix->tokens, ix->scales,
+                         ix->doclens, ix->n, ix->id_base, Qb, Qs, lq, cand, C, raw, (int)ix->ld);
+    else
+      hipLaunchKernelGGL(rerank_raw_kernel<false>, grid, dim3(kRrWaves * 64), 0, st, ix->tokens, nullptr,
+                         ix->doclens, ix->n, ix->id_base, Qb, nullptr, lq, cand, C, raw, (int)ix->ld);
+    if ((rc = launch_check("rerank_raw_kernel"))) return rc;
+    if (k == 0) return CBV2_OK;
+    hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
+                       out_pos);
+    return launch_check("select_small_kernel");
+  }
+  if (f8) {
     if (big) {
       CBV2_HIP(hipFuncSetAttribute((const void*)rerank_f8_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)dyn));
@@ -4384,6 +4446,17 @@ int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int3
                        (int)ix->ld);
   }
   return launch_check("rerank_kernel");
+}
+
+int cbv2_rerank(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
+                float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+  return rerank_impl(ix, Q, B, lq, cand, C, k, nullptr, 0, out_scores, out_ids, out_pos, stream);
+}
+
+int cbv2_rerank_ws(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
+                   void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                   void* stream) {
+  return rerank_impl(ix, Q, B, lq, cand, C, k, workspace, workspace_bytes, out_scores, out_ids, out_pos, stream);
 }
 
 int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t C, int32_t k, float* out_scores,

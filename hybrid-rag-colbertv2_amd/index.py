@@ -142,6 +142,7 @@ class ColbertIndex:
         self.id_base = int(id_base)
         self.means: Optional[torch.Tensor] = None
         self._ws: Optional[torch.Tensor] = None
+        self._rr_ws: Optional[torch.Tensor] = None      # cbv2_rerank_ws workspace (small batches)
         h = ctypes.c_void_p()
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         if self.fp8:
@@ -538,9 +539,13 @@ class ColbertIndex:
         out_s = torch.empty((B, k), dtype=torch.float32, device=self.device)
         out_i = torch.empty((B, k), dtype=torch.int32, device=self.device)
         out_p = torch.empty((B, k), dtype=torch.int32, device=self.device)
-        _lib.check(_lib.lib().cbv2_rerank(self._h, qptr, B, lq, cand.data_ptr(), C, int(k),
-                                          out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(),
-                                          _stream_ptr(self.device)))
+        L = _lib.lib()
+        need = int(L.cbv2_rerank_workspace_bytes(B, C))   # small batches: candidate-parallel scores
+        if self._rr_ws is None or self._rr_ws.numel() < need:
+            self._rr_ws = torch.empty((need,), dtype=torch.uint8, device=self.device)
+        _lib.check(L.cbv2_rerank_ws(self._h, qptr, B, lq, cand.data_ptr(), C, int(k), self._rr_ws.data_ptr(),
+                                    self._rr_ws.numel(), out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(),
+                                    _stream_ptr(self.device)))
         return out_s, out_i, out_p
 
 

@@ -196,6 +196,20 @@ int cbv2_rerank(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const i
                 int32_t C, int32_t k, float* out_scores, int32_t* out_ids, int32_t* out_pos,
                 void* stream);
 
+/* cbv2_rerank_ws — cbv2_rerank with a caller workspace of
+ * cbv2_rerank_workspace_bytes(B, C) bytes: batches of up to 32 queries then
+ * score one (query, candidate) per wave across the chip (the raw row in the
+ * workspace) and select the top-k in a second kernel — the same scores, ids
+ * and positions, bit for bit, as the one-workgroup-per-query kernel
+ * cbv2_rerank uses (a B=1 rerank of 50 candidates otherwise runs 7 docs per
+ * wave in sequence on one CU).  A null or short workspace, C > 1024 or
+ * B > 32 take cbv2_rerank's path.  (cbv2_rerank with k == 0 and B <= 32 uses
+ * the candidate-parallel kernel directly into out_scores.) */
+size_t cbv2_rerank_workspace_bytes(int32_t B, int32_t C);
+int cbv2_rerank_ws(cbv2_index* index, const void* Q, int32_t B, int32_t lq, const int32_t* cand,
+                   int32_t C, int32_t k, void* workspace, size_t workspace_bytes, float* out_scores,
+                   int32_t* out_ids, int32_t* out_pos, void* stream);
+
 /* fp32-faithful index ---------------------------------------------------------
  * The reference keeps fp32 embeddings (local_rag_complete.py:735-746: the
  * encode output, torch.save'd as is) and scores them in fp32 (:802-831).  A
