@@ -1480,7 +1480,9 @@ __device__ __forceinline__ void lds_afrag_f8x4(const uint8_t* buf, int t, int la
 // wait for them (hipcc waits lgkmcnt(0) there), and the fold of chain k-D is
 // fenced after MFMA k (hipcc otherwise hoists the fold above it and pads the
 // MFMA -> VALU hazard with s_nop).
-template <int QW, int D, int TPI = 32, bool PF = false, bool PQS = false>
+// PROBE (lab only, INVALID scores): 1 = no per-MFMA fold (each accumulator
+// chains its MFMAs and is folded once per iteration), to bound the fold's cost.
+template <int QW, int D, int TPI = 32, bool PF = false, bool PQS = false, int PROBE = 0>
 __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, const i32x8 (&qa)[QW][2],
                                                const int* qsv, float (&m)[QW][2]) {
   constexpr int NC = 2 * QW;
@@ -1502,17 +1504,26 @@ __device__ __forceinline__ void iter_f8x4_full(const uint8_t* buf, int lane, con
     for (int cc = 0; cc < NC; ++cc) {
       const int k = t * NC + cc;
       if (!PF && cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
-      acc[k % (D + 1)] = mfma_f8q<PQS>(a[t & 1], as[t & 1], qa[cc >> 1][cc & 1], qsv, cc, f32x4{});
+      if constexpr (PROBE == 1)
+        acc[k % (D + 1)] = mfma_f8q<PQS>(a[t & 1], as[t & 1], qa[cc >> 1][cc & 1], qsv, cc,
+                                         k < D + 1 ? f32x4{} : acc[k % (D + 1)]);
+      else
+        acc[k % (D + 1)] = mfma_f8q<PQS>(a[t & 1], as[t & 1], qa[cc >> 1][cc & 1], qsv, cc, f32x4{});
       if constexpr (PF) {
         __builtin_amdgcn_sched_barrier(0);
         if (cc == 0 && t + 1 < NT) lds_afrag_f8x4<TPI>(buf, t + 1, lane, a[(t + 1) & 1], as[(t + 1) & 1]);
       }
-      if (k >= D) fold(k - D);
+      if (PROBE != 1 && k >= D) fold(k - D);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  if constexpr (PROBE == 1) {
 #pragma unroll
-  for (int k = NT * NC - D; k < NT * NC; ++k) fold(k);
+    for (int k = NT * NC - D - 1; k < NT * NC; ++k) fold(k);
+  } else {
+#pragma unroll
+    for (int k = NT * NC - D; k < NT * NC; ++k) fold(k);
+  }
 }
 
 template <int QW, int TPI = 32, bool PQS = false>
@@ -1542,7 +1553,7 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
 // 0 .. WAVES/2 - 1 issue the DMA pieces (+0.2 %, within noise, 4 VGPR spills).
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
           int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false, bool SPREAD2 = false, bool SPLIT = false,
-          bool QUAD = false>
+          bool QUAD = false, int PROBE = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1654,12 +1665,16 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     }
     if (TPI * j + TPI <= dl_min)
-      iter_f8x4_full<QW, D, TPI, PF, PQS>(buf, lane, qa, qsv, m);
+      iter_f8x4_full<QW, D, TPI, PF, PQS, PROBE == 1 ? 1 : 0>(buf, lane, qa, qsv, m);
     else if (TPI * j < dl_max)
       iter_f8x4_ragged<QW, TPI, PQS>(buf, lane, j, dl_g, dl_max, qa, qsv, m);
     if (j == IPG - 1) {
 #pragma unroll
       for (int q = 0; q < QW; ++q) {
+        if constexpr (PROBE == 2) {   // INVALID: no cross-lane sum (bounds the epilogue's cost)
+          sc[q] = (c == (G & 15)) ? m[q][0] + m[q][1] : sc[q];
+          continue;
+        }
         const float v = dpp_row_sum16((c < lq ? m[q][0] : 0.0f) + (16 + c < lq ? m[q][1] : 0.0f));
         sc[q] = (c == (G & 15)) ? v : sc[q];
       }
@@ -3734,7 +3749,7 @@ constexpr float kF8DynB8 = 0.3f;      // shape 9
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
           int FK = 0, int LD = kLd, int D = 1, bool PQS = false, bool PAIR = false, bool SPREAD2 = false,
-          bool SPLIT = false, bool QUAD = false>
+          bool SPLIT = false, bool QUAD = false, int PROBE = 0>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -3747,7 +3762,7 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT, QUAD>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT, QUAD, PROBE>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -3865,6 +3880,11 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 16 = QUAD: four 32-token iterations (a whole 128-token doc group) per barrier, 8 ring slots
     case 16: return launch_f8x4<32, 8, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, false, false, true>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    // 17 / 18 = INVALID probes of shape 5: no per-MFMA fold / no epilogue row sums
+    case 17: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, false, false, false, 1>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 18: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true, false, false, false, 2>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
 #endif
     default: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true>(
