@@ -355,7 +355,7 @@ def main():
     fused_topk = ix.fused_topk_slots(B, args.k) > 0
     # HBM bytes per launch from the committed PMC passes of the same kernel and
     # shape (tools/profile_round.sh -> tools/pmc_summary.py); null otherwise
-    traffic = clock = traffic_src = None
+    traffic = clock = traffic_src = mfma_busy = None
     pmc = os.path.join(ROOT, "profiles", "pmc_scan.json")
     want = "maxsim_scan_f8x4_kernel" if args.dtype == "fp8" else SCAN_KERNEL
     variant = "fused" if fused_topk else "unfused"
@@ -366,6 +366,10 @@ def main():
             if (d.get("batch") == B and d.get("docs_per_gpu") == n_local and d.get("kernel") == want
                     and d.get("variant", "unfused") == variant):
                 traffic, clock = d.get("hbm_bytes_per_launch"), d.get("clock_ghz")
+                ctr = d.get("counters", {})
+                busy, gui = (ctr.get(c, {}).get("per_launch") for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"))
+                if busy and gui:   # busy SIMD-cycles / (1024 SIMDs x GPU-busy cycles; GRBM summed over 8 XCDs)
+                    mfma_busy = busy / (1024 * gui / 8)
                 traffic_src = (f"committed PMC pass profiles/pmc_scan.json ({want}, {variant}, batch {B}, "
                                f"{n_local} docs/GPU, one MI355X), not this run")
     # every rank's scan time and collective time per step (max-over-ranks view of N > 1)
@@ -495,7 +499,8 @@ def main():
                          "avg_ms_by_rank": [round(r[0], 3) for r in per_rank],
                          "avg_ms_min_max": [round(min(r[0] for r in per_rank), 3),
                                             round(max(r[0] for r in per_rank), 3)],
-                         "clock_ghz_under_load": round(clock, 3) if clock else None},
+                         "clock_ghz_under_load": round(clock, 3) if clock else None,
+                         "mfma_busy_at_that_clock": round(mfma_busy, 4) if mfma_busy else None},
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad,
                        "oracle_checked_queries": len(check_rows), "oracle_tolerance": tol},

@@ -34,7 +34,7 @@ for shape in $SHAPES; do
   kern=maxsim_scan16x4_kernel
   [ "$dt" = fp8 ] && kern=maxsim_scan_f8x4_kernel
   ctrs="FETCH_SIZE WRITE_SIZE GRBM_GUI_ACTIVE"
-  [ "$docs" = 1000000 ] && ctrs="$ctrs SQ_VALU_MFMA_BUSY_CYCLES"
+  ctrs="$ctrs SQ_VALU_MFMA_BUSY_CYCLES"
   csvs=""
   for c in $ctrs; do
     d="$OUT/pmc_${dt}_${docs}_${bs}_$c"
