@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--bmax", type=int, default=1, help="CBV2_OPT_TOPK_BMAX (1: block-max top-k, 0: sampled)")
+    ap.add_argument("--sleep-ms", type=float, default=2.0,
+                    help="host sleep after each search (0: back to back, as tools/config_sweep.py times them)")
     a = ap.parse_args()
     from hybrid_rag_colbertv2_amd import _lib
     dev = torch.device("cuda:0")
@@ -54,7 +56,8 @@ def main():
                 torch.cuda.synchronize()
                 if r >= a.warmup:
                     ts.append(e0.elapsed_time(e1))
-                time.sleep(0.002)
+                if a.sleep_ms > 0:
+                    time.sleep(a.sleep_ms / 1e3)
             med = sorted(ts)[len(ts) // 2]
             plan.append({"docs": n, "batch": B, "dtype": a.dtype, "bmax": a.bmax, "searches": a.warmup + a.reps,
                          "warmup": a.warmup, "event_ms_median": round(med, 4), "plan": ix.last_scan_plan()})
