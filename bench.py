@@ -23,9 +23,10 @@ The JSON line also carries, measured in the same run:
                    oracle of the fp32 values at 1e-4;
   native_exchange  (N > 1, RCCL) the same K steps with the exchange inside the
                    C ABI (cbv2_search_sharded_* / cbv2_rerank_sharded);
-  cpu_baseline     the CPU restatements timed on this host (numpy fp32 BLAS =
-                   `value`; the scalar C restatement; the literal mean-pool
-                   scorer), with the CPU model and thread count;
+  cpu_baseline     (N = 1 only; null at N > 1) the CPU restatements timed on
+                   this host (numpy fp32 BLAS = `value`; the scalar C
+                   restatement; the literal mean-pool scorer), with the CPU
+                   model and thread count;
   p50 / p99        single-query latency of the whole hot path.
 
 N>1: the SAME 1M-doc corpus is split into N contiguous shards, one per rank
@@ -431,9 +432,10 @@ def main():
             native = {"error": f"{type(e).__name__}: {e}"}
             torch.cuda.synchronize()
 
-    # ---- CPU baseline (rank 0; the other ranks wait at the barrier below)
+    # ---- CPU baseline: N = 1 only (the contract times it once, on the host of
+    # the one-GPU run; an N > 1 line carries null and the ranks do not idle)
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(Q, tokens, n_total, args.cpu_budget)
     if world > 1:
         dist.barrier()
