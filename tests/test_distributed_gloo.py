@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the sharded search / rerank protocol of
+"""CPU, world_size 2 and 4 (gloo): the sharded search / rerank protocol of
 hybrid-rag-colbertv2_amd/distributed.py (all-gather of packed (score, id)
 pairs + merge; all-reduce MAX of candidate scores + select) equals the
 unsharded oracle.  The per-shard compute is injected as oracle-backed CPU
@@ -9,6 +9,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -65,7 +66,7 @@ def _data():
     return Q, docs, doclens, cand
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, k=40):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -74,7 +75,7 @@ def _worker(rank, world, port, q):
         Q, docs, doclens, cand = _data()
         a, b = shard_range(len(docs), rank, world)
         ss = ShardedSearcher(OracleShard(Q, docs[a:b], doclens[a:b], a), ops=OracleOps())
-        s, i = ss.search(Q, 40)
+        s, i = ss.search(Q, k)
         rs, ri, rp = ss.rerank(Q, torch.from_numpy(cand), 7)
         q.put((rank, s.numpy(), i.numpy(), rs.numpy(), ri.numpy(), rp.numpy()))
     finally:
@@ -87,12 +88,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_sharded_protocol_world2_equals_unsharded():
-    world = 2
+@pytest.mark.parametrize("world,k", [(2, 40), (4, 100)])
+def test_sharded_protocol_equals_unsharded(world, k):
+    """world 4, k = 100: every shard (75-76 docs) is shorter than k, so every
+    rank's list ends in -inf / -1 padding that the merge must skip."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, k)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -101,7 +104,7 @@ def test_sharded_protocol_world2_equals_unsharded():
         assert p.exitcode == 0
     Q, docs, doclens, cand = _data()
     full = orc.maxsim(Q.numpy(), docs, doclens)
-    es, ei = orc.topk(full, 40)
+    es, ei = orc.topk(full, k)
     rs, ri, rp = orc.rerank(Q.numpy(), docs, doclens, cand, 7)
     for _, s, i, gs, gi, gp in res:        # every rank holds the identical global answer
         assert np.array_equal(i, ei)
@@ -140,9 +143,9 @@ def _hybrid_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_hybrid_exchange_world2_equals_unsharded():
+@pytest.mark.parametrize("world", [2, 4])
+def test_hybrid_exchange_equals_unsharded(world):
     """Doc-sharded BM25 (global stats by all-reduce) + stage 2 in one all-gather."""
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
