@@ -422,7 +422,10 @@ def main():
         try:   # an error inside the native leg is reported in the line, not fatal to it
             nouts, nel = timed_steps(stepper(nsearch, Q), args.steps, args.warmup, world)
             nfi = nouts[-1][1].cpu().numpy()
+            _, np50, np99 = latency(nsearch, Q1)
             native = {"value": round(B * args.steps / nel, 2), "ms_per_step": round(nel / args.steps * 1e3, 3),
+                      "p50_ms_b1": round(np50, 3) if np50 is not None else None,
+                      "p99_ms_b1": round(np99, 3) if np99 is not None else None,
                       "top10_equals_planted": float(np.mean([set(nfi[b]) == set(planted[b]) for b in range(B)])),
                       "equals_torch_exchange": bool(np.array_equal(nfi, fi_h)),
                       "main_line": "native" if args.native_exchange else "torch.distributed"}
