@@ -55,7 +55,7 @@ sys.path.insert(0, ROOT)
 from hybrid_rag_colbertv2_amd import bm25 as bm25_mod  # noqa: E402
 from hybrid_rag_colbertv2_amd import synth  # noqa: E402
 from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range  # noqa: E402
-from hybrid_rag_colbertv2_amd.hybrid import PipelinedRetriever, rrf_fuse  # noqa: E402
+from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, PipelinedRetriever, rrf_fuse  # noqa: E402
 from hybrid_rag_colbertv2_amd.index import ColbertIndex, quantize_mxfp8  # noqa: E402
 
 LQ, LD, DIM = 32, 128, 128
@@ -325,21 +325,40 @@ def main():
     top10_planted = float(np.mean([set(fi_h[b]) == set(planted[b]) for b in range(B)]))
     sorted_ok = bool((torch.diff(fs, dim=1) <= 0).all().item())
 
-    # ---- p50 / p99 latency at batch 1 (whole hot path, one query)
-    def latency(srch, Qb):
+    # ---- p50 / p99 latency at batch 1 (whole hot path, one query).  One shard
+    # (or the native exchange): the one-round-trip path (cbv2_retrieve_begin /
+    # _finish: stages 2 -> host RRF -> 3 in C++, one host round trip); the
+    # torch.distributed exchange at N > 1: the stages one by one (`step`)
+    def one_trip(srch):
+        if srch.world > 1 and srch._nx is None:
+            return None
+        return OneTripRetriever(srch, colbert_k=args.k, fused=args.fused, final_k=args.final_k, lexical_k=args.k)
+
+    def latency(srch, Qb, one=None):
         lat = []
         for it in range(args.p50_iters + 3):
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
             t = time.perf_counter()
-            step(srch, Qb, bm_one)
+            if one is not None:
+                one(Qb, bm_one)
+            else:
+                step(srch, Qb, bm_one)
             torch.cuda.synchronize()
             if it >= 3:
                 lat.append((time.perf_counter() - t) * 1e3)
         return lat, (statistics.median(lat) if lat else None), (float(np.percentile(lat, 99)) if lat else None)
 
-    lat, p50, p99 = latency(searcher, Q1)
+    def same_as_step(srch, one, Qb):
+        """The one-trip result equals the stages called one by one (bit for bit)."""
+        a, b = step(srch, Qb, bm_one), one(Qb, bm_one)
+        return all(torch.equal(x, y) for x, y in zip(a, b))
+
+    one = one_trip(searcher)
+    one_same = same_as_step(searcher, one, Q1) if one is not None else None
+    _, p50_step, _ = latency(searcher, Q1) if one is not None else (None, None, None)
+    lat, p50, p99 = latency(searcher, Q1, one)
     bm_ms = []
     for _ in range(3):                                  # stage 1 alone (host), for the record
         t = time.perf_counter()
@@ -422,12 +441,14 @@ def main():
         try:   # an error inside the native leg is reported in the line, not fatal to it
             nouts, nel = timed_steps(stepper(nsearch, Q), args.steps, args.warmup, world)
             nfi = nouts[-1][1].cpu().numpy()
-            _, np50, np99 = latency(nsearch, Q1)
+            none = one_trip(nsearch)
+            _, np50, np99 = latency(nsearch, Q1, none)
             native = {"value": round(B * args.steps / nel, 2), "ms_per_step": round(nel / args.steps * 1e3, 3),
                       "p50_ms_b1": round(np50, 3) if np50 is not None else None,
                       "p99_ms_b1": round(np99, 3) if np99 is not None else None,
                       "top10_equals_planted": float(np.mean([set(nfi[b]) == set(planted[b]) for b in range(B)])),
                       "equals_torch_exchange": bool(np.array_equal(nfi, fi_h)),
+                      "one_trip_equals_stages": same_as_step(nsearch, none, Q1),
                       "main_line": "native" if args.native_exchange else "torch.distributed"}
         except Exception as e:   # noqa: BLE001
             if args.native_exchange:
@@ -459,7 +480,8 @@ def main():
         ffs, ffi = fouts[-1]
         ffi_h = ffi.cpu().numpy()
         bs = fix.last_band.float()
-        _, fp50, fp99 = latency(fsearch, Qf32[:1].contiguous())
+        fone = one_trip(fsearch) if world == 1 else None     # a faithful shard: torch exchange at N > 1
+        _, fp50, fp99 = latency(fsearch, Qf32[:1].contiguous(), fone)
         fbad = spot_check(ffs, ffi_h, Qf32.cpu().numpy(), lambda sel: f32[sel].cpu().numpy(), begin, end,
                           check_rows, 1e-4, world, dev)
         fleg = {"value": round(B * args.steps / fel, 2), "ms_per_step": round(fel / args.steps * 1e3, 3),
@@ -496,6 +518,10 @@ def main():
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
             "p99_ms_b1": round(p99, 3) if p99 is not None else None,
             "latency_samples": len(lat),
+            "latency_path": ("one host round trip (cbv2_retrieve_begin/_finish)" if one is not None
+                             else "stages one by one (torch.distributed exchange)"),
+            "p50_ms_b1_stages_one_by_one": round(p50_step, 3) if p50_step is not None else None,
+            "one_trip_equals_stages": one_same,
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
             "roofline": {"bound": "mfma", "kernel": want, "variant": variant, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),

@@ -18,7 +18,7 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "colbert_mi355x.hip")
-SRC_HOST = [os.path.join(PKG, "csrc", f) for f in ("host_bm25.cpp", "host_rrf.cpp", "sharded.cpp", "index_file.cpp", "text_en.cpp")]
+SRC_HOST = [os.path.join(PKG, "csrc", f) for f in ("host_bm25.cpp", "host_rrf.cpp", "sharded.cpp", "index_file.cpp", "text_en.cpp", "retrieve.cpp")]
 HDR = os.path.join(ROOT, "include", "colbert_mi355x.h")
 LIB = os.path.join(PKG, "libcolbert_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

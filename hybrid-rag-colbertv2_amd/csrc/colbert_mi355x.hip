@@ -4395,6 +4395,13 @@ int cbv2_index_last_scan_plan(const cbv2_index* ix, int64_t* out4) {
   return CBV2_OK;
 }
 
+int cbv2_index_kind(const cbv2_index* ix, int32_t* dtype, int32_t* faithful) {
+  CBV2_REQUIRE(ix != nullptr && dtype != nullptr && faithful != nullptr, "null index or output");
+  *dtype = ix->dtype;
+  *faithful = ix->resid != nullptr ? 1 : 0;
+  return CBV2_OK;
+}
+
 // Batches up to kRrSplitMaxB take the candidate-parallel raw kernel (+ the
 // row select when k > 0, its raw row in the caller's workspace); larger ones
 // one workgroup per query (the batch fills the chip by itself).

@@ -27,13 +27,32 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
   std::vector<int> order;
   ids.reserve(kb + kc);
   sc.reserve(kb + kc);
+  // id -> position in `ids` by open addressing (a power of two >= 2 (kb + kc)
+  // slots, multiplicative hash, linear probing): O(1) per add instead of the
+  // reference dict's semantics restated as a linear search (the fused order
+  // and values are unchanged: first insertion decides the position, float64
+  // sums in list order)
+  int bits = 4;
+  while ((1 << bits) < 2 * (kb + kc)) ++bits;
+  const uint32_t mask = (1u << bits) - 1;
+  std::vector<int32_t> slot(mask + 1, -1);
+  std::vector<uint32_t> used;
+  used.reserve(kb + kc);
   for (int32_t b = 0; b < B; ++b) {
     ids.clear();
     sc.clear();
+    for (uint32_t h : used) slot[h] = -1;
+    used.clear();
     auto add = [&](int32_t id, int32_t rank) {
       const double inc = 1.0 / (double)(rrf_k + rank);
-      for (size_t j = 0; j < ids.size(); ++j)
+      uint32_t h = ((uint32_t)id * 2654435761u) >> (32 - bits);
+      for (;; h = (h + 1) & mask) {
+        const int32_t j = slot[h];
+        if (j < 0) break;
         if (ids[j] == id) { sc[j] = sc[j] + inc; return; }
+      }
+      slot[h] = (int32_t)ids.size();
+      used.push_back(h);
       ids.push_back(id);
       sc.push_back(0.0 + inc);
     };

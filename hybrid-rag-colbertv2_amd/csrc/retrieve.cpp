@@ -1,0 +1,200 @@
+// retrieve.cpp — HybridRetriever.retrieve (local_rag_complete.py:894-935) for one
+// query batch with ONE host round trip and no Python between the stages:
+//
+//   begin   stage 2: scan + top-k of this shard (sharded: into the send block of
+//           the exchange), enqueued on the caller's stream; returns at once so
+//           the caller runs stage 1 (host BM25, LRC:937-950) while the GPU scans.
+//   finish  (sharded: the stage-2 + stage-1 all-gather and merges) -> D2H of the
+//           ColBERT top-k (and of the merged BM25 lists) -> wait -> host RRF +
+//           [:C] cut (cbv2_rrf_fuse, LRC:960-978, :916) -> H2D of the fused
+//           candidates -> stage 3 rerank (sharded: all-reduce MAX) + top-k select.
+//
+// Results are those of the separate calls (cbv2_search / _f32 / _sharded_*,
+// cbv2_rrf_fuse, cbv2_rerank_ws / _f32 / _sharded) bit for bit: this file only
+// sequences them, so the arithmetic and the tie rules live in one place.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "colbert_mi355x.h"
+
+extern "C" int cbv2_set_error(int code, const char* msg);
+
+namespace {
+int err(int code, const char* fmt, ...) {
+  char buf[384];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return cbv2_set_error(code, buf);
+}
+
+#define RT_HIP(call)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess) return err(CBV2_EHIP, "%s (%d)", #call, (int)e_); \
+  } while (0)
+
+size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Kind {
+  int32_t dtype = 0, faithful = 0;
+};
+
+// Device workspace: [stage-2 part | s B*k | ids B*k | lex ids B*kb | cand B*C | status B | rerank part]
+struct Layout {
+  size_t stage2 = 0, rerank = 0, total = 0;
+  uint8_t* base = nullptr;
+  float* s = nullptr;
+  int32_t *ids = nullptr, *lex_ids = nullptr, *cand = nullptr, *status = nullptr;
+  uint8_t* rr = nullptr;
+};
+
+Layout layout(const cbv2_index* ix, const cbv2_comm* c, Kind kd, int32_t B, int32_t lq, int32_t k, int32_t kb,
+              int32_t C, void* ws) {
+  Layout L;
+  if (c)
+    L.stage2 = a256(cbv2_sharded_workspace_bytes(ix, c, B, k, kb, 0));
+  else if (kd.faithful)
+    L.stage2 = a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_SEARCH, B, lq, k > CBV2_RETRIEVE_BAND_CAP ? k
+                                                                                               : CBV2_RETRIEVE_BAND_CAP));
+  else
+    L.stage2 = a256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM));
+  if (kd.faithful)
+    L.rerank = a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, C));
+  else
+    L.rerank = a256(c ? (size_t)B * C * 4 : cbv2_rerank_workspace_bytes(B, C));
+  const size_t bk = a256((size_t)B * k * 4), bkb = a256((size_t)B * (kb > 0 ? kb : 1) * 4),
+               bc = a256((size_t)B * C * 4), bs = a256((size_t)B * 4);
+  L.total = L.stage2 + 2 * bk + bkb + bc + bs + L.rerank;
+  if (ws) {
+    uint8_t* p = (uint8_t*)ws;
+    L.base = p;
+    p += L.stage2;
+    L.s = (float*)p;
+    p += bk;
+    L.ids = (int32_t*)p;
+    p += bk;
+    L.lex_ids = (int32_t*)p;
+    p += bkb;
+    L.cand = (int32_t*)p;
+    p += bc;
+    L.status = (int32_t*)p;
+    p += bs;
+    L.rr = p;
+  }
+  return L;
+}
+
+// Host stage: [ids B*k | merged lex ids B*kb | cand B*C | lex ids B*kb | lex scores B*kb] (4-byte words)
+struct HostLayout {
+  int32_t *ids, *lex_merged, *cand, *lex_ids, *lex_scores;
+};
+size_t host_words(int32_t B, int32_t k, int32_t kb, int32_t C) {
+  return (size_t)B * k + (size_t)3 * B * kb + (size_t)B * C;
+}
+HostLayout host_layout(void* h, int32_t B, int32_t k, int32_t kb, int32_t C) {
+  HostLayout H;
+  int32_t* p = (int32_t*)h;
+  H.ids = p;
+  H.lex_merged = H.ids + (size_t)B * k;
+  H.cand = H.lex_merged + (size_t)B * kb;
+  H.lex_ids = H.cand + (size_t)B * C;
+  H.lex_scores = H.lex_ids + (size_t)B * kb;
+  return H;
+}
+
+int check_common(const cbv2_index* ix, Kind* kd, const cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B,
+                 int32_t lq, int32_t k, int32_t kb) {
+  if (!ix) return err(CBV2_EINVAL, "null index");
+  if (int rc = cbv2_index_kind(ix, &kd->dtype, &kd->faithful)) return rc;
+  if (!Q) return err(CBV2_EINVAL, "null queries");
+  if (B < 1 || k < 1 || kb < 0) return err(CBV2_EINVAL, "bad sizes (B %d, k %d, kb %d)", B, k, kb);
+  if (lq < 1 || lq > 32) return err(CBV2_EINVAL, "lq must be in [1, 32] (got %d); longer queries go by blocks", lq);
+  const int32_t want = kd->faithful ? CBV2_DTYPE_F32 : kd->dtype;
+  if (q_dtype != want) return err(CBV2_EINVAL, "query dtype %d does not match the index (needs %d)", q_dtype, want);
+  if (c && kd->faithful)
+    return err(CBV2_EUNSUPPORTED, "an fp32-faithful shard needs the global-bound exchange (cbv2_search_f32_begin)");
+  return CBV2_OK;
+}
+}  // namespace
+
+extern "C" {
+
+size_t cbv2_retrieve_workspace_bytes(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t lq, int32_t k,
+                                     int32_t kb, int32_t C) {
+  Kind kd;
+  if (!ix || B < 1 || k < 1 || kb < 0 || C < 1 || lq < 1 || cbv2_index_kind(ix, &kd.dtype, &kd.faithful)) return 0;
+  return layout(ix, c, kd, B, lq, k, kb, C, nullptr).total;
+}
+
+size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C) {
+  if (B < 1 || k < 1 || kb < 0 || C < 1) return 0;
+  return host_words(B, k, kb, C) * 4;
+}
+
+int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                        int32_t k, int32_t kb, int32_t C, void* workspace, size_t workspace_bytes, void* stream) {
+  Kind kd;
+  if (int rc = check_common(ix, &kd, c, Q, q_dtype, B, lq, k, kb)) return rc;
+  if (C < 1) return err(CBV2_EINVAL, "C must be >= 1 (got %d)", C);
+  const Layout L = layout(ix, c, kd, B, lq, k, kb, C, workspace);
+  if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
+    return err(CBV2_EINVAL, "workspace too small or not 256-B aligned (%zu bytes needed)", L.total);
+  if (c)
+    return cbv2_search_sharded_local(ix, c, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, kb, L.base, L.stage2, stream);
+  if (kd.faithful)
+    return cbv2_search_f32(ix, (const float*)Q, B, lq, k, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
+                           L.base, L.stage2, L.s, L.ids, L.status, stream);
+  return cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
+}
+
+int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                         int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
+                         int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
+                         size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+  Kind kd;
+  if (int rc = check_common(ix, &kd, c, Q, q_dtype, B, lq, k, kb)) return rc;
+  if (C < 1 || final_k < 1) return err(CBV2_EINVAL, "C and final_k must be >= 1 (got %d, %d)", C, final_k);
+  if (kb > 0 && (!lex_ids || (c && !lex_scores))) return err(CBV2_EINVAL, "null stage-1 lists");
+  if (!out_scores || !out_ids || !out_pos) return err(CBV2_EINVAL, "null outputs");
+  const Layout L = layout(ix, c, kd, B, lq, k, kb, C, workspace);
+  if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
+    return err(CBV2_EINVAL, "workspace too small or not 256-B aligned (%zu bytes needed)", L.total);
+  if (!host_stage || host_bytes < host_words(B, k, kb, C) * 4)
+    return err(CBV2_EINVAL, "host stage too small (%zu bytes needed)", host_words(B, k, kb, C) * 4);
+  hipStream_t st = (hipStream_t)stream;
+  const HostLayout H = host_layout(host_stage, B, k, kb, C);
+  const int32_t* bm = lex_ids;   // the stage-1 lists the RRF reads (host)
+  int rc;
+  if (c) {
+    // this rank's BM25 lists ride the stage-2 all-gather (staged in the pinned
+    // host buffer, so their H2D is asynchronous); merged lists come back
+    if (kb > 0) {
+      std::memcpy(H.lex_ids, lex_ids, (size_t)B * kb * 4);
+      std::memcpy(H.lex_scores, lex_scores, (size_t)B * kb * 4);
+    }
+    rc = cbv2_search_sharded_exchange(ix, c, B, k, kb > 0 ? H.lex_ids : nullptr,
+                                      kb > 0 ? (const float*)H.lex_scores : nullptr, kb, L.base, L.stage2, L.s,
+                                      L.ids, kb > 0 ? L.lex_ids : nullptr, st);
+    if (rc) return rc;
+    if (kb > 0) RT_HIP(hipMemcpyAsync(H.lex_merged, L.lex_ids, (size_t)B * kb * 4, hipMemcpyDeviceToHost, st));
+    bm = H.lex_merged;
+  }
+  RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
+  RT_HIP(hipStreamSynchronize(st));   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  if ((rc = cbv2_rrf_fuse(bm, kb, H.ids, k, B, rrf_k, C, H.cand, nullptr, nullptr))) return rc;
+  RT_HIP(hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st));
+  if (c)
+    return cbv2_rerank_sharded(ix, c, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+  if (kd.faithful)
+    return cbv2_rerank_f32(ix, (const float*)Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids,
+                           out_pos, st);
+  return cbv2_rerank_ws(ix, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+}
+
+}  // extern "C"

@@ -339,3 +339,91 @@ class PipelinedRetriever:
             out.append((s, i))
             cur = nxt
         return out
+
+
+# ---------------------------------------------------------------------- one host round trip
+class OneTripRetriever:
+    """``retrieve_batch`` (stages 2 -> RRF -> 3, LRC:894-935) with ONE host
+    round trip and no Python between the stages: ``cbv2_retrieve_begin``
+    enqueues the scan + top-k, stage 1 (``lexical``) runs on the host while
+    the GPU scans, and ``cbv2_retrieve_finish`` does the rest in C++ -- the
+    ColBERT top-k to the host, the native RRF + ``[:C]`` cut (LRC:960-978,
+    :916), the candidates back and the rerank + select (include/
+    colbert_mi355x.h).  The latency path: the same results as ``step``-style
+    code built from ``search_hybrid`` / ``rrf_fuse`` / ``rerank`` bit for bit,
+    without the per-stage Python hops.
+
+    ``searcher``: a ``ColbertIndex`` (one shard), or a
+    ``distributed.ShardedSearcher`` built with ``native=True`` or a
+    ``distributed.NativeExchange`` (the exchange inside the C ABI; bf16 /
+    MXFP8 shards).  ``lexical`` per call: a callable
+    returning (ids [B, kb] int32, scores [B, kb] float32) of this rank's BM25
+    (host), or a host id array [B, kb] (one shard only), or None (no stage 1).
+    Returns device (scores [B, final_k], ids [B, final_k], positions [B, final_k])."""
+
+    def __init__(self, searcher, colbert_k: int = 100, fused: int = 50, final_k: int = 10, rrf_k: int = 60,
+                 lexical_k: int = 100):
+        from .distributed import NativeExchange, ShardedSearcher
+        comm = None
+        index = searcher
+        if isinstance(searcher, NativeExchange):
+            index, comm = searcher.index, searcher._h
+        elif isinstance(searcher, ShardedSearcher):
+            index = searcher.local
+            if searcher._nx is not None:
+                comm = searcher._nx._h
+            elif searcher.world > 1:
+                raise ValueError("OneTripRetriever over several ranks needs ShardedSearcher(native=True)")
+        self.index, self.comm = index, comm
+        self._owner = searcher            # keeps the comm handle alive (NativeExchange frees it on __del__)
+        self.k, self.C, self.final_k, self.rrf_k = int(colbert_k), int(fused), int(final_k), int(rrf_k)
+        self.lexical_k = int(lexical_k)
+        self.device = index.device
+        self._ws = None
+        self._host = None
+
+    def _buffers(self, B: int, lq: int, kb: int):
+        L = _lib.lib()
+        need = int(L.cbv2_retrieve_workspace_bytes(self.index._h, self.comm, B, lq, self.k, kb, self.C))
+        if need == 0:
+            raise ValueError(f"cbv2_retrieve_workspace_bytes: bad sizes (B {B}, lq {lq}, k {self.k}, kb {kb})")
+        if self._ws is None or self._ws.numel() < need + 256:
+            self._ws = torch.empty((need + 256,), dtype=torch.uint8, device=self.device)
+        hneed = int(L.cbv2_retrieve_host_bytes(B, self.k, kb, self.C))
+        if self._host is None or self._host.numel() < hneed:
+            self._host = torch.empty((hneed,), dtype=torch.uint8, pin_memory=True)
+        off = (-self._ws.data_ptr()) % 256                 # 256-B aligned start
+        return self._ws.data_ptr() + off, self._ws.numel() - off
+
+    def __call__(self, Q: torch.Tensor, lexical=None):
+        from .index import _stream_ptr
+        L = _lib.lib()
+        _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
+        kb_cap = self.lexical_k if callable(lexical) else (0 if lexical is None else int(np.shape(lexical)[1]))
+        ws, wsb = self._buffers(B, lq, kb_cap)
+        st = _stream_ptr(self.device)
+        _lib.check(L.cbv2_retrieve_begin(self.index._h, self.comm, qptr, qdt, B, lq, self.k, kb_cap, self.C,
+                                         ws, wsb, st))
+        lex_i = lex_s = None
+        kb = 0
+        if lexical is not None:       # stage 1 on the host while the GPU scans
+            if callable(lexical):
+                lex_i, lex_s = lexical()
+                lex_s = np.ascontiguousarray(lex_s, np.float32)
+            else:
+                lex_i = lexical
+                if self.comm is not None:
+                    raise ValueError("a sharded retrieve needs the BM25 scores too: pass a callable")
+            lex_i = np.ascontiguousarray(lex_i, np.int32)
+            kb = int(lex_i.shape[1])
+            if lex_i.shape[0] != B or kb > kb_cap:
+                raise ValueError(f"stage-1 lists must be [B, <= {kb_cap}] (got {lex_i.shape})")
+        out_s = torch.empty((B, self.final_k), dtype=torch.float32, device=self.device)
+        out_i = torch.empty((B, self.final_k), dtype=torch.int32, device=self.device)
+        out_p = torch.empty((B, self.final_k), dtype=torch.int32, device=self.device)
+        _lib.check(L.cbv2_retrieve_finish(
+            self.index._h, self.comm, qptr, qdt, B, lq, self.k,
+            lex_i.ctypes.data if kb else None, lex_s.ctypes.data if (kb and lex_s is not None) else None, kb,
+            self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
+            out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), st))
+        return out_s, out_i, out_p

@@ -459,6 +459,47 @@ int cbv2_rerank_sharded(cbv2_index* index, cbv2_comm* comm, const void* Q, int32
  * Free each handle with cbv2_comm_destroy.                                  */
 int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
 
+/* One query batch through HybridRetriever.retrieve's stages 2 -> RRF -> 3
+ * (local_rag_complete.py:894-935) with ONE host round trip and no caller code
+ * between the stages (the latency path: no D2H / RRF / H2D / launch hops in the
+ * host language).  Replaces the sequence _colbert_search (:952-958) ->
+ * _reciprocal_rank_fusion (:960-978) -> [:C] (:916) -> _colbert_rerank
+ * (:996-1014) for the caller; results equal those of the separate calls
+ * (cbv2_search[_f32] / cbv2_search_sharded_*, cbv2_rrf_fuse, cbv2_rerank_ws /
+ * _f32 / cbv2_rerank_sharded) bit for bit.
+ *  comm: NULL for one shard; else a cbv2_comm (bf16 / MXFP8 shards: the
+ *        exchange above; an fp32-faithful shard is CBV2_EUNSUPPORTED there).
+ *  Q:    the index's query type: bf16 [B][lq][128] (bf16 index), the
+ *        cbv2_quantize_mxfp8 buffer (MXFP8), f32 (fp32-faithful); lq <= 32.
+ *  cbv2_retrieve_begin enqueues stage 2 (this shard's scan + top-k; the band
+ *    capacity of a faithful search is CBV2_RETRIEVE_BAND_CAP) and returns:
+ *    the caller runs stage 1 (host BM25) meanwhile.
+ *  cbv2_retrieve_finish takes the stage-1 lists (HOST pointers: lex_ids
+ *    [B][kb] global ids, -1 padded; lex_scores [B][kb], read only with a
+ *    comm; kb = 0: no stage 1), (comm: all-gather + merges), copies the
+ *    ColBERT top-k to host_stage, WAITS for it (the round trip), fuses on the
+ *    host (cbv2_rrf_fuse with rrf_k, first C), uploads the candidates and
+ *    enqueues the rerank + select: out_scores f32 [B][final_k], out_ids
+ *    int32 [B][final_k] (global ids), out_pos int32 [B][final_k] (position
+ *    in the fused list), device, best first, -inf / -1 padded.
+ *  workspace: device, 256-B aligned, cbv2_retrieve_workspace_bytes(index,
+ *    comm, B, lq, k, kb, C) bytes, the same one for begin and finish;
+ *    host_stage: host (pinned for asynchronous copies),
+ *    cbv2_retrieve_host_bytes(B, k, kb, C) bytes, one per stream.
+ * cbv2_index_kind: the index's dtype (CBV2_DTYPE_*) and whether a residual is
+ *    attached (fp32-faithful, 1) or not (0).                                */
+#define CBV2_RETRIEVE_BAND_CAP 16384
+int cbv2_index_kind(const cbv2_index* index, int32_t* dtype, int32_t* faithful);
+size_t cbv2_retrieve_workspace_bytes(const cbv2_index* index, const cbv2_comm* comm, int32_t B, int32_t lq,
+                                     int32_t k, int32_t kb, int32_t C);
+size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C);
+int cbv2_retrieve_begin(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                        int32_t k, int32_t kb, int32_t C, void* workspace, size_t workspace_bytes, void* stream);
+int cbv2_retrieve_finish(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                         int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
+                         int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
+                         size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

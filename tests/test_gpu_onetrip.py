@@ -1,0 +1,131 @@
+"""GPU: the one-round-trip retrieve (csrc/retrieve.cpp: cbv2_retrieve_begin /
+_finish, hybrid.OneTripRetriever) against the same stages called one by one
+(search -> host RRF + [:C] -> rerank; LRC:894-935, 960-978, 916).
+
+Done = scores, ids and positions equal bit for bit, for bf16, MXFP8 and
+fp32-faithful shards, B = 1 / 5 / 40, with a BM25 callable, a host id array
+and no stage 1; and at G = 2 / 4 through the test-only loopback communicator
+(every rank equals the unsharded composed path)."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from hybrid_rag_colbertv2_amd import synth
+from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+from hybrid_rag_colbertv2_amd.distributed import NativeExchange, loopback_comms
+from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, rrf_fuse
+from hybrid_rag_colbertv2_amd.index import ColbertIndex
+
+pytestmark = pytest.mark.gpu
+
+K, KB, C, KF = 100, 100, 50, 10
+
+
+def _corpus(dev, N, B, seed, dtype=torch.bfloat16):
+    Qf = synth.make_queries(B, seed=seed)
+    planted = synth.planted_ids(B, N, 10, seed=seed + 1)
+    tokens, doclens = synth.make_shard(0, N, Qf, planted, dev, dtype=dtype)
+    doclens[::11] = torch.randint(0, 129, (len(doclens[::11]),), device=dev, dtype=torch.int32)
+    doclens[torch.from_numpy(planted.reshape(-1)).to(dev)] = 128
+    terms, off, V = synth.bm25_shard(0, N, planted)
+    return Qf, planted, tokens, doclens, (terms, off, V)
+
+
+def _composed(index, Q, lex_ids):
+    """The stages one by one, as bench.step does."""
+    _, ids = index.search(Q, K)
+    bm = np.zeros((ids.shape[0], 0), np.int32) if lex_ids is None else lex_ids
+    cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=C)
+    return index.rerank(Q, torch.from_numpy(cand).to(index.device), KF)
+
+
+@pytest.mark.parametrize("kind", ["bf16", "fp8", "fp32"])
+@pytest.mark.parametrize("B", [1, 5, 40])
+def test_one_trip_equals_composed(dev, kind, B):
+    N = 7000
+    Qf, planted, tokens, doclens, (terms, off, V) = _corpus(
+        dev, N, B, seed=31 + B, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+    if kind == "fp32":
+        ix, Q = ColbertIndex.faithful_f32(tokens, doclens), Qf.to(dev)
+    elif kind == "fp8":
+        ix, Q = ColbertIndex.mxfp8(tokens, doclens), Qf.to(dev, torch.bfloat16)
+    else:
+        ix, Q = ColbertIndex(tokens, doclens), Qf.to(dev, torch.bfloat16)
+    lex = NativeBM25(terms, off, V)
+    qt, qo = synth.bm25_queries(B)
+    bm_i, bm_s = lex.search(qt, qo, KB)
+    one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+    for lexical, lex_ids in ((lambda: (bm_i, bm_s), bm_i), (bm_i, bm_i), (None, None)):
+        got = [x.cpu() for x in one(Q, lexical)]
+        want = [x.cpu() for x in _composed(ix, Q, lex_ids)]
+        for g, w, name in zip(got, want, ("scores", "ids", "positions")):
+            assert torch.equal(g, w), f"{kind} B={B}: {name} differ from the composed stages"
+    for b in range(B):                     # the planted docs win stage 3
+        assert set(got[1][b].tolist()) == set(planted[b].tolist())
+
+
+def test_one_trip_rejects_bad_input(dev):
+    N = 300
+    Qf, _, tokens, doclens, _ = _corpus(dev, N, 2, seed=5)
+    ix = ColbertIndex(tokens, doclens)
+    one = OneTripRetriever(ix)
+    with pytest.raises(ValueError):                         # 40 query tokens: the composed path splits blocks
+        one(torch.zeros(2, 40, 128, dtype=torch.bfloat16, device=dev))
+    with pytest.raises(ValueError):                         # stage-1 rows != B
+        one(Qf.to(dev, torch.bfloat16), lambda: (np.zeros((3, 5), np.int32), np.zeros((3, 5), np.float32)))
+
+
+def _run_ranks(G, fn):
+    out, errs = [None] * G, []
+
+    def body(r):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                out[r] = fn(r)
+            s.synchronize()
+        except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
+            errs.append((r, e))
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a rank thread hung"
+    if errs:
+        raise errs[0][1]
+    return out
+
+
+@pytest.mark.parametrize("G,B,fp8", [(2, 1, False), (4, 9, False), (4, 6, True)])
+def test_one_trip_sharded_loopback_equals_unsharded(dev, G, B, fp8):
+    N = 6000
+    Qf, planted, tokens, doclens, (terms, off, V) = _corpus(dev, N, B, seed=50 + G)
+    mk = (lambda t, d, base: ColbertIndex.mxfp8(t, d, id_base=base)) if fp8 else \
+        (lambda t, d, base: ColbertIndex(t, d, id_base=base))
+    full = mk(tokens, doclens, 0)
+    cuts = [0, 40] + [40 + (N - 40) * (g + 1) // (G - 1) for g in range(G - 1)]   # shard 0 < k docs
+    ranges = list(zip(cuts[:-1], cuts[1:]))
+    shards = [mk(tokens[a:b].contiguous(), doclens[a:b].contiguous(), a) for a, b in ranges]
+    Q = Qf.to(dev, torch.bfloat16)
+    df = NativeBM25.doc_freq(terms, off, V)
+    stats = (N, int(off[-1]), df)
+    lex_full = NativeBM25(terms, off, V)
+    lex = [NativeBM25(terms[off[a]:off[b]], off[a:b + 1] - off[a], V, id_base=a, stats=stats) for a, b in ranges]
+    qt, qo = synth.bm25_queries(B)
+    comms = loopback_comms(G)
+    ones = [OneTripRetriever(NativeExchange(shards[r], comm=comms[r]), colbert_k=K, fused=C, final_k=KF)
+            for r in range(G)]
+    outs = _run_ranks(G, lambda r: [x.cpu() for x in ones[r](Q, lambda: lex[r].search(qt, qo, KB))])
+    torch.cuda.synchronize()
+    bi, _ = lex_full.search(qt, qo, KB)
+    want = [x.cpu() for x in _composed(full, Q, bi)]
+    for r, got in enumerate(outs):
+        for g, w, name in zip(got, want, ("scores", "ids", "positions")):
+            assert torch.equal(g, w), f"rank {r}: {name} differ from the unsharded composed stages"
+    for b in range(B):
+        assert set(outs[0][1][b].tolist()) == set(planted[b].tolist())
+    del ones

@@ -88,6 +88,28 @@ def test_native_rrf_batch_equals_python(L):
         assert list(ids[b, : len(exp)]) == exp
 
 
+@pytest.mark.parametrize("kb,kc,span", [(100, 100, 2**31 - 1), (3000, 2000, 4000), (0, 37, 50), (64, 0, 10)])
+def test_native_rrf_hash_table_equals_python(L, kb, kc, span):
+    """The id -> slot table (open addressing) against the reference dict semantics:
+    ids over the whole int32 range, long lists (many probes), lists with many
+    repeats, one empty list; ids AND float64 scores."""
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+    rng = np.random.default_rng(kb + kc)
+    B = 6
+    bm = rng.integers(0, span, size=(B, kb)).astype(np.int32)
+    cb = rng.integers(0, span, size=(B, kc)).astype(np.int32)
+    if kc:
+        cb[:, kc // 2:] = bm[:, : kc - kc // 2] if kb >= kc - kc // 2 else cb[:, kc // 2:]
+    C = kb + kc + 3
+    ids, sc, cnt = rrf_fuse(bm, cb, C=C, return_scores=True)
+    for b in range(B):
+        exp = orc.rrf(list(bm[b]), list(cb[b]))
+        assert int(cnt[b]) == len(exp)
+        assert [(int(i), float(s)) for i, s in zip(ids[b, : len(exp)], sc[b, : len(exp)])] == \
+            [(int(i), float(s)) for i, s in exp]
+        assert (ids[b, len(exp):] == -1).all()
+
+
 def test_host_bm25_basic(tmp_path):
     from hybrid_rag_colbertv2_amd.bm25 import HostBM25
     corpus = ["the cat sat on the mat", "dogs chase cats", "a bird in the hand", "cats and dogs and cats"]

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""B=1 latency of the whole hot path (host BM25 + scan + top-100 + RRF + rerank
+top-10), the stages called one by one from Python (bench.py's ``step``) vs
+the one-round-trip C++ path (hybrid.OneTripRetriever: cbv2_retrieve_begin /
+_finish), interleaved in one process on the same index.  Prints one JSON line
+per (docs, dtype) with p50 / p99 of each and the scan's own event time.
+
+usage: latency_ab.py [--docs 125000,1000000] [--dtype bf16] [--iters 200]"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from hybrid_rag_colbertv2_amd import bm25 as bm25_mod  # noqa: E402
+from hybrid_rag_colbertv2_amd import synth  # noqa: E402
+from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, rrf_fuse  # noqa: E402
+from hybrid_rag_colbertv2_amd.index import ColbertIndex  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", default="125000,1000000")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for n in (int(x) for x in a.docs.split(",")):
+        B = 1
+        Qf = synth.make_queries(256, 32, seed=1)
+        planted = synth.planted_ids(256, n, 10, seed=2)
+        terms, off, V = synth.bm25_shard(0, n, planted)
+        lex = bm25_mod.sharded(terms, off, V, id_base=0, device=dev)
+        del terms, off
+        qt, qo = synth.bm25_queries(256)
+        bm_one = lambda: lex.search(qt[:qo[1]], qo[:2], 100)   # noqa: E731
+        f32 = a.dtype == "fp32"
+        tokens, doclens = synth.make_shard(0, n, Qf, planted, dev, seed=0,
+                                           dtype=torch.float32 if f32 else torch.bfloat16)
+        ix = (ColbertIndex.faithful_f32(tokens, doclens) if f32 else
+              ColbertIndex.mxfp8(tokens, doclens) if a.dtype == "fp8" else ColbertIndex(tokens, doclens))
+        del tokens
+        Q1 = Qf[:B].to(dev, torch.float32 if f32 else torch.bfloat16).contiguous()
+        one = OneTripRetriever(ix)
+
+        def composed():
+            _, ids = ix.search(Q1, 100)
+            bi, _ = bm_one()
+            cand = rrf_fuse(bi, ids.cpu().numpy(), rrf_k=60, C=50)
+            return ix.rerank(Q1, torch.from_numpy(cand).to(dev), 10)
+
+        def onetrip():
+            return one(Q1, bm_one)
+
+        legs = {"composed": composed, "one_trip": onetrip}
+        lat = {k: [] for k in legs}
+        for it in range(a.iters + 5):
+            for name, fn in legs.items():
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                out = fn()
+                torch.cuda.synchronize()
+                if it >= 5:
+                    lat[name].append((time.perf_counter() - t) * 1e3)
+        a_out, b_out = composed(), onetrip()
+        same = all(torch.equal(x, y) for x, y in zip(a_out, b_out))
+        ix.time_scans(True)
+        for _ in range(20):
+            ix.search(Q1, 100)
+        torch.cuda.synchronize()
+        scan = statistics.median(ix.scan_times()[-20:])
+        ix.time_scans(False)
+        rec = {"docs": n, "dtype": a.dtype, "B": B, "iters": a.iters, "scan_event_ms_p50": round(scan, 4),
+               "identical": same, "top10": out[1][0].tolist()[:3]}
+        for name, v in lat.items():
+            rec[name] = {"p50_ms": round(statistics.median(v), 4), "p99_ms": round(float(np.percentile(v, 99)), 4),
+                         "min_ms": round(min(v), 4)}
+        rec["p50_gain_us"] = round((rec["composed"]["p50_ms"] - rec["one_trip"]["p50_ms"]) * 1e3, 1)
+        print(json.dumps(rec), flush=True)
+        del ix, one, lex
+
+
+if __name__ == "__main__":
+    main()
