@@ -8,7 +8,7 @@ the whole path:
   stage 1  host BM25 top-100 (native C++, csrc/host_bm25.cpp) over the
            synthetic 1M-doc term corpus -- run while the GPU scans,
   stage 2  HIP MaxSim scan + radix top-100 (the top-k fused into the scan,
-           --fused-topk, is ~1 % slower on MI355X: profiles/r02k; sharded over
+           --fused-topk, is ~1 % slower on MI355X: profiles/history/r02/r02k; sharded over
            ranks: per-rank top-100 -> RCCL all-gather -> HIP merge; the ranks'
            BM25 lists over their doc shards ride the same all-gather),
   fusion   host RRF (native C++, reference semantics) -> top-50 candidates,
