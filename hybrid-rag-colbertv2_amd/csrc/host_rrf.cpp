@@ -66,7 +66,12 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
     }
     order.resize(ids.size());
     for (size_t j = 0; j < ids.size(); ++j) order[j] = (int)j;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return sc[a] > sc[c]; });
+    // the first C of the STABLE descending sort: (score desc, insertion order
+    // asc) is a strict total order, so a partial sort on it yields exactly the
+    // stable sort's prefix
+    const size_t m = std::min<size_t>((size_t)C, order.size());
+    std::partial_sort(order.begin(), order.begin() + m, order.end(),
+                      [&](int a, int c) { return sc[a] > sc[c] || (sc[a] == sc[c] && a < c); });
     for (int32_t j = 0; j < C; ++j) {
       const bool ok = j < (int32_t)order.size();
       out_ids[(size_t)b * C + j] = ok ? ids[order[j]] : -1;
