@@ -396,8 +396,10 @@ class OneTripRetriever:
         return self._ws.data_ptr() + off, self._ws.numel() - off
 
     def __call__(self, Q: torch.Tensor, lexical=None):
-        from .index import _stream_ptr
+        from .index import LQ_MAX, _stream_ptr
         L = _lib.lib()
+        if Q.dim() == 3 and Q.shape[1] > LQ_MAX and self.comm is None:
+            return self._stages(Q, lexical)     # long queries: the index sums blocks of <= 32 tokens
         _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
         kb_cap = self.lexical_k if callable(lexical) else (0 if lexical is None else int(np.shape(lexical)[1]))
         ws, wsb = self._buffers(B, lq, kb_cap)
@@ -427,3 +429,14 @@ class OneTripRetriever:
             self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
             out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), st))
         return out_s, out_i, out_p
+
+    def _stages(self, Q: torch.Tensor, lexical):
+        """The same stages called one by one (queries of more than 32 tokens)."""
+        _, ids = self.index.search(Q, self.k)
+        B = ids.shape[0]
+        if lexical is None:
+            bm = np.zeros((B, 0), np.int32)
+        else:
+            bm = np.ascontiguousarray(lexical()[0] if callable(lexical) else lexical, np.int32)
+        cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=self.rrf_k, C=self.C)
+        return self.index.rerank(Q, torch.from_numpy(cand).to(self.device), self.final_k)

@@ -66,13 +66,14 @@ def test_one_trip_equals_composed(dev, kind, B):
         assert set(got[1][b].tolist()) == set(planted[b].tolist())
 
 
-def test_one_trip_rejects_bad_input(dev):
+def test_one_trip_long_queries_and_bad_input(dev):
     N = 300
     Qf, _, tokens, doclens, _ = _corpus(dev, N, 2, seed=5)
     ix = ColbertIndex(tokens, doclens)
     one = OneTripRetriever(ix)
-    with pytest.raises(ValueError):                         # 40 query tokens: the composed path splits blocks
-        one(torch.zeros(2, 40, 128, dtype=torch.bfloat16, device=dev))
+    Ql = torch.randn(2, 40, 128, device=dev).to(torch.bfloat16)    # 40 query tokens: the stages by blocks
+    got, want = one(Ql), _composed(ix, Ql, None)
+    assert all(torch.equal(g, w) for g, w in zip(got, want))
     with pytest.raises(ValueError):                         # stage-1 rows != B
         one(Qf.to(dev, torch.bfloat16), lambda: (np.zeros((3, 5), np.int32), np.zeros((3, 5), np.float32)))
 
