@@ -211,6 +211,54 @@ def spot_check(fs, fi_h, Qd, docs_fn, begin, end, queries, tol, world, dev):
     return bad
 
 
+def c45_legs(args, B, world, rank, dev, backend):
+    """BASELINE configs 4 and 5: ``args.c45_docs`` (10M) docs split into one
+    contiguous shard per rank (1.25M at 8 ranks), B=256, stage 2 = scan +
+    top-100 + ONE RCCL all-gather + HIP merge, K timed steps after W warmups:
+    config 4 on bf16 tokens, config 5 on MXFP8 e4m3 tokens (block-scaled fp8
+    MFMA).  Checks: the merged top-10 of every query = its planted docs."""
+    n_c = args.c45_docs
+    b, e = shard_range(n_c, rank, world)
+    Qf = synth.make_queries(B, LQ, seed=1)
+    planted = synth.planted_ids(B, n_c, 10, seed=2)
+    Q = Qf.to(dev, torch.bfloat16)
+    out = {"corpus_docs": n_c, "docs_per_gpu": e - b, "global_batch": B, "stage": "MaxSim top-100 + all-gather merge"}
+    for name, fp8 in (("config4_bf16", False), ("config5_mxfp8", True)):
+        t0 = time.time()
+        if fp8:
+            q8, sc8, dl = synth.make_shard_mxfp8(b, e, Qf, planted, dev, seed=0)
+            ix = ColbertIndex(q8, dl, id_base=b, scales=sc8)
+        else:
+            tok, dl = synth.make_shard(b, e, Qf, planted, dev, seed=0)
+            ix = ColbertIndex(tok, dl, id_base=b)
+        srch = ShardedSearcher(ix, lexical_k=args.k)
+        torch.cuda.synchronize()
+        log(f"{name}: shard [{b},{e}) built in {time.time() - t0:.1f}s")
+        ix.time_scans(True)
+        outs, el = timed_steps(lambda K: [srch.search(Q, args.k) for _ in range(K)], args.steps, args.warmup, world)
+        scans = ix.scan_times()[-args.steps:]
+        ix.time_scans(False)
+        avg = sum(scans) / len(scans) if scans else float("nan")
+        per_rank = [r[0] for r in gather_floats([avg], world, dev, backend)]
+        ih = outs[-1][1].cpu().numpy()
+        peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
+        worst = max(per_rank)
+        achieved = B * (n_c // world) * FLOP_PER_PAIR / (worst * 1e-3) / 1e12
+        out[name] = {"value": round(B * args.steps / el, 2), "unit": "queries/s", "ms_per_step": round(el / args.steps * 1e3, 3),
+                     "scan_avg_ms_by_rank": [round(x, 3) for x in per_rank],
+                     "roofline_frac_slowest_rank": round(achieved / peak, 4), "peak_tflops": peak,
+                     "top10_equals_planted": float(np.mean([set(ih[q, :10]) == set(planted[q]) for q in range(B)])),
+                     "sorted": bool((torch.diff(outs[-1][0], dim=1) <= 0).all().item())}
+        del outs, srch, ix
+        if fp8:
+            del q8, sc8, dl
+        else:
+            del tok, dl
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +278,10 @@ def main():
     ap.add_argument("--native-exchange", action="store_true",
                     help="N>1: the MAIN timing uses the exchange inside the C ABI (the native leg always runs too)")
     ap.add_argument("--fused-topk", action="store_true", help="stage 2 with the top-k fused into the scan (A/B)")
+    ap.add_argument("--c45", choices=["auto", "on", "off"], default="auto",
+                    help="BASELINE configs 4 / 5 (10M docs sharded over the ranks, stage 2, bf16 and MXFP8) as "
+                         "extra legs of the line; auto = at 8 ranks (the configs' node)")
+    ap.add_argument("--c45-docs", type=int, default=10_000_000, help="corpus of the config-4/5 legs")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
                          "(bf16 hi scanned + residual-certified band, DESIGN §3.7)")
@@ -359,6 +411,8 @@ def main():
     one_same = same_as_step(searcher, one, Q1) if one is not None else None
     _, p50_step, _ = latency(searcher, Q1) if one is not None else (None, None, None)
     lat, p50, p99 = latency(searcher, Q1, one)
+    latency_path = ("one host round trip (cbv2_retrieve_begin/_finish)" if one is not None
+                    else "stages one by one (torch.distributed exchange)")
     bm_ms = []
     for _ in range(3):                                  # stage 1 alone (host), for the record
         t = time.perf_counter()
@@ -467,7 +521,7 @@ def main():
     # ---- the contract-precision leg: the same K steps on the fp32-faithful index
     fleg = None
     if args.dtype == "bf16" and not args.no_faithful:
-        nsearch = None
+        nsearch = none = one = None       # the one-trip paths hold their searchers (and so the bf16 index)
         del searcher, ix, tokens
         torch.cuda.empty_cache()
         f32, dl32 = synth.make_shard(begin, end, Qf, planted, dev, seed=0, dtype=torch.float32)
@@ -494,6 +548,18 @@ def main():
                 "top10_equals_planted": float(np.mean([set(ffi_h[b]) == set(planted[b]) for b in range(B)])),
                 "note": "fp32 index (the reference stores fp32, LRC:735-746); scores vs float64 oracle of the fp32 values"}
 
+    # ---- BASELINE configs 4 and 5 on the node (8 ranks): the 10M-doc corpus
+    # sharded over the ranks, stage 2 (scan + top-100 + ONE all-gather + merge)
+    c45 = None
+    if args.c45 == "on" or (args.c45 == "auto" and world == 8 and args.dtype == "bf16"):
+        one = searcher = ix = tokens = fix = fsearch = f32 = fone = nsearch = None   # noqa: F841  free HBM
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        try:   # reported in the line, not fatal to it (every rank takes the same branch: all or none raise)
+            c45 = c45_legs(args, B, world, rank, dev, backend)
+        except torch.cuda.OutOfMemoryError as e:
+            c45 = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
+
     fp8 = args.dtype == "fp8"
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     if rank == 0:
@@ -518,8 +584,7 @@ def main():
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
             "p99_ms_b1": round(p99, 3) if p99 is not None else None,
             "latency_samples": len(lat),
-            "latency_path": ("one host round trip (cbv2_retrieve_begin/_finish)" if one is not None
-                             else "stages one by one (torch.distributed exchange)"),
+            "latency_path": latency_path,
             "p50_ms_b1_stages_one_by_one": round(p50_step, 3) if p50_step is not None else None,
             "one_trip_equals_stages": one_same,
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
@@ -544,6 +609,8 @@ def main():
             line["native_exchange"] = native
         if collectives is not None:
             line["collectives"] = collectives
+        if c45 is not None:
+            line["configs_4_5"] = c45
         os.write(JSON_FD, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.barrier()
