@@ -2789,7 +2789,9 @@ __device__ __forceinline__ void tile16_x3(const bf16x8 (&ah)[4], const bf16x8 (&
 }
 
 // Faithful rescoring: query b = blockIdx.y against candidates c (cand == null:
-// c is the local doc index), kRsPerWave consecutive candidates per wave step,
+// c is the local doc index), pw consecutive candidates per wave step (1 for
+// small launches: one doc per wave, so a B=1 launch of 100 docs spreads over
+// 100 waves instead of 25 walking 4 docs in sequence; kRsPerWave otherwise),
 // grid-stride over blockIdx.x; out[b*ld_out + c].  count (nullable) bounds c
 // per query (the band collected by the search); only_neg (nullable) skips
 // every query whose status is >= 0 (the search's full-scan fallback).
@@ -2801,7 +2803,7 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
-    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld) {
+    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld, int pw) {
   const int lane = threadIdx.x & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
@@ -2811,14 +2813,14 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
     const int64_t cb = count[b];
     lim = cb < lim ? cb : lim;
   }
-  const int64_t step = (int64_t)gridDim.x * 4 * kRsPerWave;
-  int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * kRsPerWave;
+  const int64_t step = (int64_t)gridDim.x * 4 * pw;
+  int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * pw;
   if (c0 >= lim) return;  // wave-uniform
   bf16x8 qh[2][4], ql[2][4];
   load_qfrag16(qhi, b, b + 1, lq, lane, qh);
   load_qfrag16(qlo, b, b + 1, lq, lane, ql);
   for (; c0 < lim; c0 += step)
-  for (int64_t c = c0; c < c0 + kRsPerWave && c < lim; ++c) {
+  for (int64_t c = c0; c < c0 + pw && c < lim; ++c) {
     const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
     const int64_t loc = id - id_base;
     float v = neg_inf();
@@ -3131,6 +3133,8 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
 // Band select: exact top-k of the rescored band (score desc, id asc);
 // status[b] = band size when certified, -1 when the band overflowed cap.
 constexpr int kBandCapMax = 16384;
+constexpr int kBandPairMaxB = 8;       // batches up to this rescore the band pair by pair (search_f32_phase2)
+constexpr int kBandSelMax = 512;       // keys ranked by counting (the band, or its keys reaching the k-th score)
 __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __restrict__ F,
                                                                  const int32_t* __restrict__ cand,
                                                                  const int32_t* __restrict__ count, int cap, int k,
@@ -3138,14 +3142,70 @@ __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __
                                                                  int32_t* __restrict__ out_i,
                                                                  int32_t* __restrict__ status) {
   __shared__ uint64_t keys[kBandCapMax];
-  const int b = blockIdx.x;
+  __shared__ uint64_t sel[kBandSelMax];
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t misc[8];
+  const int b = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
   const int total = count[b];
   const int cnt = total < cap ? total : cap;
-  for (int t = threadIdx.x; t < cnt; t += blockDim.x)
+  for (int t = tid; t < cnt; t += nth)
     keys[t] = rank_key(F[(size_t)b * cap + t], (uint32_t)((int64_t)cand[(size_t)b * cap + t] - id_base));
+  if (tid < 8) misc[tid] = 0;
   __syncthreads();
-  sort_and_write(keys, cnt, k, id_base, out_s + (size_t)b * k, out_i + (size_t)b * k);
-  if (threadIdx.x == 0) status[b] = total > cap ? -1 : total;
+  float* os = out_s + (size_t)b * k;
+  int32_t* oi = out_i + (size_t)b * k;
+  const uint64_t* src = keys;
+  int m = cnt;
+  if (cnt > kBandSelMax) {
+    // the kk-th largest score (the keys' top 32 bits) by radix select over
+    // 11/11/10-bit digits, then the keys that reach it (the top-kk and its
+    // score ties) into sel
+    const uint32_t kk = (uint32_t)(k < cnt ? k : cnt);
+    uint32_t prefix = 0, mask = 0, kleft = kk;
+    for (int p = 0; p < 3; ++p) {
+      const int shift = p == 0 ? 21 : (p == 1 ? 10 : 0);
+      const uint32_t bits = p == 2 ? 1023u : 2047u;
+      for (int i = tid; i < 2048; i += nth) hist[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < cnt; i += nth) {
+        const uint32_t u = (uint32_t)(keys[i] >> 32);
+        hist_add(hist, (u >> shift) & bits, (u & mask) == prefix);
+      }
+      __syncthreads();
+      if ((tid >> 6) == 0) find_bin(hist, (int)bits + 1, kleft, &misc[4], &misc[5], &misc[6]);
+      __syncthreads();
+      kleft -= misc[5];
+      prefix |= misc[4] << shift;
+      mask |= bits << shift;
+      __syncthreads();
+    }
+    for (int i = tid; i < cnt; i += nth)
+      if ((uint32_t)(keys[i] >> 32) >= prefix) {
+        const uint32_t pos = atomicAdd(&misc[0], 1u);
+        if (pos < (uint32_t)kBandSelMax) sel[pos] = keys[i];
+      }
+    __syncthreads();
+    m = (int)misc[0];
+    src = sel;
+  }
+  if (m <= kBandSelMax) {   // keys are unique (distinct docs): rank = #greater, the sort's order
+    for (int i = tid; i < m; i += nth) {
+      const uint64_t key = src[i];
+      int r = 0;
+      for (int j = 0; j < m; ++j) r += src[j] > key ? 1 : 0;
+      if (r < k) {
+        os[r] = u2f((uint32_t)(key >> 32));
+        oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+      }
+    }
+    for (int j = m + tid; j < k; j += nth) {
+      os[j] = neg_inf();
+      oi[j] = -1;
+    }
+  } else {                  // more than kBandSelMax keys tie at the k-th score: sort the whole band
+    sort_and_write(keys, cnt, k, id_base, os, oi);
+  }
+  if (tid == 0) status[b] = total > cap ? -1 : total;
 }
 
 // ---------------------------------------------------------------------------
@@ -4142,11 +4202,15 @@ int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipSt
   return launch_check("split_query_kernel");
 }
 
+// pw: candidates per wave step (0 = auto: one per wave for launches of at
+// most kRsSmallPairs (query, candidate) pairs, kRsPerWave beyond)
+constexpr int64_t kRsSmallPairs = 4096;
 int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t* cand, const int32_t* count,
                    int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
-                   const int32_t* only_neg = nullptr) {
+                   const int32_t* only_neg = nullptr, int pw = 0) {
   if (limit <= 0) return CBV2_OK;
-  const int64_t per_wg = 4LL * kRsPerWave;
+  if (pw <= 0) pw = (int64_t)B * limit <= kRsSmallPairs ? 1 : kRsPerWave;
+  const int64_t per_wg = 4LL * pw;
   int64_t gx = (limit + per_wg - 1) / per_wg;
   // at most 1024 workgroups per row (4096 waves: a lone fallback row still
   // streams at full rate), grid-stride beyond; rows that skip exit at once
@@ -4154,7 +4218,7 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
   hipLaunchKernelGGL(ix->ld != kLd ? rescore_x3_kernel<true> : rescore_x3_kernel<false>, dim3((unsigned)gx, (unsigned)B),
                      dim3(256), 0, st, ix->tokens, ix->resid,
                      ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out,
-                     only_neg, (int)ix->ld);
+                     only_neg, (int)ix->ld, pw);
   return launch_check("rescore_x3_kernel");
 }
 }  // namespace
@@ -4603,7 +4667,11 @@ int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t 
   hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
                      out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb);
   if ((rc = launch_check("band_collect_kernel"))) return rc;
-  if (ix->band_doc_major) {   // pairs grouped by doc: each band doc's tiles read once per batch
+  // pairs grouped by doc (each band doc's tiles read once per batch) pay when
+  // the queries' bands overlap; a batch of at most kBandPairMaxB queries
+  // rescores pair by pair, one band doc per wave, without the doc-major
+  // passes over all n docs (count memset, offsets)
+  if (ix->band_doc_major && B > kBandPairMaxB) {
     CBV2_HIP(hipMemsetAsync(w.dcnt, 0, (size_t)ix->n * sizeof(int32_t), st));
     CBV2_HIP(hipMemsetAsync(w.dctr, 0, 2 * sizeof(int32_t), st));
     const unsigned gc = (unsigned)std::min<int64_t>((cap + 255) / 256, 16);
@@ -4623,7 +4691,8 @@ int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t 
     hipLaunchKernelGGL(kern, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, w.qhi, w.qlo, B, lq,
                        w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap, (int)ix->ld);
     if ((rc = launch_check("rescore_docs_kernel"))) return rc;
-  } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st))) {
+  } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
+                                   B <= kBandPairMaxB ? 1 : 0))) {
     return rc;
   }
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,

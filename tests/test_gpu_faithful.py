@@ -156,10 +156,11 @@ def test_faithful_shards_merge_equal_unsharded(dev):
 @pytest.mark.parametrize("N,dups", [(6000, 1), (3000, 9)])
 def test_band_doc_major_equals_pair_major(dev, N, dups):
     """Doc-major band rescoring (pairs grouped by doc, each band doc's tiles
-    read once per batch) returns the pair-by-pair rescoring's results bit for
-    bit.  dups > 1 repeats queries, so every band doc has > 4 pairs (several
-    passes of one wave over the doc)."""
-    docs, doclens, Q = make_case(N + dups, N, 6, 32)
+    read once per batch; batches of more than 8 queries) returns the
+    pair-by-pair rescoring's results bit for bit.  dups > 1 repeats queries,
+    so every band doc has > 4 pairs (several passes of one wave over the
+    doc)."""
+    docs, doclens, Q = make_case(N + dups, N, 12, 32)
     if dups > 1:
         Q = torch.cat([Q[:1].expand(dups, -1, -1), Q[1:]]).contiguous()
     ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=5)
@@ -228,3 +229,41 @@ def test_sharded_global_lower_bound_equals_unsharded(dev, N, k, parts):
     for own, b in zip(own_band, bands):
         assert ((b >= 0) & (b <= own)).all(), (own, b)
     assert sum(int(b.sum()) for b in bands) < sum(int(b.sum()) for b in own_band)
+
+
+def test_small_batch_band_pair_major_equals_batched(dev):
+    """Batches of at most 8 queries rescore their band pair by pair, one band
+    doc per wave (no doc-major passes): every row
+    equals the same query's row of a 12-query batch (doc-major, bitonic or
+    counting by band size) bit for bit, band sizes included."""
+    docs, doclens, Q = make_case(77, 20000, 12, 32)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=3)
+    sb, ib = ix.search(Q.to(dev), 100)
+    bb = ix.last_band.clone()
+    for rows in ((0,), (1, 2, 3), tuple(range(4, 12))):
+        s1, i1 = ix.search(Q[list(rows)].to(dev), 100)
+        assert torch.equal(i1, ib[list(rows)]) and torch.equal(s1, sb[list(rows)])
+        assert torch.equal(ix.last_band, bb[list(rows)])
+
+
+@pytest.mark.parametrize("copies", [300, 1500, 5000])
+def test_band_select_wide_bands_ties(dev, copies):
+    """Bands of identical docs (every copy ties at the k-th score): 300 copies
+    (+ the band's other docs) are ranked by counting after the radix select,
+    1,500 / 5,000 tie past 512 keys and the whole band is sorted; every path
+    returns the lowest ids among the tied copies first, with the oracle's
+    scores."""
+    g = torch.Generator().manual_seed(copies)
+    base = rand_unit(g, 1, 128, 128)
+    docs = torch.cat([rand_unit(g, 300, 128, 128), base.expand(copies, -1, -1)]).contiguous()
+    doclens = torch.full((docs.shape[0],), 128, dtype=torch.int32)
+    Q = (base[:, :32] + 0.3 * rand_unit(g, 1, 32, 128))
+    Q = (Q / Q.norm(dim=-1, keepdim=True)).contiguous()
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev))
+    for B in (1, 12):                                   # pair-major and doc-major band
+        s, i = ix.search(Q.expand(B, -1, -1).contiguous().to(dev), 100)
+        band = ix.last_band.cpu().numpy()
+        assert (band >= copies).all(), band
+        assert (i.cpu().numpy() == np.arange(300, 400)[None, :]).all()
+        exact = orc.maxsim(Q.numpy(), docs[300:301].numpy(), doclens[300:301].numpy())[0, 0]
+        np.testing.assert_allclose(s.cpu().numpy(), exact, atol=ATOL, rtol=0)
