@@ -248,6 +248,16 @@ class HybridRetriever:
         """
         k_final = top_k_final or self.config.final_top_k
         retr = self.indexer.colbert_retriever
+        if retr.scorer == "maxsim":       # one host round trip (cbv2_retrieve_begin / _finish), same results
+            key = (id(retr.corpus_embeddings), self.config.colbert_top_k, self.config.fused_candidates, k_final,
+                   self.config.rrf_k)
+            if getattr(self, "_one_key", None) != key:
+                self._one = OneTripRetriever(retr.corpus_embeddings, colbert_k=self.config.colbert_top_k,
+                                             fused=self.config.fused_candidates, final_k=k_final,
+                                             rrf_k=self.config.rrf_k)
+                self._one_key = key
+            s, i, _ = self._one(Q, np.ascontiguousarray(bm25_ids, np.int32))
+            return s, i
         _, ids = retr.search_embeddings(Q, self.config.colbert_top_k)
         ids_h = ids.cpu().numpy()
         cand = rrf_fuse(bm25_ids, ids_h, rrf_k=self.config.rrf_k, C=self.config.fused_candidates)

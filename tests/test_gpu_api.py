@@ -200,6 +200,13 @@ def test_retrieve_batch_equals_single(dev, tmp_path):
         assert set(i[b].tolist()) == set(planted[b].tolist())
         s1, i1 = hyb.retrieve_batch(Q[b:b + 1], bm[b:b + 1])
         assert torch.equal(i1[0], i[b]) and torch.equal(s1[0], s[b])
+    # the one-round-trip path equals the stages called one by one
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+    retr = ind.colbert_retriever
+    _, ids = retr.search_embeddings(Q, cfg.colbert_top_k)
+    cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=cfg.rrf_k, C=cfg.fused_candidates)
+    es, ei, _ = retr.rerank_ids(Q, torch.from_numpy(cand).to(dev), cfg.final_top_k)
+    assert torch.equal(ei, i) and torch.equal(es, s)
 
 
 def test_sharded_searcher_single_process(dev):
