@@ -504,6 +504,12 @@ def main():
                       "equals_torch_exchange": bool(np.array_equal(nfi, fi_h)),
                       "one_trip_equals_stages": same_as_step(nsearch, none, Q1),
                       "main_line": "native" if args.native_exchange else "torch.distributed"}
+            # every rank's native results equal the torch exchange's and the
+            # one-trip's equal the stages': the line's p50 may then come from it
+            okf = torch.tensor([1 if (native["equals_torch_exchange"] and native["one_trip_equals_stages"]
+                                      and native["top10_equals_planted"] == 1.0) else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(okf, op=dist.ReduceOp.MIN)
+            native["validated_on_every_rank"] = bool(int(okf.item()))
         except Exception as e:   # noqa: BLE001
             if args.native_exchange:
                 raise
@@ -560,6 +566,17 @@ def main():
         except torch.cuda.OutOfMemoryError as e:
             c45 = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
 
+    # N > 1: the single-query latency of the product is the one-round-trip path
+    # over the native exchange (no Python between the stages or around the
+    # collectives); the torch.distributed path's p50 stays beside it
+    p50_torch = p99_torch = None
+    if native is not None and native.get("validated_on_every_rank") and native.get("p50_ms_b1") is not None \
+            and not args.native_exchange:
+        p50_torch, p99_torch = p50, p99
+        p50, p99 = native["p50_ms_b1"], native["p99_ms_b1"]
+        latency_path = ("one host round trip over the native exchange (cbv2_retrieve_begin/_finish, "
+                        "RCCL collectives inside the C ABI)")
+
     fp8 = args.dtype == "fp8"
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     if rank == 0:
@@ -586,6 +603,8 @@ def main():
             "latency_samples": len(lat),
             "latency_path": latency_path,
             "p50_ms_b1_stages_one_by_one": round(p50_step, 3) if p50_step is not None else None,
+            "p50_ms_b1_torch_exchange": round(p50_torch, 3) if p50_torch is not None else None,
+            "p99_ms_b1_torch_exchange": round(p99_torch, 3) if p50_torch is not None else None,
             "one_trip_equals_stages": one_same,
             "host_bm25_ms_per_batch": round(min(bm_ms), 3),
             "roofline": {"bound": "mfma", "kernel": want, "variant": variant, "achieved": round(achieved, 2),
