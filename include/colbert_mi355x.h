@@ -473,7 +473,9 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *        cbv2_quantize_mxfp8 buffer (MXFP8), f32 (fp32-faithful); lq <= 32.
  *  cbv2_retrieve_begin enqueues stage 2 (this shard's scan + top-k; the band
  *    capacity of a faithful search is CBV2_RETRIEVE_BAND_CAP) and returns:
- *    the caller runs stage 1 (host BM25) meanwhile.
+ *    the caller runs stage 1 (host BM25) meanwhile.  Its kb is an upper
+ *    bound of the kb finish will pass (the stage-1 list width is known only
+ *    after stage 1 ran); B, lq, k, C and the workspace must be the same.
  *  cbv2_retrieve_finish takes the stage-1 lists (HOST pointers: lex_ids
  *    [B][kb] global ids, -1 padded; lex_scores [B][kb], read only with a
  *    comm; kb = 0: no stage 1), (comm: all-gather + merges), copies the
