@@ -11,9 +11,12 @@
  *
  * Conventions
  *  - Every pointer argument except `cbv2_index*` is a DEVICE pointer owned by
- *    the caller (torch tensors in the Python layer), except in the host-only
- *    helper cbv2_rrf_fuse, which takes HOST pointers.  Nothing is allocated or
- *    freed inside a compute call, so calls are hipGraph-capturable.
+ *    the caller (torch tensors in the Python layer), except where a
+ *    declaration says HOST: the host-only helpers (cbv2_rrf_fuse, BM25, the
+ *    index file, the stemmer) and the stage-1 lists / host stage of
+ *    cbv2_retrieve_finish.  Nothing is allocated or freed inside a compute
+ *    call; every call but cbv2_retrieve_finish (which waits for its round
+ *    trip) is asynchronous and hipGraph-capturable.
  *  - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy default
  *    stream).  One index handle belongs to one device.
  *  - Return 0 on success, a negative CBV2_E* code on error; the message is in
@@ -101,9 +104,11 @@ int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
  *                        as dynamic tasks, in 8 XCD-local slices (2: one
  *                        shared tail; 0: static chunks only).
- *  CBV2_OPT_BAND_DOC_MAJOR 1: cbv2_search_f32 rescores its band grouped by
- *                        doc (each band doc read once per batch; 0: pair by
- *                        pair).  Identical results either way.
+ *  CBV2_OPT_BAND_DOC_MAJOR 1: cbv2_search_f32 rescores the band of a batch
+ *                        of more than 8 queries grouped by doc (each band doc
+ *                        read once per batch; 0: pair by pair; smaller
+ *                        batches always go pair by pair, one band doc per
+ *                        wave).  Identical results either way.
  *  CBV2_OPT_BAND_LOWER_BOUND 1: cbv2_search_f32 first rescores the bf16
  *                        top-k, whose minimum faithful score lb bounds the
  *                        k-th from below, and bands T >= lb - beta (0: the
