@@ -1176,6 +1176,143 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_direct_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming small-batch scan (B <= 2, the production bf16 path; variants
+// 14-16): HBM-bound, so the kernel is built around the stream.  Every wave
+// owns a contiguous doc range and 1-2 queries (fragments in VGPRs), as the
+// direct scan below, but the docs' 16-row tiles arrive by LDS-DMA -- 1 KiB
+// per wave-instruction, 4 per tile, with the non-temporal policy (AUX = 2:
+// the bytes are read once) -- into a private ring of 8 tile slots per wave
+// (32 KiB; 128 KiB per 4-wave workgroup, one workgroup per CU).  Only the
+// tiles that hold tokens are streamed: the wave walks the sequence of (doc,
+// tile < ceil(doclen / 16)) pairs of its range with an issue cursor 8 tiles
+// ahead of the compute cursor, tile k in slot k % 8; after tile k is read
+// from its slot, tile k + 8 is issued into it, so the wait for the oldest
+// tile is a constant vmcnt(28) until the issue cursor runs out.  Same tiles,
+// masks, max order and epilogue as the direct scan: bit-identical scores.
+// Lab (same process, 1M docs): B=1 5.201 -> 4.704 ms (6.30 -> 6.97 TB/s),
+// B=2 5.262 -> 4.711, 125k B=1 0.656 -> 0.587; the same kernel without the
+// nt policy runs at the direct scan's rate (profiles/r03ae_*).
+// ---------------------------------------------------------------------------
+constexpr int kStreamSlots = 8;                    // tile slots per wave ring
+// A doc length through the scalar unit (s_load): a vector load of it would be
+// counted by vmcnt, and waiting for it would drain the LDS-DMA ring.
+__device__ __forceinline__ int sload_len(const int32_t* p) {
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+template <int QW, int AUX>
+__global__ __launch_bounds__(256, 1) void maxsim_scan_stream_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
+    int ld) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * kStreamSlots * 4096];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t lin = (int64_t)blockIdx.x * 4 + wave;      // one doc chunk per wave
+  const int qg = (int)(lin % nq_groups);
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;  // uniform over the wave; no block-level sync below
+  const int nd = (int)(d_end - d_begin);
+  uint8_t* ring = smem + wave * (kStreamSlots * 4096);
+  const size_t doc_bytes = (size_t)ld * kRowBytes;
+  const int32_t* dls = doclens + d_begin;
+  // 32-bit cursor arithmetic keeps every comparison on the scalar unit (a
+  // 64-bit compare goes to the VALU, the loop turns "divergent" and hipcc
+  // loads the lengths through the vector path, whose vmcnt(0) would drain
+  // the ring at every doc)
+  auto ntiles = [&](int d) -> int {
+    int dl = sload_len(dls + d);
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    return (dl + 15) >> 4;
+  };
+  // piece q of a tile = its rows 4q .. 4q + 3; lane l writes LDS slot (row
+  // 4q + (l >> 4), position l & 15), so it fetches the logical 16-B slot
+  // stored there: position ^ swz16(row) (the layout lds_afrag16 reads)
+  uint32_t src_off[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = 4 * q + g;
+    src_off[q] = (uint32_t)(t * kRowBytes + 16 * (c ^ swz16(t)));
+  }
+  // issue cursor: the next (doc, tile) to stream, and tiles issued so far
+  int idoc = 0;
+  int itile = 0, intl = ntiles(0);
+  while (intl == 0 && ++idoc < nd) intl = ntiles(idoc);
+  int issued = 0;
+  const uint8_t* tbase = tokens + (size_t)d_begin * doc_bytes;
+  auto issue_next = [&]() {
+    if (idoc >= nd) return;
+    const uint8_t* base = tbase + (size_t)idoc * doc_bytes + (size_t)itile * 16 * kRowBytes;
+    uint8_t* dst = ring + (issued & (kStreamSlots - 1)) * 4096;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + src_off[q]), (lds_void_t*)(dst + q * 1024), 16, 0, AUX);
+    ++issued;
+    if (++itile >= intl) {
+      itile = 0;
+      intl = 0;
+      while (intl == 0 && ++idoc < nd) intl = ntiles(idoc);
+    }
+  };
+  bf16x8 qf[QW][2][4];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QW + q, B, lq, lane, qf[q]);
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the query fragments: out of the ring's count
+#pragma unroll
+  for (int k = 0; k < kStreamSlots; ++k) issue_next();
+
+  int consumed = 0;
+  for (int i = 0; i < nd; ++i) {
+    int dl = sload_len(dls + i);
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    const int nt = (dl + 15) >> 4;
+    float m[QW][2];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    for (int t = 0; t < nt; ++t) {
+      // 8 tiles in flight: the oldest 4 pieces are this tile's (later loads
+      // and stores only make the wait stricter); fewer: the stream is ending
+      if (issued - consumed >= kStreamSlots)
+        asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bf16x8 a[4];
+      const uint8_t* row = ring + (consumed & (kStreamSlots - 1)) * 4096 + c * kRowBytes;
+      const int sw = swz16(c);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) a[s4] = *reinterpret_cast<const bf16x8*>(row + 16 * ((4 * g + s4) ^ sw));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is read: refill it
+      ++consumed;
+      issue_next();
+      const f32x4 init = (dl >= 16 * t + 16) ? f32x4{} : row_mask_init16(16 * t + 4 * g, dl);
+      tile16<QW>(a, qf, init, m);
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = qg * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
 // ===========================================================================
 // MXFP8 path (config 5): doc and query tokens as e4m3 bytes with one E8M0
 // power-of-two scale per token per 64 dims, scored on the block-scaled
@@ -3478,6 +3615,7 @@ enum ScanVariant {
   kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
   kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
+  kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -3701,13 +3839,37 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
   return launch_check("maxsim_scan_direct_kernel");
 }
 
+// Streaming scans (variants 14-16; 14 / 15 are the B = 1 / 2 production
+// scans of every bf16 index, long documents included): one 4-wave workgroup
+// per CU (128 KiB of LDS rings), chunks for kDirectOversub x the resident waves.
+template <int QW, int AUX>
+int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+  if (ix->dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "stream scan: bf16 index only");
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t target_waves = 4LL * cu_count(ix->device) * kDirectOversub;
+  int64_t n_chunks = target_waves / nq_groups;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  if (n_chunks < 1) n_chunks = 1;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
+  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
+  return launch_check("maxsim_scan_stream_kernel");
+}
+
 // Long documents (index ld = 256 / 512 / 1024): B <= 8 the direct scan in
 // 128-token blocks, larger B the production 8-wave doc-interleaved scan with
 // its doc group spanning ld / 64 iterations (the row maxima carried across).
 int scan_maxsim_long(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                      int* ctr_ws) {
-  if (B <= kLongDirectMaxB)
-    return B == 1 ? launch_direct<1>(ix, Q, B, lq, out, ld_out, st) : launch_direct<2>(ix, Q, B, lq, out, ld_out, st);
+  // B <= 2: the streaming scan (one query group, so the nt policy costs no L2
+  // sharing); B = 3-8 the direct scan, whose query groups share each doc's
+  // tiles through L2
+  if (B <= kDirectMaxB)
+    return B == 1 ? launch_stream<1, 2>(ix, Q, B, lq, out, ld_out, st) : launch_stream<2, 2>(ix, Q, B, lq, out, ld_out, st);
+  if (B <= kLongDirectMaxB) return launch_direct<2>(ix, Q, B, lq, out, ld_out, st);
   switch (ix->ld) {
     case 256:
       return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true, false, 0, 256>(
@@ -3735,12 +3897,18 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
                                                                                kScanDynFrac, kScanTaskDocs, nullptr,
                                                                                ctr_ws, ft);
   if (variant == kScanAuto)
-    variant = B <= kDirectMaxB ? (B == 1 ? kScanDirectQ1 : kScanDirectQ2) : pick_shape(kBf16Shapes, B);
+    variant = B <= kDirectMaxB ? (B == 1 ? kScanStreamQ1 : kScanStreamQ2) : pick_shape(kBf16Shapes, B);
   switch (variant) {
     case kScanDirectQ1:
       return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
     case kScanDirectQ2:
       return launch_direct<2>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ1:
+      return launch_stream<1, 2>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ2:
+      return launch_stream<2, 2>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ1Cached:
+      return launch_stream<1, 0>(ix, Q, B, lq, out, ld_out, st);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
