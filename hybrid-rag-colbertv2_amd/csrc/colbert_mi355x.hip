@@ -1983,6 +1983,126 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// MXFP8 streaming small-batch scan (B <= 2, QW = 2; production): the bf16
+// streaming scan's design on e4m3 tiles.  A 16-row tile is 2 KiB of tokens
+// (two 1 KiB LDS-DMA pieces, rows 8p .. 8p + 7, XOR-swizzled into the layout
+// lds_afrag_f8 reads) plus its 32 scale bytes (one 4-byte-per-lane LDS-DMA:
+// lanes 0-7 fetch the tile's scales, lanes 8-63 repeat them, so no lane reads
+// past the scale array); 3 ops per tile, 16 tile slots per wave (36 KiB), the
+// oldest tile waited with a constant vmcnt(45).  The direct scan's tiles,
+// masks, max order and epilogue: bit-identical scores.
+// ---------------------------------------------------------------------------
+constexpr int kF8SlotBytes = 2048 + 256;
+template <int QW, int AUX, int WAVES = 4, int SLOTS = 16>
+__global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_f8_stream_kernel(
+    const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
+    int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
+    float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int ld) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[WAVES * SLOTS * kF8SlotBytes];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const int nq_groups = (B + QW - 1) / QW;
+  const int64_t lin = (int64_t)blockIdx.x * WAVES + wave;      // one doc chunk per wave
+  const int qg = (int)(lin % nq_groups);
+  const int64_t chunk = lin / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;  // uniform over the wave; no block-level sync below
+  const int nd = (int)(d_end - d_begin);
+  uint8_t* ring = smem + wave * (SLOTS * kF8SlotBytes);
+  const int32_t* dls = doclens + d_begin;
+  auto ntiles = [&](int d) -> int {
+    int dl = sload_len(dls + d);
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    return (dl + 15) >> 4;
+  };
+  // token piece p of a tile = its rows 8p .. 8p + 7; lane l writes position
+  // l & 7 of row 8p + (l >> 3), so it fetches logical slot position ^ swz8(row)
+  uint32_t src_off[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int t = 8 * p + (lane >> 3);
+    src_off[p] = (uint32_t)(t * kDim + 16 * ((lane & 7) ^ swz8(t)));
+  }
+  const uint32_t sc_off = 4u * (uint32_t)(lane & 7);
+  int idoc = 0, itile = 0, intl = ntiles(0);
+  while (intl == 0 && ++idoc < nd) intl = ntiles(idoc);
+  int issued = 0;
+  const uint8_t* tb = tokens + (size_t)d_begin * ld * kDim;
+  const uint8_t* sb = tscales + (size_t)d_begin * ld * 2;
+  auto issue_next = [&]() {
+    if (idoc >= nd) return;
+    const size_t row0 = (size_t)idoc * ld + (size_t)itile * 16;
+    uint8_t* dst = ring + (issued & (SLOTS - 1)) * kF8SlotBytes;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(tb + row0 * kDim + src_off[p]), (lds_void_t*)(dst + p * 1024), 16,
+                                       0, AUX);
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)(sb + row0 * 2 + sc_off), (lds_void_t*)(dst + 2048), 4, 0, AUX);
+    ++issued;
+    if (++itile >= intl) {
+      itile = 0;
+      intl = 0;
+      while (intl == 0 && ++idoc < nd) intl = ntiles(idoc);
+    }
+  };
+  i32x8 qa[QW][2];
+  int qs[QW][2];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag_f8(Qb, Qs, qg * QW + q, B, lq, lane, qa[q], qs[q]);
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the query fragments: out of the ring's count
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) issue_next();
+
+  int consumed = 0;
+  for (int i = 0; i < nd; ++i) {
+    int dl = sload_len(dls + i);
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    const int nt = (dl + 15) >> 4;
+    float m[QW][2];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    for (int t = 0; t < nt; ++t) {
+      if (issued - consumed >= SLOTS)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (SLOTS - 1)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint8_t* slot = ring + (consumed & (SLOTS - 1)) * kF8SlotBytes;
+      const uint8_t* row = slot + c * kDim;
+      const int sw = swz8(c);
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g) ^ sw));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g + 1) ^ sw));
+      const int as = slot[2048 + c * 2 + (g & 1)];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is read: refill it
+      ++consumed;
+      issue_next();
+      const i32x8 a = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2],
+                            (int)hi[3]};
+      const f32x4 init = (dl >= 16 * t + 16) ? f32x4{} : row_mask_init16(16 * t + 4 * g, dl);
+      tile_f8<QW>(a, as, qa, qs, init, m);
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = qg * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Row top-k: exact radix select (11/11/10-bit digits of the order-preserving
 // score key; if the k-th score is tied, a second radix select over ~index picks
 // the lowest indices), then a bitonic sort of the k winners in LDS.
@@ -4012,8 +4132,29 @@ int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, 
                                                                             kScanDynFrac, kScanTaskDocs, ctr_ws);
 }
 
+// The MXFP8 streaming scan (B <= 2, any ld): one 4-wave workgroup per CU,
+// chunks for kDirectOversub x the resident waves.
+template <int WAVES = 4, int SLOTS = 16>
+int launch_f8_stream(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
+                     hipStream_t st) {
+  constexpr int QW = 2;
+  const int nq_groups = (B + QW - 1) / QW;
+  int64_t n_chunks = (int64_t)WAVES * cu_count(ix->device) * kDirectOversub / nq_groups;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  if (n_chunks < 1) n_chunks = 1;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
+  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  hipLaunchKernelGGL((maxsim_scan_f8_stream_kernel<QW, 2, WAVES, SLOTS>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
+                     ix->tokens,
+                     ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
+  return launch_check("maxsim_scan_f8_stream_kernel");
+}
+
 int scan_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                  hipStream_t st, int* ctr_ws) {
+  if (B <= kF8DirectMaxB) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
   if (B <= kF8DirectMaxB) {
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
@@ -4051,7 +4192,9 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st,
                                                                       frac(kScanDynFrac), task_docs, ctr_ws, ft);
   if (B > kF8DirectMaxB && shape == 0) shape = pick_shape(kF8Shapes, B);
-  if (B <= kF8DirectMaxB && shape == 0) {
+  if (B <= kF8DirectMaxB && shape == 0) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
+  if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<8, 8>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 20) {   // lab: the direct scan
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
     const int64_t target_waves = 8LL * cu_count(ix->device);
