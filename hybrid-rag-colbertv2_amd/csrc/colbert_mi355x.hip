@@ -1988,9 +1988,14 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
 // (two 1 KiB LDS-DMA pieces, rows 8p .. 8p + 7, XOR-swizzled into the layout
 // lds_afrag_f8 reads) plus its 32 scale bytes (one 4-byte-per-lane LDS-DMA:
 // lanes 0-7 fetch the tile's scales, lanes 8-63 repeat them, so no lane reads
-// past the scale array); 3 ops per tile, 16 tile slots per wave (36 KiB), the
-// oldest tile waited with a constant vmcnt(45).  The direct scan's tiles,
-// masks, max order and epilogue: bit-identical scores.
+// past the scale array); 3 ops per tile, SLOTS tile slots per wave, the oldest
+// tile waited with a constant vmcnt(3 (SLOTS - 1)).  The direct scan's tiles,
+// masks, max order and epilogue: bit-identical scores.  An f8 tile is half
+// the bytes of a bf16 one for the same per-tile waits, so the production
+// shape runs 8 waves x 8 slots (147 KiB per CU): lab, same process, 1.25M
+// docs B=1 3.346 -> 3.071 ms (direct -> 8 x 8; 4 x 16: 3.33 on another box,
+// 16 x 4: 3.098), B=2 3.417 -> 3.115, 125k 0.349 -> 0.311
+// (profiles/r03ai_*).
 // ---------------------------------------------------------------------------
 constexpr int kF8SlotBytes = 2048 + 256;
 template <int QW, int AUX, int WAVES = 4, int SLOTS = 16>
@@ -4134,7 +4139,7 @@ int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, 
 
 // The MXFP8 streaming scan (B <= 2, any ld): one 4-wave workgroup per CU,
 // chunks for kDirectOversub x the resident waves.
-template <int WAVES = 4, int SLOTS = 16>
+template <int WAVES = 8, int SLOTS = 8>
 int launch_f8_stream(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                      hipStream_t st) {
   constexpr int QW = 2;
@@ -4193,7 +4198,8 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                                                                       frac(kScanDynFrac), task_docs, ctr_ws, ft);
   if (B > kF8DirectMaxB && shape == 0) shape = pick_shape(kF8Shapes, B);
   if (B <= kF8DirectMaxB && shape == 0) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
-  if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<8, 8>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<4, 16>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 21) return launch_f8_stream<16, 4>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 20) {   // lab: the direct scan
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;

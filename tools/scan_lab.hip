@@ -480,7 +480,7 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
                                      variant % 100);
   if (variant == 1 || (B <= kF8SmallMaxB && variant < 10)) return scan_f8(ix, Qb, B, lq, out, ld, st);
   if (variant == 2) return scan_f8(ix, Qb, B, lq, out, ld, st, 0.0f);  // doc-interleaved, static split only
-  if (variant >= 10 && variant <= 30) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
+  if (variant >= 10 && variant <= 40) return scan_f8(ix, Qb, B, lq, out, ld, st, kScanDynFrac, kScanTaskDocs,
                                                      variant - 10);  // iteration shapes, see scan_f8
   constexpr int QPB = kF8Waves * kF8QW;
   const int nq_groups = (B + QPB - 1) / QPB;
