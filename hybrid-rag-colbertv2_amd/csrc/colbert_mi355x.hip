@@ -1202,24 +1202,24 @@ __device__ __forceinline__ int sload_len(const int32_t* p) {
   asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   return v;
 }
-template <int QW, int AUX>
-__global__ __launch_bounds__(256, 1) void maxsim_scan_stream_kernel(
+template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots>
+__global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
     int ld) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * kStreamSlots * 4096];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[WAVES * SLOTS * 4096];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
   const int nq_groups = (B + QW - 1) / QW;
-  const int64_t lin = (int64_t)blockIdx.x * 4 + wave;      // one doc chunk per wave
+  const int64_t lin = (int64_t)blockIdx.x * WAVES + wave;      // one doc chunk per wave
   const int qg = (int)(lin % nq_groups);
   const int64_t chunk = lin / nq_groups;
   const int64_t d_begin = chunk * chunk_docs;
   const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
   if (d_begin >= d_end) return;  // uniform over the wave; no block-level sync below
   const int nd = (int)(d_end - d_begin);
-  uint8_t* ring = smem + wave * (kStreamSlots * 4096);
+  uint8_t* ring = smem + wave * (SLOTS * 4096);
   const size_t doc_bytes = (size_t)ld * kRowBytes;
   const int32_t* dls = doclens + d_begin;
   // 32-bit cursor arithmetic keeps every comparison on the scalar unit (a
@@ -1249,7 +1249,7 @@ __global__ __launch_bounds__(256, 1) void maxsim_scan_stream_kernel(
   auto issue_next = [&]() {
     if (idoc >= nd) return;
     const uint8_t* base = tbase + (size_t)idoc * doc_bytes + (size_t)itile * 16 * kRowBytes;
-    uint8_t* dst = ring + (issued & (kStreamSlots - 1)) * 4096;
+    uint8_t* dst = ring + (issued & (SLOTS - 1)) * 4096;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + src_off[q]), (lds_void_t*)(dst + q * 1024), 16, 0, AUX);
@@ -1268,7 +1268,7 @@ __global__ __launch_bounds__(256, 1) void maxsim_scan_stream_kernel(
   for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the query fragments: out of the ring's count
 #pragma unroll
-  for (int k = 0; k < kStreamSlots; ++k) issue_next();
+  for (int k = 0; k < SLOTS; ++k) issue_next();
 
   int consumed = 0;
   for (int i = 0; i < nd; ++i) {
@@ -1281,12 +1281,12 @@ __global__ __launch_bounds__(256, 1) void maxsim_scan_stream_kernel(
     for (int t = 0; t < nt; ++t) {
       // 8 tiles in flight: the oldest 4 pieces are this tile's (later loads
       // and stores only make the wait stricter); fewer: the stream is ending
-      if (issued - consumed >= kStreamSlots)
-        asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+      if (issued - consumed >= SLOTS)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SLOTS - 1)) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bf16x8 a[4];
-      const uint8_t* row = ring + (consumed & (kStreamSlots - 1)) * 4096 + c * kRowBytes;
+      const uint8_t* row = ring + (consumed & (SLOTS - 1)) * 4096 + c * kRowBytes;
       const int sw = swz16(c);
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) a[s4] = *reinterpret_cast<const bf16x8*>(row + 16 * ((4 * g + s4) ^ sw));
@@ -3740,7 +3740,7 @@ enum ScanVariant {
   kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
   kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
-  kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16,
+  kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -3967,19 +3967,20 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
 // Streaming scans (variants 14-16; 14 / 15 are the B = 1 / 2 production
 // scans of every bf16 index, long documents included): one 4-wave workgroup
 // per CU (128 KiB of LDS rings), chunks for kDirectOversub x the resident waves.
-template <int QW, int AUX>
+template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots>
 int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
   if (ix->dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "stream scan: bf16 index only");
   const int nq_groups = (B + QW - 1) / QW;
-  const int64_t target_waves = 4LL * cu_count(ix->device) * kDirectOversub;
+  const int64_t target_waves = (int64_t)WAVES * cu_count(ix->device) * kDirectOversub;
   int64_t n_chunks = target_waves / nq_groups;
   if (n_chunks > ix->n) n_chunks = ix->n;
   if (n_chunks < 1) n_chunks = 1;
   const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
-  const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
+  const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
+  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
+                     ix->tokens,
                      ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
   return launch_check("maxsim_scan_stream_kernel");
 }
@@ -4034,6 +4035,8 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_stream<2, 2>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ1Cached:
       return launch_stream<1, 0>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ1W8:   // lab: 8 waves x 4 tile slots per CU
+      return launch_stream<1, 2, 8, 4>(ix, Q, B, lq, out, ld_out, st);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
