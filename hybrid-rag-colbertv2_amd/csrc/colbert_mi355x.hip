@@ -3740,7 +3740,8 @@ enum ScanVariant {
   kScan32Shfl = 0, kScan32Dpp = 1, kScan16W4 = 2, kScan16W8 = 3, kScan32DppW8 = 4,
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
   kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
-  kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17,
+  kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17, kScanStreamQ4 = 18,
+  kScanStreamQ8 = 19,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -4037,6 +4038,10 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_stream<1, 0>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ1W8:   // lab: 8 waves x 4 tile slots per CU
       return launch_stream<1, 2, 8, 4>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ4:     // lab: B <= 4 in one query group
+      return launch_stream<4, 2>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ8:     // lab: B <= 8 in one query group
+      return launch_stream<8, 2>(ix, Q, B, lq, out, ld_out, st);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
