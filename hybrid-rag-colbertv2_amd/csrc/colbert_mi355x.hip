@@ -4038,6 +4038,8 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_stream<1, 0>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ1W8:   // lab: 8 waves x 4 tile slots per CU
       return launch_stream<1, 2, 8, 4>(ix, Q, B, lq, out, ld_out, st);
+    // lab, 1M docs, same process (profiles/r03z_lab_stream_qg_1m.log): B=4
+    // 5.72 ms vs 5.69 for variant 13; B=8 9.95 (18) / 8.58 (19) vs 5.98: not kept
     case kScanStreamQ4:     // lab: B <= 4 in one query group
       return launch_stream<4, 2>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ8:     // lab: B <= 8 in one query group
