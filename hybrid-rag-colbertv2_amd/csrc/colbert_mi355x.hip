@@ -1998,7 +1998,9 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
 // (profiles/r03ai_*).
 // ---------------------------------------------------------------------------
 constexpr int kF8SlotBytes = 2048 + 256;
-template <int QW, int AUX, int WAVES = 4, int SLOTS = 16>
+// TW2 (lab): two tiles of one doc per wait (one vmcnt wait, one lgkmcnt wait
+// and one refill of two slots per pair; odd tails take the one-tile step).
+template <int QW, int AUX, int WAVES = 4, int SLOTS = 16, bool TW2 = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_f8_stream_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -2072,6 +2074,39 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_f8_stream_kernel(
 #pragma unroll
     for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     for (int t = 0; t < nt; ++t) {
+      if (TW2 && t + 1 < nt) {
+        // the ring is full unless the stream is ending: the oldest two tiles
+        // have landed once at most SLOTS - 2 tiles (3 ops each) are in flight
+        if (issued - consumed >= SLOTS)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (SLOTS - 2)) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 lo[2], hi[2];
+        int as2[2];
+        const int sw = swz8(c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint8_t* slot = ring + ((consumed + u) & (SLOTS - 1)) * kF8SlotBytes;
+          const uint8_t* row = slot + c * kDim;
+          lo[u] = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g) ^ sw));
+          hi[u] = *reinterpret_cast<const u32x4*>(row + 16 * ((2 * g + 1) ^ sw));
+          as2[u] = slot[2048 + c * 2 + (g & 1)];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // both slots read: refill them
+        consumed += 2;
+        issue_next();
+        issue_next();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const i32x8 a = i32x8{(int)lo[u][0], (int)lo[u][1], (int)lo[u][2], (int)lo[u][3],
+                                (int)hi[u][0], (int)hi[u][1], (int)hi[u][2], (int)hi[u][3]};
+          const int tt = t + u;
+          const f32x4 init = (dl >= 16 * tt + 16) ? f32x4{} : row_mask_init16(16 * tt + 4 * g, dl);
+          tile_f8<QW>(a, as2[u], qa, qs, init, m);
+        }
+        ++t;
+        continue;
+      }
       if (issued - consumed >= SLOTS)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (SLOTS - 1)) : "memory");
       else
@@ -4149,7 +4184,7 @@ int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, 
 
 // The MXFP8 streaming scan (B <= 2, any ld): one 4-wave workgroup per CU,
 // chunks for kDirectOversub x the resident waves.
-template <int WAVES = 8, int SLOTS = 8>
+template <int WAVES = 8, int SLOTS = 8, bool TW2 = false>
 int launch_f8_stream(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                      hipStream_t st) {
   constexpr int QW = 2;
@@ -4161,7 +4196,7 @@ int launch_f8_stream(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_f8_stream_kernel<QW, 2, WAVES, SLOTS>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
+  hipLaunchKernelGGL((maxsim_scan_f8_stream_kernel<QW, 2, WAVES, SLOTS, TW2>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
                      ix->tokens,
                      ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
   return launch_check("maxsim_scan_f8_stream_kernel");
@@ -4170,19 +4205,6 @@ int launch_f8_stream(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B
 int scan_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                  hipStream_t st, int* ctr_ws) {
   if (B <= kF8DirectMaxB) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
-  if (B <= kF8DirectMaxB) {
-    constexpr int QW = 2;
-    const int nq_groups = (B + QW - 1) / QW;
-    int64_t n_chunks = 8LL * cu_count(ix->device) / nq_groups;
-    if (n_chunks > ix->n) n_chunks = ix->n;
-    if (n_chunks < 1) n_chunks = 1;
-    const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
-    n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
-    const int64_t grid = ((int64_t)nq_groups * n_chunks + 3) / 4;
-    hipLaunchKernelGGL((maxsim_scan_f8_direct_kernel<QW, true>), dim3((unsigned)grid), dim3(256), 0, st, ix->tokens,
-                       ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
-    return launch_check("maxsim_scan_f8_direct_kernel");
-  }
   switch (ix->ld) {
     case 256: return launch_f8_long<256>(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
     case 512: return launch_f8_long<512>(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
@@ -4210,6 +4232,8 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   if (B <= kF8DirectMaxB && shape == 0) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
   if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<4, 16>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 21) return launch_f8_stream<16, 4>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 22) return launch_f8_stream<8, 8, true>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 23) return launch_f8_stream<4, 16, true>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 20) {   // lab: the direct scan
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
