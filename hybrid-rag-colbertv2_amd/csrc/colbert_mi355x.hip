@@ -1998,9 +1998,13 @@ __global__ __launch_bounds__(256, 2) void maxsim_scan_f8_direct_kernel(
 // (profiles/r03ai_*).
 // ---------------------------------------------------------------------------
 constexpr int kF8SlotBytes = 2048 + 256;
-// TW2 (lab): two tiles of one doc per wait (one vmcnt wait, one lgkmcnt wait
-// and one refill of two slots per pair; odd tails take the one-tile step).
-template <int QW, int AUX, int WAVES = 4, int SLOTS = 16, bool TW2 = false>
+// TW2 (production since r03z): two tiles of one doc per wait (one vmcnt
+// wait, one lgkmcnt wait and one refill of two slots per pair; odd tails take
+// the one-tile step).  Lab, same process, bit-identical
+// (profiles/r03z_lab_f8_tw2.log: variant 10 = one tile per wait, 32 = TW2 at
+// 8 x 8, 33 = TW2 at 4 x 16): 1.25M docs B=1 3.320 -> 3.282 ms, B=2 3.178 ->
+// 3.155, 125k B=1 0.318 -> 0.316; at 4 x 16 B=2 and 125k lose (3.342 / 0.423).
+template <int QW, int AUX, int WAVES = 4, int SLOTS = 16, bool TW2 = true>
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_f8_stream_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -4184,7 +4188,7 @@ int launch_f8_long(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, 
 
 // The MXFP8 streaming scan (B <= 2, any ld): one 4-wave workgroup per CU,
 // chunks for kDirectOversub x the resident waves.
-template <int WAVES = 8, int SLOTS = 8, bool TW2 = false>
+template <int WAVES = 8, int SLOTS = 8, bool TW2 = true>
 int launch_f8_stream(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                      hipStream_t st) {
   constexpr int QW = 2;
@@ -4230,10 +4234,11 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                                                                       frac(kScanDynFrac), task_docs, ctr_ws, ft);
   if (B > kF8DirectMaxB && shape == 0) shape = pick_shape(kF8Shapes, B);
   if (B <= kF8DirectMaxB && shape == 0) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
-  if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<4, 16>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
-  if (B <= kF8DirectMaxB && shape == 21) return launch_f8_stream<16, 4>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
-  if (B <= kF8DirectMaxB && shape == 22) return launch_f8_stream<8, 8, true>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
-  if (B <= kF8DirectMaxB && shape == 23) return launch_f8_stream<4, 16, true>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<4, 16, false>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  if (B <= kF8DirectMaxB && shape == 21) return launch_f8_stream<16, 4, false>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
+  // lab: one tile per wait (the production 8 x 8 ring before TW2) / TW2 at 4 x 16
+  if (B <= kF8DirectMaxB && shape == 22) return launch_f8_stream<8, 8, false>(ix, Qb, Qs, B, lq, out, ld_out, st);
+  if (B <= kF8DirectMaxB && shape == 23) return launch_f8_stream<4, 16, true>(ix, Qb, Qs, B, lq, out, ld_out, st);
   if (B <= kF8DirectMaxB && shape == 20) {   // lab: the direct scan
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
