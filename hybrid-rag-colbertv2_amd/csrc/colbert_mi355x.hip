@@ -1202,7 +1202,8 @@ __device__ __forceinline__ int sload_len(const int32_t* p) {
   asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   return v;
 }
-template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots>
+// TW2 (lab): two tiles of one doc per wait, as the MXFP8 streaming scan.
+template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
@@ -1279,6 +1280,33 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
 #pragma unroll
     for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     for (int t = 0; t < nt; ++t) {
+      if (TW2 && t + 1 < nt) {
+        if (issued - consumed >= SLOTS)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SLOTS - 2)) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bf16x8 a2[2][4];
+        const int sw = swz16(c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint8_t* row = ring + ((consumed + u) & (SLOTS - 1)) * 4096 + c * kRowBytes;
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            a2[u][s4] = *reinterpret_cast<const bf16x8*>(row + 16 * ((4 * g + s4) ^ sw));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // both slots read: refill them
+        consumed += 2;
+        issue_next();
+        issue_next();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int tt = t + u;
+          const f32x4 init = (dl >= 16 * tt + 16) ? f32x4{} : row_mask_init16(16 * tt + 4 * g, dl);
+          tile16<QW>(a2[u], qf, init, m);
+        }
+        ++t;
+        continue;
+      }
       // 8 tiles in flight: the oldest 4 pieces are this tile's (later loads
       // and stores only make the wait stricter); fewer: the stream is ending
       if (issued - consumed >= SLOTS)
@@ -3780,7 +3808,7 @@ enum ScanVariant {
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
   kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
   kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17, kScanStreamQ4 = 18,
-  kScanStreamQ8 = 19,
+  kScanStreamQ8 = 19, kScanStreamQ1Tw2 = 20, kScanStreamQ2Tw2 = 21,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -4007,7 +4035,7 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
 // Streaming scans (variants 14-16; 14 / 15 are the B = 1 / 2 production
 // scans of every bf16 index, long documents included): one 4-wave workgroup
 // per CU (128 KiB of LDS rings), chunks for kDirectOversub x the resident waves.
-template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots>
+template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
 int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
   if (ix->dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "stream scan: bf16 index only");
   const int nq_groups = (B + QW - 1) / QW;
@@ -4019,7 +4047,7 @@ int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
+  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS, TW2>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
                      ix->tokens,
                      ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
   return launch_check("maxsim_scan_stream_kernel");
@@ -4083,6 +4111,10 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_stream<4, 2>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ8:     // lab: B <= 8 in one query group
       return launch_stream<8, 2>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ1Tw2:  // lab: two tiles per wait
+      return launch_stream<1, 2, 4, kStreamSlots, true>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ2Tw2:
+      return launch_stream<2, 2, 4, kStreamSlots, true>(ix, Q, B, lq, out, ld_out, st);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
