@@ -1202,7 +1202,8 @@ __device__ __forceinline__ int sload_len(const int32_t* p) {
   asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   return v;
 }
-// TW2 (lab): two tiles of one doc per wait, as the MXFP8 streaming scan.
+// TW2 (lab): two tiles of one doc per wait, as the MXFP8 streaming scan;
+// neutral here (1M B=1 4.722 vs 4.708 ms, profiles/r03z_lab_bf16_tw2.log).
 template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
