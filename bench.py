@@ -3,24 +3,29 @@
 1M-chunk x 128-token synthetic corpus, top-10 rerank (BASELINE.json metric,
 config 3).
 
-One STEP = one batch of B=256 queries (embeddings + BM25 term ids) through
-the whole path:
+The headline line runs on the fp32-FAITHFUL index (the default, and the
+package's: RAGConfig.index_dtype = "fp32"): the reference keeps fp32
+embeddings and scores them in fp32 (LRC:735-746, 802-831), and this index
+returns those scores within 1e-4 (bf16 hi scanned on the MFMA, every doc that
+can reach the top-k rescored with the bf16 residual).
+
+One STEP = one batch of B=256 queries through the whole path:
   stage 1  host BM25 top-100 (native C++, csrc/host_bm25.cpp) over the
            synthetic 1M-doc term corpus -- run while the GPU scans,
-  stage 2  HIP MaxSim scan + radix top-100 (the top-k fused into the scan,
-           --fused-topk, is ~1 % slower on MI355X: profiles/history/r02/r02k; sharded over
-           ranks: per-rank top-100 -> RCCL all-gather -> HIP merge; the ranks'
-           BM25 lists over their doc shards ride the same all-gather),
+  stage 2  HIP MaxSim scan + top-100 (+ the faithful band: rescoring of the
+           docs the bf16 scan cannot rule out); sharded over ranks: per-rank
+           top-100 -> RCCL all-gather -> HIP merge (the ranks' BM25 lists over
+           their doc shards ride the same all-gather),
   fusion   host RRF (native C++, reference semantics) -> top-50 candidates,
   stage 3  HIP gather-by-id MaxSim rerank -> top-10 (sharded: RCCL all-reduce MAX).
 Inputs (the query batch and term ids, both indexes) are resident before the
 timed region; every stage runs in full inside every timed step.
 
 The JSON line also carries, measured in the same run:
-  faithful         the same K steps on the fp32-faithful index (the reference's
-                   fp32 arithmetic within 1e-4: bf16 scan + certified band
-                   rescoring), checked against the float64
-                   oracle of the fp32 values at 1e-4;
+  bf16             (fp32 main) the same K steps + p50 on a bf16 index of the
+                   same corpus (the faithful index's hi tokens, no copy);
+                   `--dtype bf16` swaps the two (main bf16, side leg "faithful");
+  roofline.band_ms the faithful band work per step (HIP events, timed region);
   native_exchange  (N > 1, RCCL) the same K steps with the exchange inside the
                    C ABI (cbv2_search_sharded_* / cbv2_rerank_sharded);
   cpu_baseline     (N = 1 only; null at N > 1) the CPU restatements timed on
@@ -28,11 +33,13 @@ The JSON line also carries, measured in the same run:
                    restatement; the literal mean-pool scorer), with the CPU
                    model and thread count;
   p50 / p99        single-query latency of the whole hot path.
+Every optional leg agrees across ranks before its collectives (run_leg): a
+rank that fails one records the error in the line with every other rank.
 
 N>1: the SAME 1M-doc corpus is split into N contiguous shards, one per rank
 (strong scaling); value = B*K / max-over-ranks wall time.
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
+Run:  python bench.py [--gpus N --steps K --warmup W] [--dtype fp32|bf16|fp8]
       torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
@@ -133,11 +140,11 @@ def cpu_baseline(Q: torch.Tensor, tokens: torch.Tensor, n_total: int, budget_s: 
                      "value": round(reps / (dt_l * n_total / n_s), 6), "cores": threads,
                      "sample": f"{reps} queries x {n_s} docs, {dt_l:.1f}s"})
     try:   # scalar C restatement on the same bf16 values (oracle/cbv2_oracle.c)
-        qb = Q[:1].contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
+        qb = Q[:1].to(torch.bfloat16).contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
         n_c = 64
         t0 = time.perf_counter()
         while True:
-            db = tokens[:n_c].contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
+            db = tokens[:n_c].to(torch.bfloat16).contiguous().cpu().view(torch.int16).numpy().view(np.uint16)
             t1 = time.perf_counter()
             orc.c_maxsim_bf16(qb, db, np.full(n_c, LD, np.int32))
             dt_c = time.perf_counter() - t1
@@ -216,7 +223,10 @@ def c45_legs(args, B, world, rank, dev, backend):
     contiguous shard per rank (1.25M at 8 ranks), B=256, stage 2 = scan +
     top-100 + ONE RCCL all-gather + HIP merge, K timed steps after W warmups:
     config 4 on bf16 tokens, config 5 on MXFP8 e4m3 tokens (block-scaled fp8
-    MFMA).  Checks: the merged top-10 of every query = its planted docs."""
+    MFMA).  Checks: the merged top-10 of every query = its planted docs.  Each
+    config is a ``run_leg``: a rank whose shard build fails (e.g. out of
+    memory) records the error with every other rank instead of stranding them
+    in the all-gather."""
     n_c = args.c45_docs
     b, e = shard_range(n_c, rank, world)
     Qf = synth.make_queries(B, LQ, seed=1)
@@ -224,38 +234,90 @@ def c45_legs(args, B, world, rank, dev, backend):
     Q = Qf.to(dev, torch.bfloat16)
     out = {"corpus_docs": n_c, "docs_per_gpu": e - b, "global_batch": B, "stage": "MaxSim top-100 + all-gather merge"}
     for name, fp8 in (("config4_bf16", False), ("config5_mxfp8", True)):
-        t0 = time.time()
-        if fp8:
-            q8, sc8, dl = synth.make_shard_mxfp8(b, e, Qf, planted, dev, seed=0)
-            ix = ColbertIndex(q8, dl, id_base=b, scales=sc8)
-        else:
-            tok, dl = synth.make_shard(b, e, Qf, planted, dev, seed=0)
-            ix = ColbertIndex(tok, dl, id_base=b)
-        srch = ShardedSearcher(ix, lexical_k=args.k)
-        torch.cuda.synchronize()
-        log(f"{name}: shard [{b},{e}) built in {time.time() - t0:.1f}s")
-        ix.time_scans(True)
-        outs, el = timed_steps(lambda K: [srch.search(Q, args.k) for _ in range(K)], args.steps, args.warmup, world)
-        scans = ix.scan_times()[-args.steps:]
-        ix.time_scans(False)
-        avg = sum(scans) / len(scans) if scans else float("nan")
-        per_rank = [r[0] for r in gather_floats([avg], world, dev, backend)]
-        ih = outs[-1][1].cpu().numpy()
-        peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
-        worst = max(per_rank)
-        achieved = B * (n_c // world) * FLOP_PER_PAIR / (worst * 1e-3) / 1e12
-        out[name] = {"value": round(B * args.steps / el, 2), "unit": "queries/s", "ms_per_step": round(el / args.steps * 1e3, 3),
-                     "scan_avg_ms_by_rank": [round(x, 3) for x in per_rank],
-                     "roofline_frac_slowest_rank": round(achieved / peak, 4), "peak_tflops": peak,
-                     "top10_equals_planted": float(np.mean([set(ih[q, :10]) == set(planted[q]) for q in range(B)])),
-                     "sorted": bool((torch.diff(outs[-1][0], dim=1) <= 0).all().item())}
-        del outs, srch, ix
-        if fp8:
-            del q8, sc8, dl
-        else:
-            del tok, dl
+        def prepare(fp8=fp8, name=name):
+            t0 = time.time()
+            if fp8:
+                q8, sc8, dl = synth.make_shard_mxfp8(b, e, Qf, planted, dev, seed=0)
+                ix = ColbertIndex(q8, dl, id_base=b, scales=sc8)
+            else:
+                tok, dl = synth.make_shard(b, e, Qf, planted, dev, seed=0)
+                ix = ColbertIndex(tok, dl, id_base=b)
+            ix.search(Q, args.k)           # local only: allocates the search workspace before any collective
+            torch.cuda.synchronize()
+            log(f"{name}: shard [{b},{e}) built in {time.time() - t0:.1f}s")
+            return ix
+
+        def run(ix, fp8=fp8):
+            srch = ShardedSearcher(ix, lexical_k=args.k)
+            ix.time_scans(True)
+            outs, el = timed_steps(lambda K: [srch.search(Q, args.k) for _ in range(K)], args.steps, args.warmup,
+                                   world)
+            scans = ix.scan_times()[-args.steps:]
+            avg = sum(scans) / len(scans) if scans else float("nan")
+            per_rank = [r[0] for r in gather_floats([avg], world, dev, backend)]
+            ih = outs[-1][1].cpu().numpy()
+            peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
+            achieved = B * (n_c // world) * FLOP_PER_PAIR / (max(per_rank) * 1e-3) / 1e12
+            return {"value": round(B * args.steps / el, 2), "unit": "queries/s",
+                    "ms_per_step": round(el / args.steps * 1e3, 3),
+                    "scan_avg_ms_by_rank": [round(x, 3) for x in per_rank],
+                    "roofline_frac_slowest_rank": round(achieved / peak, 4), "peak_tflops": peak,
+                    "top10_equals_planted": float(np.mean([set(ih[q, :10]) == set(planted[q]) for q in range(B)])),
+                    "sorted": bool((torch.diff(outs[-1][0], dim=1) <= 0).all().item())}
+
+        out[name] = run_leg(name, prepare, run, world, rank, dev, backend)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    return out
+
+
+def agree(ok: bool, world: int, dev, backend: str) -> bool:
+    """True on every rank iff ``ok`` on every rank (one all-reduce MIN; no-op at N = 1)."""
+    if world == 1:
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def _maybe_fail(name: str, rank: int):
+    """Failure injection for the N > 1 rehearsals (never set by the driver):
+    BENCH_FAIL_LEG=<leg> BENCH_FAIL_RANK=<r> raises inside that leg's local
+    preparation on rank r only."""
+    if os.environ.get("BENCH_FAIL_LEG") == name and int(os.environ.get("BENCH_FAIL_RANK", "-1")) == rank:
+        raise RuntimeError(f"injected failure (BENCH_FAIL_LEG={name}, rank {rank})")
+
+
+def run_leg(name: str, prepare, run, world: int, rank: int, dev, backend: str):
+    """An optional leg of the line, with symmetric failure handling across ranks.
+
+    ``prepare()`` does the leg's LOCAL work (index build, workspace warm-up with
+    a local search; no collectives) and may fail on one rank only (e.g. an OOM
+    from uneven free memory); ``run(state)`` runs the leg's collectives.  The
+    ranks agree (one all-reduce MIN) after ``prepare``: every rank then either
+    enters ``run`` or records the same error, so a failing rank never strands
+    its peers inside a collective.  ``run`` executes the same code on the same
+    shapes on every rank; its result is agreed on again afterwards.  Returns
+    the leg's dict, or {"error": ...} (the line still prints)."""
+    state, err = None, None
+    try:
+        _maybe_fail(name, rank)
+        state = prepare()
+    except Exception as e:   # noqa: BLE001  reported in the line
+        err = f"{type(e).__name__}: {str(e)[:300]}"
+    if not agree(err is None, world, dev, backend):
+        state = None
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        return {"error": err or f"{name}: failed on another rank (local preparation)"}
+    out, err = None, None
+    try:
+        out = run(state)
+    except Exception as e:   # noqa: BLE001
+        err = f"{type(e).__name__}: {str(e)[:300]}"
+    if not agree(err is None, world, dev, backend):
+        out = {"error": err or f"{name}: failed on another rank"}
     return out
 
 
@@ -272,7 +334,8 @@ def main():
     ap.add_argument("--p50-iters", type=int, default=100)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-faithful", action="store_true", help="skip the fp32-faithful leg")
+    ap.add_argument("--no-side-leg", "--no-faithful", dest="no_side_leg", action="store_true",
+                    help="skip the side leg (fp32 main: the bf16 leg; bf16 main: the fp32-faithful leg)")
     ap.add_argument("--check-queries", type=int, default=8)
     ap.add_argument("--no-pipeline", action="store_true", help="time unpipelined steps")
     ap.add_argument("--native-exchange", action="store_true",
@@ -282,9 +345,10 @@ def main():
                     help="BASELINE configs 4 / 5 (10M docs sharded over the ranks, stage 2, bf16 and MXFP8) as "
                          "extra legs of the line; auto = at 8 ranks (the configs' node)")
     ap.add_argument("--c45-docs", type=int, default=10_000_000, help="corpus of the config-4/5 legs")
-    ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
-                    help="index tokens: bf16 (config 3), MXFP8 e4m3 + E8M0 (config 5) or fp32-faithful "
-                         "(bf16 hi scanned + residual-certified band, DESIGN §3.7)")
+    ap.add_argument("--dtype", choices=["fp32", "bf16", "fp8"], default="fp32",
+                    help="index: fp32-faithful (default: the reference's fp32 arithmetic, LRC:735-746 / 802-831, "
+                         "within 1e-4 -- bf16 hi scanned + residual-certified band, DESIGN §3.7), bf16 tokens, "
+                         "or MXFP8 e4m3 + E8M0 (config 5)")
     args = ap.parse_args()
     # stdout carries exactly the ONE JSON line: everything else any layer prints
     # to fd 1 (Python, RCCL / gloo C++ logging) is sent to stderr from here on
@@ -323,12 +387,13 @@ def main():
     bm_all = lambda: lex.search(qt, qo, args.k)                 # noqa: E731  stage 1, whole batch
     bm_one = lambda: lex.search(qt[:qo[1]], qo[:2], args.k)     # noqa: E731  stage 1, query 0
     faithful = args.dtype == "fp32"
+    fp8 = args.dtype == "fp8"
     tokens, doclens = synth.make_shard(begin, end, Qf, planted, dev, seed=0,
                                        dtype=torch.float32 if faithful else torch.bfloat16)
     if faithful:
         # fp32-faithful index: bf16 hi scanned, bf16 residual gathered for the band (HIP split)
         ix = ColbertIndex.faithful_f32(tokens, doclens, id_base=begin)
-    elif args.dtype == "fp8":
+    elif fp8:
         ix = ColbertIndex.mxfp8(tokens, doclens, id_base=begin)   # quantized on the GPU (HIP kernel)
     else:
         ix = ColbertIndex(tokens, doclens, id_base=begin)
@@ -340,7 +405,7 @@ def main():
     Q = Qf.to(dev, torch.float32 if faithful else torch.bfloat16)
     Q1 = Q[:1].contiguous()
     torch.cuda.synchronize()
-    log(f"setup {time.time() - t_setup:.1f}s: rank {rank}/{world} docs [{begin},{end}) B={B}")
+    log(f"setup {time.time() - t_setup:.1f}s: rank {rank}/{world} docs [{begin},{end}) B={B} index {args.dtype}")
 
     def step(srch, Qb, lexical):
         """One batch, unpipelined (used for the B=1 latency)."""
@@ -358,29 +423,6 @@ def main():
             return lambda K: [step(srch, Qb, bm_all)[:2] for _ in range(K)]
         return lambda K: pipe.run([(Qb, bm_all)] * K)
 
-    ix.time_scans(True)      # HIP events around each scan launch, on its own stream (C ABI)
-    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world,
-                                on_start=lambda: searcher.time_collectives(True))
-    coll = searcher.collective_times()                  # the K timed steps' all-gathers / all-reduces
-    scan_ms = ix.scan_times()                           # the warmup + K scans; keep the K of the timed region
-    scan_ms = scan_ms[-args.steps:] if len(scan_ms) >= args.steps else scan_ms
-    qps = B * args.steps / elapsed
-    band = None
-    if faithful:                         # the band each query of the last timed batch rescored
-        bs = ix.last_band.float()
-        band = {"batch": B, "mean": round(float(bs.mean()), 1), "max": int(bs.max()),
-                "overflow_rows": int((bs < 0).sum())}
-
-    # ---- correctness of the timed output (size-independent properties)
-    fs, fi = outs[-1]
-    fi_h = fi.cpu().numpy()
-    top10_planted = float(np.mean([set(fi_h[b]) == set(planted[b]) for b in range(B)]))
-    sorted_ok = bool((torch.diff(fs, dim=1) <= 0).all().item())
-
-    # ---- p50 / p99 latency at batch 1 (whole hot path, one query).  One shard
-    # (or the native exchange): the one-round-trip path (cbv2_retrieve_begin /
-    # _finish: stages 2 -> host RRF -> 3 in C++, one host round trip); the
-    # torch.distributed exchange at N > 1: the stages one by one (`step`)
     def one_trip(srch):
         if srch.world > 1 and srch._nx is None:
             return None
@@ -407,6 +449,41 @@ def main():
         a, b = step(srch, Qb, bm_one), one(Qb, bm_one)
         return all(torch.equal(x, y) for x, y in zip(a, b))
 
+    def planted_frac(ids_h):
+        return float(np.mean([set(ids_h[b]) == set(planted[b]) for b in range(B)]))
+
+    # ---- the main leg: K timed steps.  The scan launches (and, fp32-faithful,
+    # each search's band work) are bracketed by HIP events recorded on their own
+    # stream by the C ABI (cbv2_index_time_scans); the collective times are
+    # read from a separate untimed pass below, not from the timed region
+    ix.time_scans(True)
+    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world)
+    scan_ms = ix.scan_times()                           # the warmup + K scans; keep the K of the timed region
+    scan_ms = scan_ms[-args.steps:] if len(scan_ms) >= args.steps else scan_ms
+    band_ms = ix.band_times()[-args.steps:] if faithful else []
+    qps = B * args.steps / elapsed
+    band = None
+    if faithful:                         # the band each query of the last timed batch rescored
+        bs = ix.last_band.float()
+        band = {"batch": B, "mean": round(float(bs.mean()), 1), "max": int(bs.max()),
+                "overflow_rows": int((bs < 0).sum())}
+    coll = {}
+    if world > 1:                        # per-step collective times: 2 untimed steps, instrumented
+        searcher.time_collectives(True)
+        stepper(searcher, Q)(2)
+        torch.cuda.synchronize()
+        coll = {k: {f: v / 2 for f, v in d.items()} for k, d in searcher.collective_times().items()}
+
+    # ---- correctness of the timed output (size-independent properties)
+    fs, fi = outs[-1]
+    fi_h = fi.cpu().numpy()
+    top10_planted = planted_frac(fi_h)
+    sorted_ok = bool((torch.diff(fs, dim=1) <= 0).all().item())
+
+    # ---- p50 / p99 latency at batch 1 (whole hot path, one query).  One shard
+    # (or the native exchange): the one-round-trip path (cbv2_retrieve_begin /
+    # _finish: stages 2 -> host RRF -> 3 in C++, one host round trip); the
+    # torch.distributed exchange at N > 1: the stages one by one (`step`)
     one = one_trip(searcher)
     one_same = same_as_step(searcher, one, Q1) if one is not None else None
     _, p50_step, _ = latency(searcher, Q1) if one is not None else (None, None, None)
@@ -419,19 +496,19 @@ def main():
         bm_all()
         bm_ms.append((time.perf_counter() - t) * 1e3)
 
-    # ---- dominant kernel: the MaxSim scan launches of the timed region above,
-    # each bracketed by HIP events recorded on the scan's own stream by the C
-    # ABI (cbv2_index_time_scans); fp32-faithful: the bf16 scan of hi
+    # ---- dominant kernel: the MaxSim scan launches of the timed region above
+    # (fp32-faithful: the bf16 scan of hi, the same kernel and template)
     if len(scan_ms) != args.steps:
         log(f"warning: {len(scan_ms)} timed scans recorded for {args.steps} steps")
     scan_avg = sum(scan_ms) / len(scan_ms) if scan_ms else float("nan")
+    band_avg = sum(band_ms) / len(band_ms) if band_ms else None
     achieved = B * n_local * FLOP_PER_PAIR / (scan_avg * 1e-3) / 1e12
     fused_topk = ix.fused_topk_slots(B, args.k) > 0
     # HBM bytes per launch from the committed PMC passes of the same kernel and
     # shape (tools/profile_round.sh -> tools/pmc_summary.py); null otherwise
     traffic = clock = traffic_src = mfma_busy = None
     pmc = os.path.join(ROOT, "profiles", "pmc_scan.json")
-    want = "maxsim_scan_f8x4_kernel" if args.dtype == "fp8" else SCAN_KERNEL
+    want = "maxsim_scan_f8x4_kernel" if fp8 else SCAN_KERNEL
     variant = "fused" if fused_topk else "unfused"
     if os.path.exists(pmc):
         with open(pmc) as f:
@@ -448,8 +525,8 @@ def main():
                                f"{n_local} docs/GPU, one MI355X), not this run")
     # every rank's scan time and collective time per step (max-over-ranks view of N > 1)
     names = ("all_gather", "all_reduce_max")
-    mine = [scan_avg] + [coll.get(k, {}).get(f, 0.0) / args.steps for k in names for f in ("device_ms", "host_ms")] \
-        + [coll.get(k, {}).get("calls", 0) / args.steps for k in names]
+    mine = [scan_avg] + [coll.get(k, {}).get(f, 0.0) for k in names for f in ("device_ms", "host_ms")] \
+        + [coll.get(k, {}).get("calls", 0) for k in names]
     per_rank = gather_floats(mine, world, dev, backend)
     collectives = None
     if world > 1:
@@ -458,63 +535,51 @@ def main():
                            "host_ms_per_step_max": round(max(r[2 + 2 * j] for r in per_rank), 4),
                            "device_ms_per_step_by_rank": [round(r[1 + 2 * j], 4) for r in per_rank]}
                        for j, k in enumerate(names)}
-        collectives["timing"] = ("HIP events on the issuing stream (device_ms; RCCL) and host wall time of "
-                                 "the call (host_ms; gloo blocks the host), summed per step over the K timed steps")
+        collectives["timing"] = ("2 untimed steps after the timed region, instrumented: HIP events on the issuing "
+                                 "stream (device_ms; RCCL) and host wall time of the call (host_ms; gloo blocks "
+                                 "the host), per step")
 
     # ---- spot parity: oracle MaxSim of the final candidates, on the owning rank
     check_rows = list(range(min(args.check_queries, B)))
-    if args.dtype == "fp8":              # the oracle scores the same dequantized fp8 values
+    if fp8:                              # the oracle scores the same dequantized fp8 values
         from oracle import oracle as orc
         qq, qs = quantize_mxfp8(Q)
         Qd = orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy())
         docs_fn = lambda sel: orc.mxfp8_dequant(ix.tokens[sel].cpu().numpy(), ix.scales[sel].cpu().numpy())  # noqa: E731
         tol = 2e-3
-    else:                                # bf16: the stored bf16 values; fp32: the fp32 values themselves
+    else:                                # fp32: the fp32 values themselves; bf16: the stored bf16 values
         Qd = Q.float().cpu().numpy()
         docs_fn = lambda sel: tokens[sel].float().cpu().numpy()   # noqa: E731
         tol = 1e-4 if faithful else 1e-3
     bad = spot_check(fs, fi_h, Qd, docs_fn, begin, end, check_rows, tol, world, dev)
 
     # ---- N > 1 over RCCL: the same K steps with the native (in-ABI) exchange
-    native = nsearch = None
-    if nccl and not faithful:
-        # every rank builds the native exchange (cbv2_comm_init on torch's RCCL
-        # comm); the leg runs only if all of them could, so a failure there is
-        # reported in the line instead of stranding the other ranks in a collective
-        init_err = None
-        try:
-            nsearch = searcher if args.native_exchange else ShardedSearcher(ix, native=True, lexical_k=args.k)
-        except Exception as e:   # noqa: BLE001  reported, not fatal
-            init_err = f"{type(e).__name__}: {e}"
-        ok = torch.tensor([0 if init_err else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            native = {"error": init_err or "the native exchange failed to initialise on another rank"}
-            nsearch = None
-    if nsearch is not None:
-        try:   # an error inside the native leg is reported in the line, not fatal to it
+    native = None
+    if nccl:
+        def native_prepare():
+            return searcher if args.native_exchange else ShardedSearcher(ix, native=True, lexical_k=args.k)
+
+        def native_run(nsearch):
             nouts, nel = timed_steps(stepper(nsearch, Q), args.steps, args.warmup, world)
             nfi = nouts[-1][1].cpu().numpy()
             none = one_trip(nsearch)
             _, np50, np99 = latency(nsearch, Q1, none)
-            native = {"value": round(B * args.steps / nel, 2), "ms_per_step": round(nel / args.steps * 1e3, 3),
-                      "p50_ms_b1": round(np50, 3) if np50 is not None else None,
-                      "p99_ms_b1": round(np99, 3) if np99 is not None else None,
-                      "top10_equals_planted": float(np.mean([set(nfi[b]) == set(planted[b]) for b in range(B)])),
-                      "equals_torch_exchange": bool(np.array_equal(nfi, fi_h)),
-                      "one_trip_equals_stages": same_as_step(nsearch, none, Q1),
-                      "main_line": "native" if args.native_exchange else "torch.distributed"}
+            res = {"value": round(B * args.steps / nel, 2), "ms_per_step": round(nel / args.steps * 1e3, 3),
+                   "p50_ms_b1": round(np50, 3) if np50 is not None else None,
+                   "p99_ms_b1": round(np99, 3) if np99 is not None else None,
+                   "top10_equals_planted": planted_frac(nfi),
+                   "equals_torch_exchange": bool(np.array_equal(nfi, fi_h)),
+                   "one_trip_equals_stages": same_as_step(nsearch, none, Q1),
+                   "main_line": "native" if args.native_exchange else "torch.distributed"}
             # every rank's native results equal the torch exchange's and the
             # one-trip's equal the stages': the line's p50 may then come from it
-            okf = torch.tensor([1 if (native["equals_torch_exchange"] and native["one_trip_equals_stages"]
-                                      and native["top10_equals_planted"] == 1.0) else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(okf, op=dist.ReduceOp.MIN)
-            native["validated_on_every_rank"] = bool(int(okf.item()))
-        except Exception as e:   # noqa: BLE001
-            if args.native_exchange:
-                raise
-            native = {"error": f"{type(e).__name__}: {e}"}
-            torch.cuda.synchronize()
+            res["validated_on_every_rank"] = agree(res["equals_torch_exchange"] and res["one_trip_equals_stages"]
+                                                   and res["top10_equals_planted"] == 1.0, world, dev, backend)
+            return res
+
+        native = run_leg("native_exchange", native_prepare, native_run, world, rank, dev, backend)
+        if "error" in native and args.native_exchange:
+            raise RuntimeError(f"native exchange (the main line's): {native['error']}")
 
     # ---- CPU baseline: N = 1 only (the contract times it once, on the host of
     # the one-GPU run; an N > 1 line carries null and the ranks do not idle)
@@ -524,47 +589,72 @@ def main():
     if world > 1:
         dist.barrier()
 
-    # ---- the contract-precision leg: the same K steps on the fp32-faithful index
-    fleg = None
-    if args.dtype == "bf16" and not args.no_faithful:
-        nsearch = none = one = None       # the one-trip paths hold their searchers (and so the bf16 index)
-        del searcher, ix, tokens
+    # ---- the side leg, same K steps + p50 on the same corpus:
+    #   fp32 main -> "bf16": a plain bf16 index over the faithful index's hi
+    #                tokens (bf16(x), exactly what a bf16 index of the corpus
+    #                holds; no copy), scores within 1e-3 of the bf16 values;
+    #   bf16 main -> "faithful": the fp32-faithful index of the same corpus.
+    side = None
+    if not args.no_side_leg and args.dtype in ("fp32", "bf16"):
+        side_name = "bf16" if faithful else "faithful"
+
+        def side_prepare():
+            if faithful:
+                six = ColbertIndex(ix.tokens, ix.doclens, id_base=begin)
+                ssrch = ShardedSearcher(six, native=nccl and native is not None and "error" not in native,
+                                        lexical_k=args.k)
+                return six, ssrch, Q.to(torch.bfloat16), None
+            f32, dl32 = synth.make_shard(begin, end, Qf, planted, dev, seed=0, dtype=torch.float32)
+            six = ColbertIndex.faithful_f32(f32, dl32, id_base=begin)
+            return six, ShardedSearcher(six, lexical_k=args.k), Qf.to(dev), f32
+
+        def side_run(st):
+            six, ssrch, Qs, f32 = st
+            six.time_scans(True)
+            souts, sel = timed_steps(stepper(ssrch, Qs), args.steps, args.warmup, world)
+            sscan = six.scan_times()[-args.steps:]
+            sband = six.band_times()[-args.steps:] if six.faithful else []
+            sfs, sfi = souts[-1]
+            sfi_h = sfi.cpu().numpy()
+            sone = one_trip(ssrch)
+            _, sp50, sp99 = latency(ssrch, Qs[:1].contiguous(), sone)
+            if six.faithful:
+                sbad = spot_check(sfs, sfi_h, Qs.cpu().numpy(), lambda sel: f32[sel].cpu().numpy(), begin, end,
+                                  check_rows, 1e-4, world, dev)
+            else:
+                sbad = spot_check(sfs, sfi_h, Qs.float().cpu().numpy(), lambda sel: six.tokens[sel].float().cpu().numpy(),
+                                  begin, end, check_rows, 1e-3, world, dev)
+            res = {"value": round(B * args.steps / sel, 2), "ms_per_step": round(sel / args.steps * 1e3, 3),
+                   "scan_avg_ms": round(sum(sscan) / len(sscan), 3) if sscan else None,
+                   "p50_ms_b1": round(sp50, 3) if sp50 is not None else None,
+                   "p99_ms_b1": round(sp99, 3) if sp99 is not None else None,
+                   "latency_path": "one host round trip" if sone is not None else "stages one by one",
+                   "tolerance": 1e-4 if six.faithful else 1e-3, "oracle_mismatch_queries": sbad,
+                   "top10_equals_planted": planted_frac(sfi_h)}
+            if six.faithful:
+                bs = six.last_band.float()
+                res["band_ms"] = round(sum(sband) / len(sband), 3) if sband else None
+                res["band"] = {"mean": round(float(bs.mean()), 1), "max": int(bs.max()),
+                               "overflow_rows": int((bs < 0).sum())}
+                res["note"] = ("fp32 index (the reference stores fp32, LRC:735-746); scores vs float64 oracle "
+                               "of the fp32 values")
+            else:
+                res["note"] = ("bf16 index over the same corpus (hi = bf16(x)); scores vs float64 oracle of "
+                               "the bf16 values; ~5e-3 from the fp32 scores (DESIGN §3.7)")
+            return res
+
+        side = run_leg(side_name, side_prepare, side_run, world, rank, dev, backend)
+        torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        f32, dl32 = synth.make_shard(begin, end, Qf, planted, dev, seed=0, dtype=torch.float32)
-        fix = ColbertIndex.faithful_f32(f32, dl32, id_base=begin)
-        fsearch = ShardedSearcher(fix, lexical_k=args.k)
-        Qf32 = Qf.to(dev)
-        fix.time_scans(True)
-        fouts, fel = timed_steps(stepper(fsearch, Qf32), args.steps, args.warmup, world)
-        fscan = fix.scan_times()[-args.steps:]
-        ffs, ffi = fouts[-1]
-        ffi_h = ffi.cpu().numpy()
-        bs = fix.last_band.float()
-        fone = one_trip(fsearch) if world == 1 else None     # a faithful shard: torch exchange at N > 1
-        _, fp50, fp99 = latency(fsearch, Qf32[:1].contiguous(), fone)
-        fbad = spot_check(ffs, ffi_h, Qf32.cpu().numpy(), lambda sel: f32[sel].cpu().numpy(), begin, end,
-                          check_rows, 1e-4, world, dev)
-        fleg = {"value": round(B * args.steps / fel, 2), "ms_per_step": round(fel / args.steps * 1e3, 3),
-                "scan_avg_ms": round(sum(fscan) / len(fscan), 3) if fscan else None,
-                "p50_ms_b1": round(fp50, 3) if fp50 is not None else None,
-                "p99_ms_b1": round(fp99, 3) if fp99 is not None else None,
-                "band": {"mean": round(float(bs.mean()), 1), "max": int(bs.max()),
-                         "overflow_rows": int((bs < 0).sum())},
-                "tolerance": 1e-4, "oracle_mismatch_queries": fbad,
-                "top10_equals_planted": float(np.mean([set(ffi_h[b]) == set(planted[b]) for b in range(B)])),
-                "note": "fp32 index (the reference stores fp32, LRC:735-746); scores vs float64 oracle of the fp32 values"}
 
     # ---- BASELINE configs 4 and 5 on the node (8 ranks): the 10M-doc corpus
     # sharded over the ranks, stage 2 (scan + top-100 + ONE all-gather + merge)
     c45 = None
-    if args.c45 == "on" or (args.c45 == "auto" and world == 8 and args.dtype == "bf16"):
-        one = searcher = ix = tokens = fix = fsearch = f32 = fone = nsearch = None   # noqa: F841  free HBM
+    if args.c45 == "on" or (args.c45 == "auto" and world == 8 and args.dtype in ("fp32", "bf16")):
+        one = searcher = ix = tokens = None   # noqa: F841  free HBM for the 10M-doc shards
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        try:   # reported in the line, not fatal to it (every rank takes the same branch: all or none raise)
-            c45 = c45_legs(args, B, world, rank, dev, backend)
-        except torch.cuda.OutOfMemoryError as e:
-            c45 = {"error": f"OutOfMemoryError: {str(e)[:200]}"}
+        c45 = c45_legs(args, B, world, rank, dev, backend)
 
     # N > 1: the single-query latency of the product is the one-round-trip path
     # over the native exchange (no Python between the stages or around the
@@ -577,22 +667,23 @@ def main():
         latency_path = ("one host round trip over the native exchange (cbv2_retrieve_begin/_finish, "
                         "RCCL collectives inside the C ABI)")
 
-    fp8 = args.dtype == "fp8"
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     if rank == 0:
+        workload = ("config 5 (MXFP8 e4m3 tokens, block-scaled fp8 MFMA)" if fp8 else
+                    "config 3, fp32-faithful index (the reference's fp32 arithmetic within 1e-4: bf16 scan + "
+                    "certified hi/lo band rescoring)" if faithful else "config 3, bf16 index")
         line = {
             "metric": "queries/sec + p50 retrieval latency, 1M-chunk corpus, top-10 rerank",
             "value": round(qps, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "fp32 (faithful: bf16 hi/lo split, fp32 accumulate)" if faithful else args.dtype,
             "data": "synthetic (unit-norm N(0,I) tokens, Zipf term-id corpus for BM25, 10 planted positives/query)",
-            "config": {"workload": ("config 5 (MXFP8 e4m3 tokens, block-scaled fp8 MFMA)" if fp8 else
-                                    "config 3, fp32-faithful index (bf16 scan + certified hi/lo band rescoring)"
-                                    if faithful else "config 3") +
-                                   f": {n_total} chunks x 128 tokens x 128-d, host BM25 top-100 + "
-                                   "ColBERT MaxSim top-100 + RRF + rerank top-10",
+            "config": {"workload": workload + f": {n_total} chunks x 128 tokens x 128-d, host BM25 top-100 + "
+                                              "ColBERT MaxSim top-100 + RRF + rerank top-10",
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
+                       "index_dtype": args.dtype,
                        "parallelism": f"corpus sharded x{world}" + (
                            ((" (RCCL all-gather + all-reduce, " + ("native in-ABI" if args.native_exchange
                                                                    else "torch.distributed") + " exchange)")
@@ -614,6 +705,10 @@ def main():
                          "avg_ms_by_rank": [round(r[0], 3) for r in per_rank],
                          "avg_ms_min_max": [round(min(r[0] for r in per_rank), 3),
                                             round(max(r[0] for r in per_rank), 3)],
+                         "band_ms": round(band_avg, 3) if band_avg is not None else None,
+                         "band_ms_note": ("fp32-faithful band work per step (HIP events in the timed region: end "
+                                          "of the bf16 top-k -> end of the band select), rank 0; not part of avg_ms"
+                                          if faithful else None),
                          "clock_ghz_under_load": round(clock, 3) if clock else None,
                          "mfma_busy_at_that_clock": round(mfma_busy, 4) if mfma_busy else None},
             "cpu_baseline": cpu,
@@ -622,8 +717,8 @@ def main():
         }
         if band is not None:
             line["faithful_band"] = band
-        if fleg is not None:
-            line["faithful"] = fleg
+        if side is not None:
+            line["bf16" if faithful else "faithful"] = side
         if native is not None:
             line["native_exchange"] = native
         if collectives is not None:

@@ -34,6 +34,7 @@ _SIGS = {
     "cbv2_index_destroy": (ctypes.c_int, [_p]),
     "cbv2_index_time_scans": (ctypes.c_int, [_p, _i32]),
     "cbv2_index_scan_times": (ctypes.c_int, [_p, _p, _i32, ctypes.POINTER(ctypes.c_int32)]),
+    "cbv2_index_band_times": (ctypes.c_int, [_p, _p, _i32, ctypes.POINTER(ctypes.c_int32)]),
     "cbv2_index_create_mxfp8": (ctypes.c_int, [ctypes.c_int, _p, _p, _i64, _i32, _i32, _p, _i64,
                                                ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_quantize_mxfp8": (ctypes.c_int, [_p, _i32, _i64, _p, _p, _p]),

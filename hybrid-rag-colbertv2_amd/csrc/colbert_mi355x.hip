@@ -3460,6 +3460,40 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
     if (s_base + t < cap) crow[s_base + t] = s_ids[t];
 }
 
+// k-th largest value of the union of G lists of k scores, list g of row b at
+// fk[g * g_stride + b * k .. + k): the cross-shard lower bound of the global
+// k-th faithful score (every shard's exact faithful scores of its bf16 top-k;
+// k docs of the corpus score at least the union's k-th largest).  Radix select
+// over the order-preserving score bits (11/11/10-bit digits), one workgroup
+// per row; -inf padding (an empty shard) counts as a value like any other.
+__global__ __launch_bounds__(kTkThreads) void union_kth_kernel(const float* __restrict__ fk, int G, int k,
+                                                               size_t g_stride, float* __restrict__ lb) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t misc[8];
+  const int b = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
+  const int m = G * k;
+  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)k;
+  for (int p = 0; p < 3; ++p) {
+    const int shift = p == 0 ? 21 : (p == 1 ? 10 : 0);
+    const uint32_t bits = p == 2 ? 1023u : 2047u;
+    for (int i = tid; i < 2048; i += nth) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < m; i += nth) {
+      const int g = i / k, j = i - g * k;
+      const uint32_t u = f2u(fk[(size_t)g * g_stride + (size_t)b * k + j]);
+      hist_add(hist, (u >> shift) & bits, (u & mask) == prefix);
+    }
+    __syncthreads();
+    if ((tid >> 6) == 0) find_bin(hist, (int)bits + 1, kleft, &misc[4], &misc[5], &misc[6]);
+    __syncthreads();
+    kleft -= misc[5];
+    prefix |= misc[4] << shift;
+    mask |= bits << shift;
+    __syncthreads();
+  }
+  if (tid == 0) lb[b] = u2f(prefix);
+}
+
 // Band select: exact top-k of the rescored band (score desc, id asc);
 // status[b] = band size when certified, -1 when the band overflowed cap.
 constexpr int kBandCapMax = 16384;
@@ -3721,6 +3755,13 @@ struct cbv2_index {
   bool time_scans = false;
   size_t scan_ev_used = 0;
   std::vector<hipEvent_t> scan_ev;  // [2 * i] start, [2 * i + 1] stop
+  // Band timing (same switch): a faithful search's work after the bf16 top-k
+  // of its scan (band bound, collect, rescoring, select, fallback) is
+  // bracketed by band_ev[2 * i] / [2 * i + 1]; band_open = a start recorded
+  // whose stop is still to come (cbv2_search_f32_begin -> _finish).
+  size_t band_ev_used = 0;
+  bool band_open = false;
+  std::vector<hipEvent_t> band_ev;
 };
 
 namespace {
@@ -4447,6 +4488,30 @@ int scan_maxsim_timed(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, floa
   return rc;
 }
 
+// Band timing marks (cbv2_index_band_times): start after the bf16 top-k of a
+// faithful search, stop after its band select / fallback.  A stop without a
+// recorded start (timing switched on in between) records nothing.
+int band_mark(cbv2_index* ix, bool stop, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->time_scans) return CBV2_OK;
+  const size_t i = ix->band_ev_used;
+  if (!stop) {
+    while (ix->band_ev.size() < 2 * i + 2) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return CBV2_OK;   // untimed, as for the scans
+      ix->band_ev.push_back(e);
+    }
+    CBV2_HIP(hipEventRecord(ix->band_ev[2 * i], st));
+    ix->band_open = true;
+    return CBV2_OK;
+  }
+  if (!ix->band_open) return CBV2_OK;
+  CBV2_HIP(hipEventRecord(ix->band_ev[2 * i + 1], st));
+  ix->band_open = false;
+  ++ix->band_ev_used;
+  return CBV2_OK;
+}
+
 int score_impl(cbv2_index* ix, int32_t scorer, const void* Q, int32_t B, int32_t lq, float* out,
                int64_t ld_out, hipStream_t st, int* ctr_ws = nullptr) {
   if (scorer == CBV2_SCORER_MAXSIM) return scan_maxsim_timed(ix, Q, B, lq, out, ld_out, st, ctr_ws);
@@ -4701,6 +4766,7 @@ int cbv2_index_destroy(cbv2_index* index) {
       for (hipEvent_t e : index->ring_ev)
         if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : index->scan_ev) (void)hipEventDestroy(e);
+      for (hipEvent_t e : index->band_ev) (void)hipEventDestroy(e);
       (void)hipSetDevice(prev);
     }
   }
@@ -4711,7 +4777,7 @@ int cbv2_index_destroy(cbv2_index* index) {
 int cbv2_index_time_scans(cbv2_index* ix, int32_t enable) {
   CBV2_REQUIRE(ix != nullptr, "null index");
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (enable) ix->scan_ev_used = 0;
+  if (enable) ix->scan_ev_used = ix->band_ev_used = 0, ix->band_open = false;
   ix->time_scans = enable != 0;
   return CBV2_OK;
 }
@@ -4730,6 +4796,24 @@ int cbv2_index_scan_times(cbv2_index* ix, float* ms, int32_t max, int32_t* count
       return fail(CBV2_EHIP, "scan event %zu: %s", i, hipGetErrorString(hipGetLastError()));
   }
   ix->scan_ev_used = 0;  // read once: the record is consumed
+  return CBV2_OK;
+}
+
+int cbv2_index_band_times(cbv2_index* ix, float* ms, int32_t max, int32_t* count) {
+  CBV2_REQUIRE(ix != nullptr && count != nullptr, "null index or count");
+  CBV2_REQUIRE(max >= 0 && (max == 0 || ms != nullptr), "bad output buffer");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  CBV2_REQUIRE(!ix->time_scans, "disable timing (cbv2_index_time_scans(ix, 0)) before reading the times");
+  *count = (int32_t)ix->band_ev_used;
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  for (size_t i = 0; i < ix->band_ev_used && i < (size_t)max; ++i) {
+    if (hipEventSynchronize(ix->band_ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(ms + i, ix->band_ev[2 * i], ix->band_ev[2 * i + 1]) != hipSuccess)
+      return fail(CBV2_EHIP, "band event %zu: %s", i, hipGetErrorString(hipGetLastError()));
+  }
+  ix->band_ev_used = 0;
+  ix->band_open = false;
   return CBV2_OK;
 }
 
@@ -5032,6 +5116,7 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
                 : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st,
                             ix->device)))
     return rc;
+  if ((rc = band_mark(ix, false, st))) return rc;
   if (fk_out != nullptr)     // the bf16 top-k's own faithful scores, for the caller's cross-shard bound
     return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, fk_out, k, st);
   if (lb_out != nullptr) {   // the bf16 top-k's own faithful scores: k docs score at least their minimum
@@ -5045,8 +5130,8 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
 // Phase 2: the band (every doc with T >= lb - beta; lb == nullptr: T_k - 2
 // beta, the one-pass band), its faithful rescoring, the exact top-k of the
 // band, and the full faithful scan for rows whose band overflowed cap.
-int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w, const float* lb,
-                      float* out_scores, int32_t* out_ids, int32_t* out_status, hipStream_t st) {
+int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w,
+                           const float* lb, float* out_scores, int32_t* out_ids, int32_t* out_status, hipStream_t st) {
   int rc;
   CBV2_HIP(hipMemsetAsync(w.count, 0, (size_t)B * sizeof(int32_t), st));
   int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
@@ -5095,6 +5180,27 @@ int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t 
   hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.T, ix->n, ix->n, k, ix->id_base,
                      out_scores, out_ids, out_status);
   return launch_check("topk_rows_kernel");
+}
+
+int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w, const float* lb,
+                      float* out_scores, int32_t* out_ids, int32_t* out_status, hipStream_t st) {
+  const int rc = search_f32_phase2_impl(ix, B, lq, k, cap, w, lb, out_scores, out_ids, out_status, st);
+  if (rc) return rc;
+  return band_mark(ix, true, st);
+}
+
+// The faithful rerank after its query split: rescoring of the C candidates
+// (raw scores), then the top-k select (k == 0: the raw scores themselves).
+int rerank_f32_split(cbv2_index* ix, F32Ws& w, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
+                     float* out_scores, int32_t* out_ids, int32_t* out_pos, hipStream_t st) {
+  int rc;
+  float* raw = k == 0 ? out_scores : w.F;
+  if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
+  if (k == 0) return CBV2_OK;
+  if (C > kSmallMax) return topk_multi(raw, B, C, C, k, 0, cand, C, out_scores, out_ids, out_pos, st);
+  hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
+                     out_pos);
+  return launch_check("select_small_kernel");
 }
 
 int check_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
@@ -5177,13 +5283,33 @@ int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
   hipStream_t st = (hipStream_t)stream;
   if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
-  float* raw = k == 0 ? out_scores : w.F;
-  if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
-  if (k == 0) return CBV2_OK;
-  if (C > kSmallMax) return topk_multi(raw, B, C, C, k, 0, cand, C, out_scores, out_ids, out_pos, st);
-  hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
-                     out_pos);
-  return launch_check("select_small_kernel");
+  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st);
+}
+
+// Internal (retrieve.cpp): cbv2_rerank_f32 for the queries a cbv2_search_f32
+// with the same (B, lq) and band capacity `cap` split into `search_ws` just
+// before on the same stream: the rerank reads that split (qhi / qlo) instead
+// of launching the query split again.  Same arithmetic, same results.
+int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t search_wsb, int32_t cap, int32_t B,
+                                 int32_t lq, const int32_t* cand, int32_t C, int32_t k, void* ws, size_t wsb,
+                                 float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+  CBV2_REQUIRE(cand != nullptr && C >= 1 && k >= 0 && out_scores != nullptr && (k == 0 || out_ids != nullptr),
+               "bad candidates / outputs");
+  CBV2_REQUIRE(ix != nullptr && ix->resid != nullptr, "not an fp32-faithful index");
+  CBV2_REQUIRE(B >= 1 && B <= 65535 && lq >= 1 && lq <= kLqMax, "bad B / lq");
+  F32Ws sw, w;
+  const size_t sneed = f32_ws_layout(ix, CBV2_F32_SEARCH, B, lq, cap, nullptr, &sw);
+  CBV2_REQUIRE(search_ws != nullptr && search_wsb >= sneed && aligned16(search_ws), "search workspace too small");
+  f32_ws_layout(ix, CBV2_F32_SEARCH, B, lq, cap, (uint8_t*)search_ws, &sw);
+  const size_t need = f32_ws_layout(ix, CBV2_F32_RERANK, B, lq, C, nullptr, &w);
+  CBV2_REQUIRE(ws != nullptr && wsb >= need && aligned16(ws), "workspace too small or misaligned (%zu < %zu)", wsb,
+               need);
+  f32_ws_layout(ix, CBV2_F32_RERANK, B, lq, C, (uint8_t*)ws, &w);
+  w.qhi = sw.qhi;
+  w.qlo = sw.qlo;
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, (hipStream_t)stream);
 }
 
 size_t cbv2_topk_workspace_bytes(int32_t B, int64_t n) { return B >= 1 && n >= 1 ? topk_ws_bytes(B, n) : 0; }
@@ -5208,6 +5334,17 @@ int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32
 int cbv2_merge_topk(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
                     float* out_scores, int32_t* out_ids, void* stream) {
   return cbv2_merge_topk_strided(in_scores, in_ids, G, B, k, (size_t)B * k, out_scores, out_ids, stream);
+}
+
+// Internal (sharded.cpp): lb[b] = the k-th largest of the G lists of row b
+// (union_kth_kernel), shard g's lists at g * g_stride.
+int cbv2_union_kth(const float* fk, int32_t G, int32_t B, int32_t k, size_t g_stride, float* lb, void* stream) {
+  CBV2_REQUIRE(fk && lb, "null pointer");
+  CBV2_REQUIRE(G >= 1 && G <= 64 && B >= 1 && k >= 1, "bad sizes (G %d, B %d, k %d)", G, B, k);
+  CBV2_REQUIRE((int64_t)G * k <= 0x7fffffffLL && g_stride >= (size_t)B * k, "bad list layout");
+  hipLaunchKernelGGL(union_kth_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, (hipStream_t)stream, fk, G, k, g_stride,
+                     lb);
+  return launch_check("union_kth_kernel");
 }
 
 // Internal (sharded.cpp): the same merge with shard g's lists at g * g_stride.

@@ -22,6 +22,10 @@
 #include "colbert_mi355x.h"
 
 extern "C" int cbv2_set_error(int code, const char* msg);
+extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t search_wsb, int32_t cap,
+                                            int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k, void* ws,
+                                            size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                                            void* stream);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -64,10 +68,13 @@ Layout layout(const cbv2_index* ix, const cbv2_comm* c, Kind kd, int32_t B, int3
                                                                                                : CBV2_RETRIEVE_BAND_CAP));
   else
     L.stage2 = a256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM));
-  if (kd.faithful)
+  if (c)        // cbv2_rerank_sharded: raw [B][C] (+ a faithful shard's rerank workspace after it)
+    L.rerank = a256((size_t)B * C * 4) +
+               (kd.faithful ? a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, C)) : 0);
+  else if (kd.faithful)
     L.rerank = a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, C));
   else
-    L.rerank = a256(c ? (size_t)B * C * 4 : cbv2_rerank_workspace_bytes(B, C));
+    L.rerank = a256(cbv2_rerank_workspace_bytes(B, C));
   const size_t bk = a256((size_t)B * k * 4), bkb = a256((size_t)B * (kb > 0 ? kb : 1) * 4),
                bc = a256((size_t)B * C * 4), bs = a256((size_t)B * 4);
   L.total = L.stage2 + 2 * bk + bkb + bc + bs + L.rerank;
@@ -117,8 +124,6 @@ int check_common(const cbv2_index* ix, Kind* kd, const cbv2_comm* c, const void*
   if (lq < 1 || lq > 32) return err(CBV2_EINVAL, "lq must be in [1, 32] (got %d); longer queries go by blocks", lq);
   const int32_t want = kd->faithful ? CBV2_DTYPE_F32 : kd->dtype;
   if (q_dtype != want) return err(CBV2_EINVAL, "query dtype %d does not match the index (needs %d)", q_dtype, want);
-  if (c && kd->faithful)
-    return err(CBV2_EUNSUPPORTED, "an fp32-faithful shard needs the global-bound exchange (cbv2_search_f32_begin)");
   return CBV2_OK;
 }
 }  // namespace
@@ -191,9 +196,9 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
   RT_HIP(hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st));
   if (c)
     return cbv2_rerank_sharded(ix, c, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
-  if (kd.faithful)
-    return cbv2_rerank_f32(ix, (const float*)Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids,
-                           out_pos, st);
+  if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank too
+    return cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
+                                        B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
   return cbv2_rerank_ws(ix, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
 }
 

@@ -11,6 +11,16 @@
 //   rerank:  raw candidate scores (-inf for ids this shard does not own)
 //            -> ncclAllReduce(MAX) -> HIP top-k select.
 //
+// An fp32-faithful shard bounds its band by the GLOBAL k-th
+// faithful score: the local call runs the bf16 scan + top-k and the exact
+// faithful scores fk [B][k] of that top-k (cbv2_search_f32_begin), ONE
+// ncclAllGather of fk, the k-th largest of the union (union_kth_kernel) as
+// the lower bound lb, then the band rescoring of only the docs that can reach
+// the global top-k (cbv2_search_f32_finish) into the send block; the rerank
+// scores the owned candidates faithfully (cbv2_rerank_f32).  Results equal
+// the unsharded faithful search and rerank bit for bit (the merge completes
+// the exact global top-k; any lower bound of the k-th score keeps it exact).
+//
 // No reference counterpart: the reference is single-process.
 // RCCL is resolved with dlsym from the library that created the communicator
 // (passed by path; NULL = "librccl.so"), so the borrowed ncclComm_t and the
@@ -31,6 +41,8 @@
 extern "C" int cbv2_set_error(int code, const char* msg);
 extern "C" int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in_ids, int32_t G, int32_t B, int32_t k,
                                        size_t g_stride, float* out_scores, int32_t* out_ids, void* stream);
+extern "C" int cbv2_union_kth(const float* fk, int32_t G, int32_t B, int32_t k, size_t g_stride, float* lb,
+                              void* stream);
 
 namespace {
 // The RCCL entry points used here (rccl.h: ncclResult_t is an int enum,
@@ -293,34 +305,75 @@ int cbv2_comm_destroy(cbv2_comm* c) {
   return CBV2_OK;
 }
 
+namespace {
+// The band capacity of a faithful shard's search (as cbv2_retrieve_* use) and
+// its workspaces, sized for lq = 32 (the most a MaxSim call takes; a call
+// with fewer query tokens needs less).
+int32_t band_cap(int32_t k) { return k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP; }
+bool is_faithful(const cbv2_index* ix) {
+  int32_t dt = 0, f = 0;
+  return ix && cbv2_index_kind(ix, &dt, &f) == CBV2_OK && f != 0;
+}
+size_t f32_search_bytes(const cbv2_index* ix, int32_t B, int32_t k) {
+  return align256(cbv2_f32_workspace_bytes(ix, CBV2_F32_SEARCH, B, 32, band_cap(k)));
+}
+// rerank part: raw [B][C] at the head of the workspace (+ a faithful shard's
+// rerank workspace after it, for queries of lq tokens)
+size_t rerank_bytes(const cbv2_index* ix, int32_t B, int32_t C, int32_t lq = 32) {
+  const size_t raw = align256((size_t)B * (C > 0 ? C : 1) * 4);
+  return raw + (is_faithful(ix) && C > 0 ? align256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, C)) : 0);
+}
+
+// [local search part | send block | recv blocks | merged BM25 scores | rerank part]
+// local search part: bf16 / MXFP8: the cbv2_search workspace; fp32-faithful:
+// [f32 search workspace | fk B*k | fk of every rank G*B*k | lb B | status B].
+struct Layout {
+  size_t search_ws, blk, f32_ws;
+  int32_t *send, *recv;
+  float* lex_s_out;
+  float *fk, *fk_all, *lb;
+  int32_t* status;
+};
+Layout layout(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, int32_t kb, void* ws) {
+  Layout L{};
+  uint8_t* base = (uint8_t*)ws;
+  if (is_faithful(ix)) {
+    L.f32_ws = f32_search_bytes(ix, B, k);
+    const size_t bk = align256((size_t)B * k * 4), gbk = align256((size_t)c->nranks * B * k * 4),
+                 b4 = align256((size_t)B * 4);
+    L.search_ws = L.f32_ws + bk + gbk + 2 * b4;
+    if (base) {
+      L.fk = (float*)(base + L.f32_ws);
+      L.fk_all = (float*)(base + L.f32_ws + bk);
+      L.lb = (float*)(base + L.f32_ws + bk + gbk);
+      L.status = (int32_t*)(base + L.f32_ws + bk + gbk + b4);
+    }
+  } else {
+    L.search_ws = align256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM));
+  }
+  L.blk = (size_t)2 * B * (k + kb);
+  if (base) {
+    uint8_t* p = base + L.search_ws;
+    L.send = (int32_t*)p;
+    L.recv = (int32_t*)(p + align256(L.blk * 4));
+    L.lex_s_out = (float*)(p + align256(L.blk * 4) + align256(L.blk * 4 * c->nranks));
+  }
+  return L;
+}
+}  // namespace
+
 size_t cbv2_sharded_workspace_bytes(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, int32_t kb,
                                     int32_t C) {
   if (!ix || !c || B < 1 || k < 1 || kb < 0 || C < 0) return 0;
-  const size_t blk = (size_t)2 * B * (k + kb);  // 4-byte words per rank
-  const size_t gather = align256(blk * 4) + align256(blk * 4 * c->nranks);
+  const Layout L = layout(ix, c, B, k, kb, nullptr);
+  const size_t gather = align256(L.blk * 4) + align256(L.blk * 4 * c->nranks);
   const size_t lex_out = align256((size_t)B * (kb > 0 ? kb : 1) * 4);
-  const size_t raw = align256((size_t)B * (C > 0 ? C : 1) * 4);
   // the local search's part is sized for MaxSim (the sharded exchange's scorer;
   // cbv2_search rejects another scorer's larger need with CBV2_EINVAL)
-  return align256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM)) + gather + lex_out + raw;
+  return L.search_ws + gather + lex_out + rerank_bytes(ix, B, C);
 }
 
 namespace {
-struct Layout {
-  size_t search_ws, blk;
-  int32_t *send, *recv;
-  float* lex_s_out;
-};
-Layout layout(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, int32_t kb, void* ws) {
-  Layout L;
-  L.search_ws = align256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM));
-  L.blk = (size_t)2 * B * (k + kb);
-  uint8_t* p = (uint8_t*)ws + L.search_ws;
-  L.send = (int32_t*)p;
-  L.recv = (int32_t*)(p + align256(L.blk * 4));
-  L.lex_s_out = (float*)(p + align256(L.blk * 4) + align256(L.blk * 4 * c->nranks));
-  return L;
-}
 int check_sizes(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, int32_t kb, void* ws, size_t ws_bytes) {
   if (!ix || !c) return err(CBV2_EINVAL, "null index/comm");
   if (B < 1 || k < 1 || kb < 0) return err(CBV2_EINVAL, "bad sizes (B %d, k %d, kb %d)", B, k, kb);
@@ -335,9 +388,22 @@ int cbv2_search_sharded_local(cbv2_index* ix, cbv2_comm* c, int32_t scorer, cons
                               void* stream) {
   if (int rc = check_sizes(ix, c, B, k, kb, workspace, workspace_bytes)) return rc;
   const Layout L = layout(ix, c, B, k, kb, workspace);
-  // local stage 2 straight into this rank's send block
-  return cbv2_search(ix, scorer, Q, q_dtype, B, lq, k, workspace, L.search_ws, (float*)L.send,
-                     L.send + (size_t)B * k, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  float* send_s = (float*)L.send;
+  int32_t* send_i = L.send + (size_t)B * k;
+  if (!is_faithful(ix))   // local stage 2 straight into this rank's send block
+    return cbv2_search(ix, scorer, Q, q_dtype, B, lq, k, workspace, L.search_ws, send_s, send_i, st);
+  if (scorer != CBV2_SCORER_MAXSIM || q_dtype != CBV2_DTYPE_F32)
+    return err(CBV2_EINVAL, "an fp32-faithful shard takes MaxSim with f32 queries");
+  const int32_t cap = band_cap(k);
+  int rc = cbv2_search_f32_begin(ix, (const float*)Q, B, lq, k, cap, workspace, L.f32_ws, L.fk, send_s, send_i,
+                                 L.status, st);
+  if (rc) return rc;
+  // the global bound: every rank's fk, the k-th largest of their union
+  rc = nccl_check(c, c->all_gather(L.fk, L.fk_all, (size_t)B * k, kNcclFloat32, c->nccl, st), "ncclAllGather");
+  if (rc) return rc;
+  if ((rc = cbv2_union_kth(L.fk_all, c->nranks, B, k, (size_t)B * k, L.lb, st))) return rc;
+  return cbv2_search_f32_finish(ix, B, lq, k, cap, workspace, L.f32_ws, L.lb, send_s, send_i, L.status, st);
 }
 
 int cbv2_search_sharded_exchange(cbv2_index* ix, cbv2_comm* c, int32_t B, int32_t k, const int32_t* lex_ids,
@@ -378,11 +444,19 @@ int cbv2_rerank_sharded(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t B, 
                         int32_t C, int32_t k, void* workspace, size_t workspace_bytes, float* out_scores,
                         int32_t* out_ids, int32_t* out_pos, void* stream) {
   if (!ix || !c) return err(CBV2_EINVAL, "null index/comm");
-  if (B < 1 || C < 1 || k < 1) return err(CBV2_EINVAL, "bad sizes (B, C, k)");
-  if (!workspace || workspace_bytes < (size_t)B * C * 4) return err(CBV2_EINVAL, "workspace too small");
+  if (B < 1 || C < 1 || k < 1 || lq < 1) return err(CBV2_EINVAL, "bad sizes (B, C, k, lq)");
+  if (!workspace || workspace_bytes < rerank_bytes(ix, B, C, lq))
+    return err(CBV2_EINVAL, "workspace too small (%zu bytes needed)", rerank_bytes(ix, B, C, lq));
   hipStream_t st = (hipStream_t)stream;
   float* raw = (float*)workspace;
-  int rc = cbv2_rerank(ix, Q, B, lq, cand, C, 0, raw, nullptr, nullptr, st);
+  int rc;
+  if (is_faithful(ix)) {   // faithful scores of the owned candidates (f32 queries)
+    const size_t off = align256((size_t)B * C * 4);
+    rc = cbv2_rerank_f32(ix, (const float*)Q, B, lq, cand, C, 0, (uint8_t*)workspace + off, workspace_bytes - off,
+                         raw, nullptr, nullptr, st);
+  } else {
+    rc = cbv2_rerank(ix, Q, B, lq, cand, C, 0, raw, nullptr, nullptr, st);
+  }
   if (rc) return rc;
   rc = nccl_check(c, c->all_reduce(raw, raw, (size_t)B * C, kNcclFloat32, kNcclMax, c->nccl, st), "ncclAllReduce");
   if (rc) return rc;

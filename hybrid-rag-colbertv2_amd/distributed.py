@@ -159,7 +159,9 @@ class NativeExchange:
     cbv2_search_sharded_local/_exchange, cbv2_rerank_sharded) over the RCCL
     communicator torch.distributed's "nccl" backend already holds: scan,
     all-gather and merges are all enqueued by C++ on the current stream, with
-    no Python between them."""
+    no Python between them.  An fp32-faithful shard takes the same calls: the
+    global k-th bound (``ShardedSearcher._global_kth`` in Python) is one more
+    all-gather inside ``cbv2_search_sharded_local``."""
 
     def __init__(self, index, group: Optional[dist.ProcessGroup] = None, lexical_k: int = 100, comm=None):
         """``comm``: an existing ``cbv2_comm*`` handle to adopt (e.g. one rank of
@@ -168,9 +170,6 @@ class NativeExchange:
         import os
 
         from . import _lib
-        if getattr(index, "faithful", False):
-            raise ValueError("the native exchange scans bf16/MXFP8 shards; an fp32-faithful shard uses the "
-                             "torch.distributed exchange (ShardedSearcher(native=False))")
         self.index, self.dev, self.lexical_k = index, index.device, int(lexical_k)
         self._lib = _lib
         if comm is not None:

@@ -401,6 +401,11 @@ class OneTripRetriever:
             self._ws = torch.empty((need + 256,), dtype=torch.uint8, device=self.device)
         hneed = int(L.cbv2_retrieve_host_bytes(B, self.k, kb, self.C))
         if self._host is None or self._host.numel() < hneed:
+            if self._host is not None:
+                # the previous finish's candidate upload reads the old pinned block
+                # through a raw pointer (no allocator event): wait for it before
+                # the block can go back to torch's pinned-memory cache
+                torch.cuda.current_stream(self.device).synchronize()
             self._host = torch.empty((hneed,), dtype=torch.uint8, pin_memory=True)
         off = (-self._ws.data_ptr()) % 256                 # 256-B aligned start
         return self._ws.data_ptr() + off, self._ws.numel() - off

@@ -341,6 +341,17 @@ class ColbertIndex:
         _lib.check(_lib.lib().cbv2_index_scan_times(self._h, ms, int(max_launches), ctypes.byref(cnt)))
         return [float(ms[i]) for i in range(min(cnt.value, max_launches))]
 
+    def band_times(self, max_searches: int = 4096) -> List[float]:
+        """Durations (ms) of the fp32-faithful searches' band work recorded since
+        ``time_scans(True)`` (from the end of the bf16 top-k to the end of the
+        band select; cbv2_index_band_times); disables timing first, then clears
+        the record.  Read after ``scan_times`` or before it: both disable."""
+        self.time_scans(False)
+        ms = (ctypes.c_float * max_searches)()
+        cnt = ctypes.c_int32(0)
+        _lib.check(_lib.lib().cbv2_index_band_times(self._h, ms, int(max_searches), ctypes.byref(cnt)))
+        return [float(ms[i]) for i in range(min(cnt.value, max_searches))]
+
     def __del__(self):
         try:
             self.close()

@@ -92,9 +92,15 @@ int cbv2_index_destroy(cbv2_index* index);
  * without a side launch.  enable=1 clears the previous record.
  * cbv2_index_scan_times (timing disabled first) waits for the recorded launches
  * and writes min(count, max) durations in ms; *count = launches recorded;
- * the record is then cleared.  */
+ * the record is then cleared.
+ * cbv2_index_band_times: the same for the fp32-faithful searches' band work
+ * (cbv2_search_f32 / _begin + _finish), each bracketed from the end of the
+ * bf16 top-k of its scan to the end of its band select and full-scan fallback:
+ * the time the faithful arithmetic adds to a bf16 search (the query split
+ * before the scan, one small kernel, is outside the bracket).  */
 int cbv2_index_time_scans(cbv2_index* index, int32_t enable);
 int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
+int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
 
 /* Handle options (A/B and tests; defaults = production):
  *  CBV2_OPT_FUSED_TOPK   1: cbv2_search fuses the top-k into eligible scans
@@ -428,7 +434,17 @@ int cbv2_index_writer_close(cbv2_index_writer* w);
  *   head of the send block; its kb just sizes its workspace check).
  * cbv2_rerank_sharded — every rank scores the candidates it owns (-inf
  *   otherwise) -> ncclAllReduce(MAX) -> top-k select; cand [B][C] global ids
- *   (device).  Workspace >= B*C*4 bytes (or the size above with C).
+ *   (device).  Workspace: the size above with C (a bf16 / MXFP8 shard needs
+ *   only B*C*4 bytes).
+ * fp32-faithful shards (cbv2_index_attach_residual; Q f32, q_dtype
+ *   CBV2_DTYPE_F32): the local call runs the faithful search against the
+ *   GLOBAL k-th bound -- bf16 scan + top-k + the exact faithful scores of that
+ *   top-k (cbv2_search_f32_begin), ONE ncclAllGather of those [B][k] scores,
+ *   their union's k-th largest as lb, the band rescoring (cbv2_search_f32_finish,
+ *   band capacity CBV2_RETRIEVE_BAND_CAP) -- so the local call is itself a
+ *   collective; the rerank scores the owned candidates faithfully
+ *   (cbv2_rerank_f32).  Results equal the unsharded faithful search / rerank
+ *   bit for bit.
  * Collectives are enqueued on `stream`; every rank must call in the same
  * order (as with any RCCL program).                                        */
 typedef struct cbv2_comm cbv2_comm;
@@ -472,8 +488,8 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  * (:996-1014) for the caller; results equal those of the separate calls
  * (cbv2_search[_f32] / cbv2_search_sharded_*, cbv2_rrf_fuse, cbv2_rerank_ws /
  * _f32 / cbv2_rerank_sharded) bit for bit.
- *  comm: NULL for one shard; else a cbv2_comm (bf16 / MXFP8 shards: the
- *        exchange above; an fp32-faithful shard is CBV2_EUNSUPPORTED there).
+ *  comm: NULL for one shard; else a cbv2_comm (the exchange above, for
+ *        bf16, MXFP8 and fp32-faithful shards alike).
  *  Q:    the index's query type: bf16 [B][lq][128] (bf16 index), the
  *        cbv2_quantize_mxfp8 buffer (MXFP8), f32 (fp32-faithful); lq <= 32.
  *  cbv2_retrieve_begin enqueues stage 2 (this shard's scan + top-k; the band

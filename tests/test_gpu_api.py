@@ -31,10 +31,10 @@ class RecordedBM25:
         return np.array([bm["ids"][:k]]), np.array([bm["scores"][:k]])
 
 
-def _system(tmp_path, scorer, index_dtype="bf16"):
+def _system(tmp_path, scorer, index_dtype="bf16", encoder_cls=None):
     cfg = RAGConfig(scorer=scorer, colbert_index_path=str(tmp_path / "colbert"),
                     bm25_index_path=str(tmp_path / "bm25"), index_dtype=index_dtype)
-    ind = DualIndexer(cfg, encoder=FakeEncoder(**TOY["encoder"]))
+    ind = DualIndexer(cfg, encoder=(encoder_cls or FakeEncoder)(**TOY["encoder"]))
     ind.colbert_retriever.index(TOY["corpus"])
     ind.bm25_retriever = RecordedBM25()
     store = ChunkStore([{"chunk_id": c["id"], "text": t, "document_id": c["document_id"],
@@ -44,8 +44,13 @@ def _system(tmp_path, scorer, index_dtype="bf16"):
     return cfg, ind, HybridRetriever(cfg, ind, store, verbose=False)
 
 
-def test_c1_literal_search_rerank_retrieve_match_reference(dev, tmp_path):
-    cfg, ind, hyb = _system(tmp_path, "ref_meanpool_cosine")
+@pytest.mark.parametrize("strict", [False, True])
+def test_c1_literal_search_rerank_retrieve_match_reference(dev, tmp_path, strict):
+    """strict: the encoder has sentence-transformers 2.x's ``encode`` signature
+    (no ``is_query``, no ``**kwargs``; LRC:758-761 / 782-783 pass only
+    ``convert_to_tensor=True``) and the golden reference outputs are still
+    reproduced through index, search, rerank and HybridRetriever.retrieve."""
+    cfg, ind, hyb = _system(tmp_path, "ref_meanpool_cosine", encoder_cls=StrictEncoder if strict else None)
     r = ind.colbert_retriever
     for i, q in enumerate(TOY["queries"]):
         got = r.search(q, k=10)

@@ -386,6 +386,31 @@ def test_scan_timing_events(dev):
     assert ix.scan_times() == []
 
 
+@pytest.mark.gpu
+def test_band_timing_events(dev):
+    """cbv2_index_band_times: one positive duration per fp32-faithful search
+    (end of the bf16 top-k -> end of the band select) while timing is on,
+    alongside the scan's own; plain searches record none; results unchanged."""
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    g = torch.Generator().manual_seed(5)
+    tok = torch.randn(3000, 128, 128, generator=g)
+    tok = (tok / tok.norm(dim=-1, keepdim=True)).to(dev)
+    dl = torch.full((3000,), 128, dtype=torch.int32, device=dev)
+    Q = torch.randn(3, 32, 128, generator=g).to(dev)
+    ix = ColbertIndex.faithful_f32(tok, dl)
+    ref = [x.clone() for x in ix.search(Q, 10)]
+    ix.time_scans(True)
+    got = ix.search(Q, 10)
+    ix.search(Q[:1], 10)
+    scans, bands = ix.scan_times(), ix.band_times()
+    assert len(scans) == 2 and len(bands) == 2 and all(x > 0 for x in scans + bands)
+    assert all(torch.equal(a, b) for a, b in zip(got, ref))
+    plain = ColbertIndex(ix.tokens, ix.doclens)
+    plain.time_scans(True)
+    plain.search(Q.bfloat16(), 10)
+    assert len(plain.scan_times()) == 1 and plain.band_times() == []
+
+
 def test_dynamic_tail_b16_bit_identical(dev):
     """B = 9-16 (4-wave shape, 60 % dynamic share): every score equals the B=1
     direct scan's and a small index's over the same docs, bit for bit (100k

@@ -127,3 +127,69 @@ def test_loopback_shard_smaller_than_k_pads(dev):
         assert torch.equal(s, es.cpu()) and torch.equal(i, ei.cpu())
         assert (i[:, N:] == -1).all() and torch.isinf(s[:, N:]).all()   # slots past n: -inf / -1
     del nxs
+
+
+@pytest.mark.parametrize("G,B", [(2, 1), (4, 5), (8, 12)])
+def test_native_exchange_loopback_faithful_equals_unsharded(dev, G, B):
+    """fp32-faithful shards through the in-ABI exchange: the local call runs the
+    faithful search against the GLOBAL k-th bound (one more all-gather of the
+    bf16 top-k's faithful scores inside cbv2_search_sharded_local), the rerank
+    scores the owned candidates faithfully.  Every rank equals the unsharded
+    faithful search, rerank and BM25 lists bit for bit -- with a shard smaller
+    than k, ragged docs, and exact ties: copies of planted docs placed N/2 ids
+    away (another shard at G >= 4) score exactly like their originals, so the
+    (score desc, id asc) rule decides between them.  B = 1 / 5 take the pair-by-pair band, B = 12 the
+    doc-major one."""
+    N, k, kb, C, kf = 6000, 100, 100, 50, 10
+    Qf = synth.make_queries(B, seed=71 + G)
+    planted = synth.planted_ids(B, N, 10, seed=70 + G)
+    tokens, doclens = synth.make_shard(0, N, Qf, planted, dev, dtype=torch.float32)
+    doclens[::13] = torch.randint(0, 129, (len(doclens[::13]),), device=dev, dtype=torch.int32)
+    doclens[torch.from_numpy(planted.reshape(-1)).to(dev)] = 128
+    ranges = _ranges(N, G, small=40)
+    # ties: the first planted doc of every query copied to an id in another shard
+    src = torch.from_numpy(planted[:, 0].copy()).to(dev)
+    dst = (src + N // 2) % N
+    keep = ~torch.isin(dst, torch.from_numpy(planted.reshape(-1)).to(dev))
+    tokens[dst[keep]] = tokens[src[keep]]
+    doclens[dst[keep]] = doclens[src[keep]]
+    full = ColbertIndex.faithful_f32(tokens, doclens)
+    shards = [ColbertIndex.faithful_f32(tokens[a:b].contiguous(), doclens[a:b].contiguous(), id_base=a)
+              for a, b in ranges]
+    Q = Qf.to(dev)
+
+    terms, off, V = synth.bm25_shard(0, N, planted)
+    df = NativeBM25.doc_freq(terms, off, V)
+    stats = (N, int(off[-1]), df)
+    lex_full = NativeBM25(terms, off, V)
+    lex = [NativeBM25(terms[off[a]:off[b]], off[a:b + 1] - off[a], V, id_base=a, stats=stats) for a, b in ranges]
+    qt, qo = synth.bm25_queries(B)
+
+    comms = loopback_comms(G)
+    nxs = [NativeExchange(shards[r], comm=comms[r]) for r in range(G)]
+    es, ei = full.search(Q, k)
+    cand = ei[:, :C].clone()
+    cand[:, -1] = -1
+    cand = cand.contiguous()
+
+    def rank(r):
+        s, i, li = nxs[r].search(Q, k, lexical=lambda: lex[r].search(qt, qo, kb))
+        rr = nxs[r].rerank(Q, cand, kf)
+        return [x.cpu() for x in (s, i, li, *rr)]
+
+    outs = _run_ranks(G, rank)
+    torch.cuda.synchronize()
+    bi, _ = lex_full.search(qt, qo, kb)
+    ers, eri, erp = full.rerank(Q, cand, kf)
+    for r, (s, i, li, rs, ri, rp) in enumerate(outs):
+        assert torch.equal(i, ei.cpu()), f"rank {r}: ids differ from the unsharded faithful search"
+        assert torch.equal(s, es.cpu()), f"rank {r}: scores differ from the unsharded faithful search"
+        assert np.array_equal(li.numpy(), bi)
+        assert torch.equal(ri, eri.cpu()) and torch.equal(rp, erp.cpu()) and torch.equal(rs, ers.cpu())
+    tied = 0
+    for b in range(B):
+        row = outs[0][0][b]
+        tied += int((row[1:] == row[:-1]).sum())
+        assert set(planted[b].tolist()) <= set(outs[0][1][b, :20].tolist())
+    assert tied >= 1, "the copies must produce exact ties in the merged lists"
+    del nxs

@@ -4,8 +4,9 @@ _finish, hybrid.OneTripRetriever) against the same stages called one by one
 
 Done = scores, ids and positions equal bit for bit, for bf16, MXFP8 and
 fp32-faithful shards, B = 1 / 5 / 40, with a BM25 callable, a host id array
-and no stage 1; and at G = 2 / 4 through the test-only loopback communicator
-(every rank equals the unsharded composed path)."""
+and no stage 1; and at G = 2 / 4 / 8 through the test-only loopback
+communicator, bf16, MXFP8 and fp32-faithful shards (every rank equals the
+unsharded composed path)."""
 import threading
 
 import numpy as np
@@ -101,17 +102,25 @@ def _run_ranks(G, fn):
     return out
 
 
-@pytest.mark.parametrize("G,B,fp8", [(2, 1, False), (4, 9, False), (4, 6, True)])
-def test_one_trip_sharded_loopback_equals_unsharded(dev, G, B, fp8):
+@pytest.mark.parametrize("G,B,kind,kb_ret", [(2, 1, "bf16", KB), (4, 9, "bf16", KB), (4, 6, "fp8", KB),
+                                             (2, 3, "bf16", 60), (2, 1, "fp32", KB), (4, 5, "fp32", 60),
+                                             (8, 12, "fp32", KB)])
+def test_one_trip_sharded_loopback_equals_unsharded(dev, G, B, kind, kb_ret):
+    """kb_ret < KB: the stage-1 callable returns fewer columns than begin's
+    kb (an upper bound, include/colbert_mi355x.h), so finish lays out its
+    workspace for a smaller kb than begin did.  fp32: faithful shards over the
+    native exchange (the global k-th bound inside the local call)."""
     N = 6000
-    Qf, planted, tokens, doclens, (terms, off, V) = _corpus(dev, N, B, seed=50 + G)
-    mk = (lambda t, d, base: ColbertIndex.mxfp8(t, d, id_base=base)) if fp8 else \
-        (lambda t, d, base: ColbertIndex(t, d, id_base=base))
+    Qf, planted, tokens, doclens, (terms, off, V) = _corpus(
+        dev, N, B, seed=50 + G, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+    mk = {"fp8": lambda t, d, base: ColbertIndex.mxfp8(t, d, id_base=base),
+          "fp32": lambda t, d, base: ColbertIndex.faithful_f32(t, d, id_base=base),
+          "bf16": lambda t, d, base: ColbertIndex(t, d, id_base=base)}[kind]
     full = mk(tokens, doclens, 0)
     cuts = [0, 40] + [40 + (N - 40) * (g + 1) // (G - 1) for g in range(G - 1)]   # shard 0 < k docs
     ranges = list(zip(cuts[:-1], cuts[1:]))
     shards = [mk(tokens[a:b].contiguous(), doclens[a:b].contiguous(), a) for a, b in ranges]
-    Q = Qf.to(dev, torch.bfloat16)
+    Q = Qf.to(dev) if kind == "fp32" else Qf.to(dev, torch.bfloat16)
     df = NativeBM25.doc_freq(terms, off, V)
     stats = (N, int(off[-1]), df)
     lex_full = NativeBM25(terms, off, V)
@@ -120,9 +129,9 @@ def test_one_trip_sharded_loopback_equals_unsharded(dev, G, B, fp8):
     comms = loopback_comms(G)
     ones = [OneTripRetriever(NativeExchange(shards[r], comm=comms[r]), colbert_k=K, fused=C, final_k=KF)
             for r in range(G)]
-    outs = _run_ranks(G, lambda r: [x.cpu() for x in ones[r](Q, lambda: lex[r].search(qt, qo, KB))])
+    outs = _run_ranks(G, lambda r: [x.cpu() for x in ones[r](Q, lambda: lex[r].search(qt, qo, kb_ret))])
     torch.cuda.synchronize()
-    bi, _ = lex_full.search(qt, qo, KB)
+    bi, _ = lex_full.search(qt, qo, kb_ret)
     want = [x.cpu() for x in _composed(full, Q, bi)]
     for r, got in enumerate(outs):
         for g, w, name in zip(got, want, ("scores", "ids", "positions")):

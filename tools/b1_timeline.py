@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Where the B=1 latency goes: the one-round-trip path (hybrid.OneTripRetriever)
+on one index, run --iters times back to back, for a rocprofv3 kernel +
+memory-copy trace; then `--parse <dir>` folds the trace into a per-iteration
+timeline (median over iterations): every kernel and copy after the scan, its
+duration and the idle gap before it, and the scan-end -> last-event total.
+
+  run:    rocprofv3 --kernel-trace --memory-copy-trace -f csv -d D -o t -- \
+              python3 tools/b1_timeline.py --dtype fp32 --docs 1000000
+  parse:  python3 tools/b1_timeline.py --parse D"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(a):
+    import torch
+    sys.path.insert(0, ROOT)
+    from hybrid_rag_colbertv2_amd import bm25 as bm25_mod
+    from hybrid_rag_colbertv2_amd import synth
+    from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever
+    from hybrid_rag_colbertv2_amd.index import ColbertIndex
+    dev = torch.device("cuda:0")
+    n = a.docs
+    Qf = synth.make_queries(256, 32, seed=1)
+    planted = synth.planted_ids(256, n, 10, seed=2)
+    terms, off, V = synth.bm25_shard(0, n, planted)
+    lex = bm25_mod.sharded(terms, off, V, id_base=0, device=dev)
+    del terms, off
+    qt, qo = synth.bm25_queries(256)
+    bm_one = lambda: lex.search(qt[:qo[1]], qo[:2], 100)   # noqa: E731
+    f32 = a.dtype == "fp32"
+    tokens, doclens = synth.make_shard(0, n, Qf, planted, dev, seed=0,
+                                       dtype=torch.float32 if f32 else torch.bfloat16)
+    ix = (ColbertIndex.faithful_f32(tokens, doclens) if f32 else
+          ColbertIndex.mxfp8(tokens, doclens) if a.dtype == "fp8" else ColbertIndex(tokens, doclens))
+    del tokens
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    Q1 = Qf[:1].to(dev, torch.float32 if f32 else torch.bfloat16).contiguous()
+    one = OneTripRetriever(ix)
+    lat = []
+    for it in range(a.iters + 5):
+        torch.cuda.synchronize()
+        time.sleep(0.002)          # the GPU idles between queries, as in the bench's latency loop
+        t = time.perf_counter()
+        one(Q1, bm_one)
+        torch.cuda.synchronize()
+        if it >= 5:
+            lat.append((time.perf_counter() - t) * 1e3)
+    print(json.dumps({"docs": n, "dtype": a.dtype, "iters": a.iters, "p50_ms": round(statistics.median(lat), 4),
+                      "min_ms": round(min(lat), 4)}), flush=True)
+
+
+def short(name):
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return name.split("(")[0][:60]
+
+
+def parse(d, scan_key):
+    kf = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    mf = glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=True)
+    ev = []
+    for f in kf:
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
+    for f in mf:
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r.get("Direction", "?")))
+    ev.sort()
+    groups, cur = [], []   # iterations: runs of events separated by > 1 ms idle (the sleep between queries)
+    for e in ev:
+        if cur and e[0] - max(x[1] for x in cur) > 1_000_000:
+            groups.append(cur)
+            cur = []
+        cur.append(e)
+    if cur:
+        groups.append(cur)
+    per = []
+    for g in groups:
+        if not any(scan_key in e[2] for e in g):
+            continue
+        rows, prev = [], g[0][0]
+        for (a, b, nm) in g:
+            rows.append((nm, (b - a) / 1e3, max(0, a - prev) / 1e3))
+            prev = max(prev, b)
+        per.append((rows, (prev - g[0][0]) / 1e3))
+    if not per:
+        print("no iterations found")
+        return
+    L = statistics.mode(len(r) for r, _ in per)
+    same = [p for p in per if len(p[0]) == L]
+    print(f"{len(per)} iterations ({len(same)} with the modal {L} events); medians:")
+    tot_d = tot_g = scan = 0.0
+    for k in range(L):
+        nm = same[0][0][k][0]
+        dur = statistics.median(p[0][k][1] for p in same)
+        gap = statistics.median(p[0][k][2] for p in same)
+        if scan_key in nm:
+            scan = dur
+        else:
+            tot_d += dur
+        tot_g += gap
+        print(f"  {nm:60s} {dur:9.1f} us  gap {gap:7.1f} us")
+    span = statistics.median(t for _, t in same)
+    print(f"outside the scan: busy {tot_d:.1f} us + gaps {tot_g:.1f} us; first -> last event {span:.1f} us "
+          f"(scan {scan:.1f} us)")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=1_000_000)
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp8", "fp32"])
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--parse", default=None, help="a rocprofv3 output directory to fold")
+    ap.add_argument("--scan", default="maxsim_scan", help="substring naming the scan kernel")
+    a = ap.parse_args()
+    if a.parse:
+        parse(a.parse, a.scan)
+    else:
+        run(a)
