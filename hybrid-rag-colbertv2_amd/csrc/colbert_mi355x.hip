@@ -1204,11 +1204,16 @@ __device__ __forceinline__ int sload_len(const int32_t* p) {
 }
 // TW2 (lab): two tiles of one doc per wait, as the MXFP8 streaming scan;
 // neutral here (1M B=1 4.722 vs 4.708 ms, profiles/r03z_lab_bf16_tw2.log).
+// bm (nullable): the block maxima of the block-max top-k (block_max_kernel's
+// keys: max of f2u(score) over each 64-doc block) folded into the epilogue --
+// a wave writes its scores 64 docs at a time, which with chunks of a multiple
+// of 64 docs (the launcher's rounding) are exactly one block: one wave max and
+// one store per block, and the separate block-max launch is skipped.
 template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
-    int ld) {
+    int ld, uint32_t* __restrict__ bm, int64_t bm_ld) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[WAVES * SLOTS * 4096];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1337,6 +1342,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
       for (int q = 0; q < QW; ++q) {
         const int qi = qg * QW + q;
         if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
+        if (bm != nullptr) {
+          uint32_t u = lane < cnt ? f2u(sc[q]) : 0u;
+#pragma unroll
+          for (int off = 1; off < 64; off <<= 1) u = max(u, (uint32_t)__shfl_xor((int)u, off));
+          if (lane == 0 && qi < B) bm[(size_t)qi * bm_ld + ((d_begin + i0) >> 6)] = u;
+        }
       }
     }
   }
@@ -3083,10 +3094,17 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 
 // Query split: one wave per query, 4 rows at a time.  beta[b] bounds
 // |T - S| for every doc: sum_i ||q_i|| E + ||q_i - qhi_i|| M + slack (||q_i|| + ||q_i - qhi_i||) M
-// with E = max ||x - hi||, M = max ||hi|| of the index.
+// with E = max ||x - hi||, M = max ||hi|| of the index.  A search's split also
+// resets the row's band state (each nullable): count[b] = 0 (the band
+// collect's counter), lbu[b] = ~0 (the atomic-min of the bf16 top-k's
+// faithful scores, order-preserving bits) and done[b] = 0 (the fallback's
+// finished-workgroup counter) -- one launch fewer than separate memsets.
 __global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict__ Q, int lq,
                                                          uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
-                                                         float E, float M, float* __restrict__ beta) {
+                                                         float E, float M, float* __restrict__ beta,
+                                                         int32_t* __restrict__ count = nullptr,
+                                                         uint32_t* __restrict__ lbu = nullptr,
+                                                         int32_t* __restrict__ done = nullptr) {
   const int b = blockIdx.x, lane = threadIdx.x, grp = lane >> 4, sub = lane & 15;
   float acc = 0.0f;
   for (int r = grp; r < lq; r += 4) {
@@ -3099,7 +3117,12 @@ __global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict
   acc = sub == 0 ? acc : 0.0f;
 #pragma unroll
   for (int off = 16; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
-  if (lane == 0) beta[b] = acc * kBoundUp;
+  if (lane == 0) {
+    beta[b] = acc * kBoundUp;
+    if (count != nullptr) count[b] = 0;
+    if (lbu != nullptr) lbu[b] = 0xffffffffu;
+    if (done != nullptr) done[b] = 0;
+  }
 }
 
 // One row tile, faithful product: acc = init + lo.qhi + hi.qlo + hi.qhi.
@@ -3118,6 +3141,47 @@ __device__ __forceinline__ void tile16_x3(const bf16x8 (&ah)[4], const bf16x8 (&
   }
 }
 
+// Faithful MaxSim of local doc `loc` (ld token slots, `dl` of them scoring)
+// for one query whose split fragments are qh / ql: 128-token blocks of hi +
+// lo, row maxima carried across blocks (LONG), then the sum over the query's
+// lq tokens.  Every faithful rescoring kernel scores a pair through this one
+// function, so a pair's bits never depend on which kernel scored it.
+template <bool LONG>
+__device__ __forceinline__ float faithful_doc16(const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo,
+                                                int64_t loc, int ld, int dl, const bf16x8 (&qh)[2][4],
+                                                const bf16x8 (&ql)[2][4], int lane, int lq) {
+  const int g = lane >> 4;
+  const int lmax = LONG ? ld : kLd;
+  float m[2] = {neg_inf(), neg_inf()};
+  for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {
+    const int dlb = dl - kLd * blk;
+    const size_t at = ((size_t)loc * lmax + (size_t)kLd * blk) * kRowBytes;
+    const uint8_t* dh = hi + at;
+    const uint8_t* dlo = lo + at;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 ah[4][4], al[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int rt = 4 * half + t;
+        if (16 * rt < dlb) {
+          gbl_afrag16(dh, rt, lane, ah[t]);
+          gbl_afrag16(dlo, rt, lane, al[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int rt = 4 * half + t;
+        if (16 * rt < dlb) {
+          const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+          tile16_x3(ah[t], al[t], qh, ql, init, m);
+        }
+      }
+    }
+  }
+  return reduce16(m[0], m[1], lane, lq);
+}
+
 // Faithful rescoring: query b = blockIdx.y against candidates c (cand == null:
 // c is the local doc index), pw consecutive candidates per wave step (1 for
 // small launches: one doc per wave, so a B=1 launch of 100 docs spreads over
@@ -3126,15 +3190,19 @@ __device__ __forceinline__ void tile16_x3(const bf16x8 (&ah)[4], const bf16x8 (&
 // per query (the band collected by the search); only_neg (nullable) skips
 // every query whose status is >= 0 (the search's full-scan fallback).
 // LONG: docs of ld = 256 / 512 / 1024 token slots (128-token blocks, the row
-// maxima carried); the 128-slot build keeps its single-block code.
+// maxima carried); the 128-slot build keeps its single-block code.  lb_min
+// (nullable): every score is also atomic-min'ed into lb_min[b] as
+// order-preserving bits (the two-pass band's lower bound: the minimum
+// faithful score of the bf16 top-k, with no separate reduction launch).
 constexpr int kRsPerWave = 4;
 template <bool LONG = false>
-__global__ __launch_bounds__(256) void rescore_x3_kernel(
+__global__ __launch_bounds__(256, 2) void rescore_x3_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
-    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld, int pw) {
-  const int lane = threadIdx.x & 63, g = lane >> 4;
+    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld, int pw,
+    uint32_t* __restrict__ lb_min) {
+  const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
   if (only_neg != nullptr && only_neg[b] >= 0) return;  // block-uniform; no block-level sync below
@@ -3158,36 +3226,109 @@ __global__ __launch_bounds__(256) void rescore_x3_kernel(
       const int lmax = LONG ? ld : kLd;
       int dl = doclens[loc];
       dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
-      float m[2] = {neg_inf(), neg_inf()};
-      for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {
-        const int dlb = dl - kLd * blk;
-        const size_t at = ((size_t)loc * lmax + (size_t)kLd * blk) * kRowBytes;
-        const uint8_t* dh = hi + at;
-        const uint8_t* dlo = lo + at;
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          bf16x8 ah[4][4], al[4][4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int rt = 4 * half + t;
-            if (16 * rt < dlb) {
-              gbl_afrag16(dh, rt, lane, ah[t]);
-              gbl_afrag16(dlo, rt, lane, al[t]);
-            }
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int rt = 4 * half + t;
-            if (16 * rt < dlb) {
-              const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
-              tile16_x3(ah[t], al[t], qh, ql, init, m);
-            }
-          }
-        }
-      }
-      v = reduce16(m[0], m[1], lane, lq);
+      v = faithful_doc16<LONG>(hi, lo, loc, ld, dl, qh, ql, lane, lq);
     }
-    if (lane == 0) out[(size_t)b * ld_out + c] = v;
+    if (lane == 0) {
+      out[(size_t)b * ld_out + c] = v;
+      if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
+    }
+  }
+}
+
+// Faithful rescoring, one (query, candidate) pair per WORKGROUP: the doc's
+// token rows are split over the 4 waves (wave w takes row tiles 2w, 2w + 1
+// of every 128-token block), each wave folds its rows' maxima to per-query-
+// token column maxima, the workgroup takes the max of the 4 in LDS and wave 0
+// sums them exactly as reduce16 does -- max is exact and order-free, so the
+// score's bits equal rescore_x3_kernel's (one wave walking all 8 tiles).  A
+// pair costs one HBM round trip of 16 KiB per wave and 48 MFMAs per wave
+// instead of two round trips of 32 KiB and 192 MFMAs on one wave: the
+// latency path's rescorings (the bf16 top-k, the band, the 50 candidates)
+// are bound by that per-pair latency, not by bytes.  Same arguments as
+// rescore_x3_kernel (pw unused); grid (pairs, B), grid-stride over pairs.
+// The split pair's score (called by every thread of the workgroup; the result
+// is valid in wave 0): waves' row maxima -> column maxima -> LDS -> max of
+// the 4 -> reduce16's sum.
+template <bool LONG>
+__device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo,
+                                                    int64_t loc, int ld, int dl, const bf16x8 (&qh)[2][4],
+                                                    const bf16x8 (&ql)[2][4], int lane, int wave, int lq,
+                                                    float (&s_m)[4][32]) {
+  const int g = lane >> 4, c16 = lane & 15;
+  const int lmax = LONG ? ld : kLd;
+  float m[2] = {neg_inf(), neg_inf()};
+  for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {
+    const int dlb = dl - kLd * blk;
+    const size_t at = ((size_t)loc * lmax + (size_t)kLd * blk) * kRowBytes;
+    bf16x8 ah[2][4], al[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int rt = 2 * wave + t;
+      if (16 * rt < dlb) {
+        gbl_afrag16(hi + at, rt, lane, ah[t]);
+        gbl_afrag16(lo + at, rt, lane, al[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int rt = 2 * wave + t;
+      if (16 * rt < dlb) {
+        const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+        tile16_x3(ah[t], al[t], qh, ql, init, m);
+      }
+    }
+  }
+  const float w0 = fold16_max(fold32_max(m[0])), w1 = fold16_max(fold32_max(m[1]));
+  if (lane < 16) {
+    s_m[wave][lane] = w0;
+    s_m[wave][16 + lane] = w1;
+  }
+  __syncthreads();
+  float v = 0.0f;
+  if (wave == 0) {
+    const float m0 = fmaxf(fmaxf(s_m[0][c16], s_m[1][c16]), fmaxf(s_m[2][c16], s_m[3][c16]));
+    const float m1 = fmaxf(fmaxf(s_m[0][16 + c16], s_m[1][16 + c16]), fmaxf(s_m[2][16 + c16], s_m[3][16 + c16]));
+    v = dpp_row_sum16((c16 < lq ? m0 : 0.0f) + (16 + c16 < lq ? m1 : 0.0f));
+  }
+  __syncthreads();   // s_m is rewritten by the next pair
+  return v;
+}
+
+template <bool LONG = false>
+__global__ __launch_bounds__(256, 2) void rescore_split_kernel(
+    const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
+    int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
+    const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
+    float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld,
+    uint32_t* __restrict__ lb_min) {
+  __shared__ float s_m[4][32];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  if (only_neg != nullptr && only_neg[b] >= 0) return;  // block-uniform
+  int64_t lim = limit;
+  if (count != nullptr) {
+    const int64_t cb = count[b];
+    lim = cb < lim ? cb : lim;
+  }
+  if ((int64_t)blockIdx.x >= lim) return;  // block-uniform
+  bf16x8 qh[2][4], ql[2][4];
+  load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+  load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+  const int lmax = LONG ? ld : kLd;
+  for (int64_t c = blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
+    const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
+    const int64_t loc = id - id_base;
+    float v = neg_inf();
+    if (id >= 0 && loc >= 0 && loc < n) {                    // block-uniform
+      int dl = doclens[loc];
+      dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
+      v = faithful_doc_split<LONG>(hi, lo, loc, ld, dl, qh, ql, lane, wave, lq, s_m);
+    }
+    if (threadIdx.x == 0) {
+      out[(size_t)b * ld_out + c] = v;
+      if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
+    }
   }
 }
 
@@ -3386,17 +3527,16 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
   }
 }
 
-// Exact lower bound of each row's k-th faithful score: the minimum of the
-// faithful scores of the k docs the bf16 scan ranked first (F[b][0..k), row
-// stride ld): k docs score at least that much, so the k-th best does too.
-__global__ __launch_bounds__(64) void band_lb_kernel(const float* __restrict__ F, int ld, int k,
-                                                     float* __restrict__ lb) {
-  const int b = blockIdx.x;
-  float m = __builtin_inff();
-  for (int j = threadIdx.x; j < k; j += 64) m = fminf(m, F[(size_t)b * ld + j]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off));
-  if (threadIdx.x == 0) lb[b] = m;
+// The band's threshold for row b: the exact lower bound of the k-th faithful
+// score minus beta(b) -- from the caller (lb, floats: the sharded path's
+// global bound) or from the atomic-min of the bf16 top-k's faithful scores
+// (lbu, order-preserving bits) -- or, without either, T_k - 2 beta(b).
+__device__ __forceinline__ float band_threshold(int b, const float* __restrict__ lb, const uint32_t* __restrict__ lbu,
+                                                const float* __restrict__ topk_s, int k,
+                                                const float* __restrict__ beta) {
+  if (lbu != nullptr) return u2f(lbu[b]) - beta[b];
+  if (lb != nullptr) return lb[b] - beta[b];
+  return topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b];
 }
 
 // Band collect: row b of the bf16 scan's scores T; every doc with T >= thr is
@@ -3413,13 +3553,14 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
                                                            const float* __restrict__ beta, int64_t id_base,
                                                            int cap, int32_t* __restrict__ cand,
                                                            int32_t* __restrict__ count,
-                                                           const float* __restrict__ lb = nullptr) {
+                                                           const float* __restrict__ lb,
+                                                           const uint32_t* __restrict__ lbu) {
   __shared__ int32_t s_ids[kBandLds];
   __shared__ int s_n, s_base;
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
-  const float thr = lb != nullptr ? lb[b] - beta[b] : topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b];
+  const float thr = band_threshold(b, lb, lbu, topk_s, k, beta);
   const float* row = T + (size_t)b * n;
   int32_t* crow = cand + (size_t)b * cap;
   constexpr int U = 8;  // 8 coalesced loads in flight per thread, then the ballots
@@ -3458,6 +3599,73 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
   __syncthreads();
   for (int t = threadIdx.x; t < nl; t += blockDim.x)
     if (s_base + t < cap) crow[s_base + t] = s_ids[t];
+}
+
+// Band collect + rescoring in ONE launch, for batches of at most
+// kBandPairMaxB queries over 128-slot docs (the latency path): workgroup x of
+// row b scans docs [x * kBcrDocs, (x + 1) * kBcrDocs) of T, gathers the docs
+// with T >= thr in LDS (never more than its slice: no overflow path),
+// reserves their slots of the band with ONE atomic on count[b], then scores
+// them one after another with the whole workgroup (faithful_doc_split: the
+// same bits as every other faithful rescoring) and writes (global id, score)
+// at the reserved slots.  Slots >= cap are dropped: count[b] > cap marks the
+// row for the full faithful scan.
+constexpr int kBcrDocs = 256 * 2;
+__global__ __launch_bounds__(256, 2) void band_collect_rescore_kernel(
+    const float* __restrict__ T, int64_t n, const float* __restrict__ topk_s, int k, const float* __restrict__ beta,
+    const float* __restrict__ lb, const uint32_t* __restrict__ lbu, const uint8_t* __restrict__ hi,
+    const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t id_base,
+    const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq, int cap, int32_t* __restrict__ cand,
+    float* __restrict__ F, int32_t* __restrict__ count) {
+  __shared__ int32_t s_loc[kBcrDocs];
+  __shared__ float s_m[4][32];
+  __shared__ int s_n, s_base;
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  {
+    const float thr = band_threshold(b, lb, lbu, topk_s, k, beta);
+    const float* row = T + (size_t)b * n;
+    const int64_t i0 = (int64_t)blockIdx.x * kBcrDocs;
+    constexpr int U = kBcrDocs / 256;
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * 256 + threadIdx.x;
+      v[u] = i < n ? row[i] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * 256 + threadIdx.x;
+      const bool take = i < n && v[u] >= thr;
+      const uint64_t mask = __ballot(take);
+      if (mask == 0) continue;   // wave-uniform
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&s_n, __popcll(mask));
+      base = __shfl(base, 0);
+      if (take) s_loc[base + __popcll(mask & ((1ull << lane) - 1ull))] = (int32_t)i;
+    }
+  }
+  __syncthreads();
+  const int nl = s_n;
+  if (nl == 0) return;   // block-uniform
+  if (threadIdx.x == 0) s_base = atomicAdd(count + b, nl);
+  __syncthreads();
+  const int base = s_base;
+  bf16x8 qh[2][4], ql[2][4];
+  load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+  load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+  for (int j = 0; j < nl && base + j < cap; ++j) {   // block-uniform
+    const int64_t loc = s_loc[j];
+    int dl = doclens[loc];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    const float v = faithful_doc_split<false>(hi, lo, loc, kLd, dl, qh, ql, lane, wave, lq, s_m);
+    if (threadIdx.x == 0) {
+      cand[(size_t)b * cap + base + j] = (int32_t)(id_base + loc);
+      F[(size_t)b * cap + base + j] = v;
+    }
+  }
 }
 
 // k-th largest value of the union of G lists of k scores, list g of row b at
@@ -3743,6 +3951,8 @@ struct cbv2_index {
   int topk_bmax = 1;         // CBV2_OPT_TOPK_BMAX (1: block-max top-k where eligible, 0: sampled filter + select)
   int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
   bool band_lower_bound = true;  // CBV2_OPT_BAND_LOWER_BOUND
+  bool band_fused = true;        // CBV2_OPT_BAND_FUSED (B <= 8: collect + rescore in one launch)
+  bool rescore_split = true;     // CBV2_OPT_RESCORE_SPLIT (one pair per workgroup, rows over 4 waves)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -4077,21 +4287,25 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
 // Streaming scans (variants 14-16; 14 / 15 are the B = 1 / 2 production
 // scans of every bf16 index, long documents included): one 4-wave workgroup
 // per CU (128 KiB of LDS rings), chunks for kDirectOversub x the resident waves.
+// bm (nullable): fold the block maxima into the scan (chunks rounded up to a
+// multiple of the 64-doc block; row stride bm_blocks(n)).
 template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
-int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
+                  uint32_t* bm = nullptr) {
   if (ix->dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "stream scan: bf16 index only");
   const int nq_groups = (B + QW - 1) / QW;
   const int64_t target_waves = (int64_t)WAVES * cu_count(ix->device) * kDirectOversub;
   int64_t n_chunks = target_waves / nq_groups;
   if (n_chunks > ix->n) n_chunks = ix->n;
   if (n_chunks < 1) n_chunks = 1;
-  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  if (bm != nullptr) chunk_docs = (chunk_docs + 63) & ~(int64_t)63;
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
   hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS, TW2>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
                      ix->tokens,
-                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
+                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld, bm, bm_blocks(ix->n));
   return launch_check("maxsim_scan_stream_kernel");
 }
 
@@ -4121,8 +4335,14 @@ int scan_maxsim_long(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* ou
   }
 }
 
+// bm (nullable): the production B <= 2 streaming scans fold the block maxima
+// of the block-max top-k into their epilogue (scan_folds_bmax); other scans
+// ignore it.
+bool scan_folds_bmax(const cbv2_index* ix, int B) {
+  return ix->dtype == CBV2_DTYPE_BF16 && ix->ld == kLd && B <= kDirectMaxB && kDefaultScan == kScanAuto;
+}
 int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
-                int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
+                int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr, uint32_t* bm = nullptr) {
   if (ix->n == 0) return CBV2_OK;
   if (ix->ld != kLd) {
     if (ft != nullptr || variant != kScanAuto) return fail(CBV2_EUNSUPPORTED, "long-doc index: automatic scan only");
@@ -4132,8 +4352,12 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, kFusedCap, true>(ix, Q, B, lq, nullptr, 0, st,
                                                                                kScanDynFrac, kScanTaskDocs, nullptr,
                                                                                ctr_ws, ft);
-  if (variant == kScanAuto)
-    variant = B <= kDirectMaxB ? (B == 1 ? kScanStreamQ1 : kScanStreamQ2) : pick_shape(kBf16Shapes, B);
+  if (variant == kScanAuto) {
+    if (B <= kDirectMaxB)
+      return B == 1 ? launch_stream<1, 2>(ix, Q, B, lq, out, ld_out, st, bm)
+                    : launch_stream<2, 2>(ix, Q, B, lq, out, ld_out, st, bm);
+    variant = pick_shape(kBf16Shapes, B);
+  }
   switch (variant) {
     case kScanDirectQ1:
       return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
@@ -4409,8 +4633,9 @@ bool bmax_eligible(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) {
 }
 size_t bm_ws_bytes(int32_t B, int64_t n) { return ((size_t)B * (size_t)bm_blocks(n) * 4 + 255) & ~(size_t)255; }
 
+// blocks_ready: bm already holds the block maxima (folded into the scan)
 int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, uint32_t* bm,
-              float* out_s, int32_t* out_i, hipStream_t st, int dev) {
+              float* out_s, int32_t* out_i, hipStream_t st, int dev, bool blocks_ready = false) {
   static std::atomic<bool> attr_set[64] = {};
   if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
     CBV2_HIP(hipFuncSetAttribute((const void*)topk_bmax_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4418,9 +4643,11 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
     if (dev >= 0 && dev < 64) attr_set[dev].store(true, std::memory_order_relaxed);
   }
   const int64_t nb = bm_blocks(n);
-  hipLaunchKernelGGL(block_max_kernel, dim3((unsigned)((nb + kBmBlocksPerWg - 1) / kBmBlocksPerWg), (unsigned)B),
-                     dim3(256), 0, st, scores, n, ld, bm, nb);
-  if (int rc = launch_check("block_max_kernel")) return rc;
+  if (!blocks_ready) {
+    hipLaunchKernelGGL(block_max_kernel, dim3((unsigned)((nb + kBmBlocksPerWg - 1) / kBmBlocksPerWg), (unsigned)B),
+                       dim3(256), 0, st, scores, n, ld, bm, nb);
+    if (int rc = launch_check("block_max_kernel")) return rc;
+  }
   const size_t lds = kBmFixedLds + (size_t)nb * 4;
   hipLaunchKernelGGL(topk_bmax_kernel, dim3((unsigned)B), dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm,
                      bm_blocks(n), out_s, out_i);
@@ -4476,13 +4703,13 @@ bool scan_event_pair(cbv2_index* ix, hipEvent_t* e0, hipEvent_t* e1) {
 }
 
 int scan_maxsim_timed(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, float* out, int64_t ld_out,
-                      hipStream_t st, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
+                      hipStream_t st, int* ctr_ws = nullptr, FusedTopk* ft = nullptr, uint32_t* bm = nullptr) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timed = scan_event_pair(ix, &e0, &e1);
   if (timed && hipEventRecord(e0, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
   const int rc = ix->dtype == CBV2_DTYPE_MXFP8
                      ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st, kF8DynAuto, kScanTaskDocs, 0, ctr_ws, ft)
-                     : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st, kDefaultScan, ctr_ws, ft);
+                     : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st, kDefaultScan, ctr_ws, ft, bm);
   // the stop event is recorded even after a failed launch, so the reserved pair stays readable
   if (timed && hipEventRecord(e1, st) != hipSuccess && rc == CBV2_OK) return fail(CBV2_EHIP, "hipEventRecord failed");
   return rc;
@@ -4583,8 +4810,9 @@ struct F32Ws {
   uint16_t* qhi = nullptr;
   uint16_t* qlo = nullptr;
   float* beta = nullptr;
-  float* lb = nullptr;
+  float* lb = nullptr;        // SEARCH: the two-pass band's bound, order-preserving bits (atomic min)
   int32_t* count = nullptr;
+  int32_t* done = nullptr;    // SEARCH: finished-workgroup counter per row (reset by the split)
   int32_t* cand = nullptr;
   float* F = nullptr;
   void* tk = nullptr;
@@ -4618,6 +4846,7 @@ size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8
   if (op == CBV2_F32_RERANK) w->F = (float*)take((size_t)B * cap * sizeof(float));
   if (op == CBV2_F32_SEARCH) {
     w->count = (int32_t*)take((size_t)B * sizeof(int32_t));
+    w->done = (int32_t*)take((size_t)B * sizeof(int32_t));
     w->cand = (int32_t*)take((size_t)B * cap * sizeof(int32_t));
     w->F = (float*)take((size_t)B * cap * sizeof(float));
     w->tk_bytes = std::max(topk_ws_bytes(B, ix->n), bm_ws_bytes(B, ix->n));   // either top-k of T
@@ -4650,19 +4879,28 @@ int check_f32(cbv2_index* ix, int op, const float* Q, int32_t B, int32_t lq, int
   return CBV2_OK;
 }
 
+// (a SEARCH workspace's split also resets the rows' band state: count, lb, done)
 int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st) {
   hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(64), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
-                     ix->norm_max, w->beta);
+                     ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done);
   return launch_check("split_query_kernel");
 }
 
 // pw: candidates per wave step (0 = auto: one per wave for launches of at
 // most kRsSmallPairs (query, candidate) pairs, kRsPerWave beyond)
 constexpr int64_t kRsSmallPairs = 4096;
+constexpr int64_t kRsSplitGrid = 1024;   // workgroups per row of a split rescoring launch (grid-stride beyond)
 int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t* cand, const int32_t* count,
                    int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
-                   const int32_t* only_neg = nullptr, int pw = 0) {
+                   const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr) {
   if (limit <= 0) return CBV2_OK;
+  if (ix->rescore_split) {   // one pair per workgroup (its doc split over the 4 waves)
+    const unsigned gx = (unsigned)(limit < kRsSplitGrid ? limit : kRsSplitGrid);
+    hipLaunchKernelGGL(ix->ld != kLd ? rescore_split_kernel<true> : rescore_split_kernel<false>, dim3(gx, (unsigned)B),
+                       dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq,
+                       cand, count, limit, ld_c, out, ld_out, only_neg, (int)ix->ld, lb_min);
+    return launch_check("rescore_split_kernel");
+  }
   if (pw <= 0) pw = (int64_t)B * limit <= kRsSmallPairs ? 1 : kRsPerWave;
   const int64_t per_wg = 4LL * pw;
   int64_t gx = (limit + per_wg - 1) / per_wg;
@@ -4672,7 +4910,7 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
   hipLaunchKernelGGL(ix->ld != kLd ? rescore_x3_kernel<true> : rescore_x3_kernel<false>, dim3((unsigned)gx, (unsigned)B),
                      dim3(256), 0, st, ix->tokens, ix->resid,
                      ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out,
-                     only_neg, (int)ix->ld, pw);
+                     only_neg, (int)ix->ld, pw, lb_min);
   return launch_check("rescore_x3_kernel");
 }
 }  // namespace
@@ -4756,6 +4994,33 @@ int cbv2_quantize_mxfp8(const void* x, int32_t dtype, int64_t rows, void* q, voi
     return fail(CBV2_EINVAL, "quantize takes bf16 or f32 input (got dtype %d)", dtype);
   }
   return launch_check("quantize_mxfp8_kernel");
+}
+
+int cbv2_hbm_alloc(int device, size_t bytes, void** out, int32_t* contiguous) {
+  CBV2_REQUIRE(out != nullptr, "null output pointer");
+  *out = nullptr;
+  if (contiguous) *contiguous = 0;
+  if (bytes == 0) return CBV2_OK;
+  DeviceGuard dg(device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", device);
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p != nullptr) {
+    *out = p;
+    if (contiguous) *contiguous = 1;
+    return CBV2_OK;
+  }
+  (void)hipGetLastError();   // no contiguous range of that size: plain VRAM
+  CBV2_HIP(hipMalloc(&p, bytes));
+  *out = p;
+  return CBV2_OK;
+}
+
+int cbv2_hbm_free(int device, void* p) {
+  if (p == nullptr) return CBV2_OK;
+  DeviceGuard dg(device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", device);
+  CBV2_HIP(hipFree(p));
+  return CBV2_OK;
 }
 
 int cbv2_index_destroy(cbv2_index* index) {
@@ -4887,8 +5152,9 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
   if (bmax_eligible(ix, scorer, B, k)) {   // block maxima, then one select reading only the blocks that can win
     uint32_t* bm = (uint32_t*)rest;
     float* sc = (float*)(rest + bm_ws_bytes(B, ix->n));
-    if ((rc = scan_maxsim_timed(ix, Q, B, lq, sc, ix->n, st, ctr))) return rc;
-    return topk_bmax(sc, B, ix->n, ix->n, k, ix->id_base, bm, out_scores, out_ids, st, ix->device);
+    const bool fold = scan_folds_bmax(ix, B);   // the B <= 2 streaming scans write the block maxima themselves
+    if ((rc = scan_maxsim_timed(ix, Q, B, lq, sc, ix->n, st, ctr, nullptr, fold ? bm : nullptr))) return rc;
+    return topk_bmax(sc, B, ix->n, ix->n, k, ix->id_base, bm, out_scores, out_ids, st, ix->device, fold);
   }
   const size_t tk = topk_ws_bytes(B, ix->n);
   float* sc = (float*)(rest + tk);
@@ -4915,6 +5181,12 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
       return CBV2_OK;
     case CBV2_OPT_TOPK_BMAX:
       ix->topk_bmax = (int)value;
+      return CBV2_OK;
+    case CBV2_OPT_BAND_FUSED:
+      ix->band_fused = value != 0;
+      return CBV2_OK;
+    case CBV2_OPT_RESCORE_SPLIT:
+      ix->rescore_split = value != 0;
       return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);
@@ -5087,13 +5359,14 @@ int cbv2_score_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, void* 
 
 namespace {
 // Faithful search, phase 1: split the queries, bf16 scan of hi (T), its top-k
-// (out), and -- with the two-pass band -- the exact lower bound lb of each
-// row's k-th faithful score (the minimum faithful score of the bf16 top-k)
-// into lb_out; fk_out (nullable): those k faithful scores themselves, [B][k].
+// (out), and -- with the two-pass band (want_lb) -- the exact lower bound of
+// each row's k-th faithful score (the minimum faithful score of the bf16
+// top-k, atomic-min'ed into w.lb as order-preserving bits by the rescoring
+// itself); fk_out (nullable): those k faithful scores themselves, [B][k].
 // Returns 1 when the whole search is already done (k beyond any band: the
 // full faithful scan ran, status -1 everywhere).
 int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w,
-                      float* out_scores, int32_t* out_ids, int32_t* out_status, float* lb_out, hipStream_t st,
+                      float* out_scores, int32_t* out_ids, int32_t* out_status, bool want_lb, hipStream_t st,
                       float* fk_out = nullptr) {
   int rc;
   if (ix->n == 0) {
@@ -5110,20 +5383,21 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     return 1;
   }
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
-  if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr))) return rc;
-  if ((rc = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k)
-                ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st, ix->device)
-                : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st,
-                            ix->device)))
+  const bool bmax = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k);
+  const bool fold = bmax && scan_folds_bmax(ix, B);
+  if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr, nullptr, fold ? (uint32_t*)w.tk : nullptr)))
+    return rc;
+  if ((rc = bmax ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st,
+                             ix->device, fold)
+                 : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st,
+                             ix->device)))
     return rc;
   if ((rc = band_mark(ix, false, st))) return rc;
   if (fk_out != nullptr)     // the bf16 top-k's own faithful scores, for the caller's cross-shard bound
     return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, fk_out, k, st);
-  if (lb_out != nullptr) {   // the bf16 top-k's own faithful scores: k docs score at least their minimum
-    if ((rc = launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, w.F, cap, st))) return rc;
-    hipLaunchKernelGGL(band_lb_kernel, dim3((unsigned)B), dim3(64), 0, st, w.F, cap, k, lb_out);
-    if ((rc = launch_check("band_lb_kernel"))) return rc;
-  }
+  if (want_lb)   // the bf16 top-k's own faithful scores: k docs score at least their minimum
+    return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, w.F, cap, st, nullptr, 0,
+                          reinterpret_cast<uint32_t*>(w.lb));
   return CBV2_OK;
 }
 
@@ -5131,21 +5405,33 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
 // beta, the one-pass band), its faithful rescoring, the exact top-k of the
 // band, and the full faithful scan for rows whose band overflowed cap.
 int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w,
-                           const float* lb, float* out_scores, int32_t* out_ids, int32_t* out_status, hipStream_t st) {
+                           const float* lb, const uint32_t* lbu, float* out_scores, int32_t* out_ids,
+                           int32_t* out_status, hipStream_t st) {
   int rc;
-  CBV2_HIP(hipMemsetAsync(w.count, 0, (size_t)B * sizeof(int32_t), st));
+  // (count[b] was reset by the query split of phase 1)
   int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
   const int64_t max_splits = (ix->n + 8191) / 8192;
   splits = splits < max_splits ? splits : max_splits;
   splits = splits < 1 ? 1 : splits;
-  hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
-                     out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb);
-  if ((rc = launch_check("band_collect_kernel"))) return rc;
+  if (B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused) {
+    // the latency path: collect + rescore in one launch, one band doc per wave
+    const int64_t gx = (ix->n + kBcrDocs - 1) / kBcrDocs;
+    hipLaunchKernelGGL(band_collect_rescore_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
+                       out_scores, k, w.beta, lb, lbu, ix->tokens, ix->resid, ix->doclens, ix->id_base, w.qhi, w.qlo,
+                       lq, cap, w.cand, w.F, w.count);
+    if ((rc = launch_check("band_collect_rescore_kernel"))) return rc;
+  } else {
+    hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
+                       out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb, lbu);
+    if ((rc = launch_check("band_collect_kernel"))) return rc;
+  }
   // pairs grouped by doc (each band doc's tiles read once per batch) pay when
   // the queries' bands overlap; a batch of at most kBandPairMaxB queries
   // rescores pair by pair, one band doc per wave, without the doc-major
   // passes over all n docs (count memset, offsets)
-  if (ix->band_doc_major && B > kBandPairMaxB) {
+  if (B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused) {
+    // rescored above
+  } else if (ix->band_doc_major && B > kBandPairMaxB) {
     CBV2_HIP(hipMemsetAsync(w.dcnt, 0, (size_t)ix->n * sizeof(int32_t), st));
     CBV2_HIP(hipMemsetAsync(w.dctr, 0, 2 * sizeof(int32_t), st));
     const unsigned gc = (unsigned)std::min<int64_t>((cap + 255) / 256, 16);
@@ -5183,8 +5469,9 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
 }
 
 int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w, const float* lb,
-                      float* out_scores, int32_t* out_ids, int32_t* out_status, hipStream_t st) {
-  const int rc = search_f32_phase2_impl(ix, B, lq, k, cap, w, lb, out_scores, out_ids, out_status, st);
+                      const uint32_t* lbu, float* out_scores, int32_t* out_ids, int32_t* out_status,
+                      hipStream_t st) {
+  const int rc = search_f32_phase2_impl(ix, B, lq, k, cap, w, lb, lbu, out_scores, out_ids, out_status, st);
   if (rc) return rc;
   return band_mark(ix, true, st);
 }
@@ -5225,10 +5512,11 @@ int cbv2_search_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32
   //    the k-th faithful score (the bf16 top-k's own faithful scores: the
   //    minimum of k of them), or T_k - 2 beta without that pass (A/B);
   // 3. faithful rescoring of the band, 4. exact top-k of the band
-  float* lb = ix->band_lower_bound ? w.lb : nullptr;
-  rc = search_f32_phase1(ix, Q, B, lq, k, cap, w, out_scores, out_ids, out_status, lb, st);
+  const bool two_pass = ix->band_lower_bound;
+  rc = search_f32_phase1(ix, Q, B, lq, k, cap, w, out_scores, out_ids, out_status, two_pass, st);
   if (rc) return rc < 0 ? rc : CBV2_OK;
-  return search_f32_phase2(ix, B, lq, k, cap, w, lb, out_scores, out_ids, out_status, st);
+  return search_f32_phase2(ix, B, lq, k, cap, w, nullptr, two_pass ? reinterpret_cast<const uint32_t*>(w.lb) : nullptr,
+                           out_scores, out_ids, out_status, st);
 }
 
 int cbv2_search_f32_begin(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, void* ws,
@@ -5245,7 +5533,7 @@ int cbv2_search_f32_begin(cbv2_index* ix, const float* Q, int32_t B, int32_t lq,
   hipLaunchKernelGGL(fill_neg_inf_kernel, dim3((unsigned)(((int64_t)B * k + 255) / 256)), dim3(256), 0, st, fk,
                      (int64_t)B * k);
   if ((rc = launch_check("fill_neg_inf_kernel"))) return rc;
-  rc = search_f32_phase1(ix, Q, B, lq, k, cap, w, out_scores, out_ids, out_status, nullptr, st, fk);
+  rc = search_f32_phase1(ix, Q, B, lq, k, cap, w, out_scores, out_ids, out_status, false, st, fk);
   return rc < 0 ? rc : CBV2_OK;
 }
 
@@ -5265,7 +5553,7 @@ int cbv2_search_f32_finish(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
   if (ix->n == 0 || k > kBandCapMax) return CBV2_OK;   // phase 1 already finished these
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
-  return search_f32_phase2(ix, B, lq, k, cap, w, lb, out_scores, out_ids, out_status, (hipStream_t)stream);
+  return search_f32_phase2(ix, B, lq, k, cap, w, lb, nullptr, out_scores, out_ids, out_status, (hipStream_t)stream);
 }
 
 int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const int32_t* cand, int32_t C,

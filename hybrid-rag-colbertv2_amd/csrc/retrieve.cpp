@@ -14,6 +14,7 @@
 // sequences them, so the arithmetic and the tie rules live in one place.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -44,6 +45,33 @@ int err(int code, const char* fmt, ...) {
   } while (0)
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// The round trip's wait: an event after the D2H copy, polled by this thread
+// (hipEventQuery) for up to kSpinNs, then a blocking wait.  The stream work
+// ahead of the copy is one scan (~5 ms at B=1, 1M docs) or one batch; a
+// blocking hipStreamSynchronize wakes the host tens of microseconds after the
+// copy lands (measured: 26-39 us from the D2H copy's end to the next H2D
+// copy's start), a poll within about a microsecond.  One event per thread
+// and device, created once.
+constexpr long long kSpinNs = 50LL * 1000 * 1000;
+int wait_copy(hipStream_t st) {
+  thread_local hipEvent_t ev[64] = {};
+  int dev = 0;
+  RT_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return hipStreamSynchronize(st) == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "sync failed");
+  if (!ev[dev]) RT_HIP(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+  RT_HIP(hipEventRecord(ev[dev], st));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev[dev]);
+    if (q == hipSuccess) return CBV2_OK;
+    if (q != hipErrorNotReady) return err(CBV2_EHIP, "hipEventQuery (%d)", (int)q);
+    if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kSpinNs)
+      break;
+  }
+  RT_HIP(hipEventSynchronize(ev[dev]));
+  return CBV2_OK;
+}
 
 struct Kind {
   int32_t dtype = 0, faithful = 0;
@@ -191,7 +219,7 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     bm = H.lex_merged;
   }
   RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
-  RT_HIP(hipStreamSynchronize(st));   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  if ((rc = wait_copy(st))) return rc;   // the one host round trip: the ColBERT (and merged BM25) top-k are here
   if ((rc = cbv2_rrf_fuse(bm, kb, H.ids, k, B, rrf_k, C, H.cand, nullptr, nullptr))) return rc;
   RT_HIP(hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st));
   if (c)

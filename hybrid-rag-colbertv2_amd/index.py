@@ -38,6 +38,70 @@ def _stream_ptr(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_HBM_MIN_BYTES = 64 << 20   # buffers below this stay in torch's caching allocator
+
+
+class _HbmBlock:
+    """Device memory from ``cbv2_hbm_alloc`` -- physically contiguous when the
+    driver can provide it (the streaming scans' translation is then one
+    contiguous range: the B=1 scan over 1M docs ran 4.63-4.67 ms vs 4.75-4.99
+    from plain hipMalloc, tools/probes/alloc_probe.cpp) -- exposed to torch
+    through ``__cuda_array_interface__`` (torch keeps a reference for as long
+    as a tensor views it) and freed by ``cbv2_hbm_free`` with the last one."""
+
+    def __init__(self, device: torch.device, nbytes: int):
+        self.device = device.index if device.index is not None else torch.cuda.current_device()
+        h, c = ctypes.c_void_p(), ctypes.c_int32(0)
+        _lib.check(_lib.lib().cbv2_hbm_alloc(self.device, int(nbytes), ctypes.byref(h), ctypes.byref(c)))
+        self.ptr, self.nbytes, self.contiguous = int(h.value or 0), int(nbytes), bool(c.value)
+        self.__cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 3, "strides": None, "stream": None}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                _HBM_BLOCKS.pop(self.ptr, None)
+                _lib.lib().cbv2_hbm_free(self.device, ctypes.c_void_p(self.ptr))
+                self.ptr = 0
+        except Exception:
+            pass
+
+
+def hbm_empty(shape, dtype: torch.dtype, device) -> torch.Tensor:
+    """An uninitialised device tensor for an index array: at least
+    ``_HBM_MIN_BYTES`` -> ``cbv2_hbm_alloc`` (physically contiguous HBM when
+    available), smaller -> torch's allocator.  ``hbm_placement(t)`` tells which."""
+    device = torch.device(device)
+    shape = tuple(int(x) for x in shape)
+    numel = 1
+    for x in shape:
+        numel *= x
+    nbytes = numel * torch.empty((), dtype=dtype).element_size()
+    if device.type != "cuda" or nbytes < _HBM_MIN_BYTES:
+        return torch.empty(shape, dtype=dtype, device=device)
+    blk = _HbmBlock(device, nbytes)
+    raw = torch.as_tensor(blk, device=device)
+    if raw.data_ptr() != blk.ptr or raw.numel() != nbytes:
+        raise RuntimeError("torch.as_tensor did not alias the HBM block")
+    t = raw.view(dtype).view(shape)
+    _HBM_BLOCKS[t.data_ptr()] = blk.contiguous
+    return t
+
+
+_HBM_BLOCKS: dict = {}
+
+
+def hbm_zeros(shape, dtype: torch.dtype, device) -> torch.Tensor:
+    return hbm_empty(shape, dtype, device).zero_()
+
+
+def hbm_placement(t: torch.Tensor) -> str:
+    """"contiguous" / "hipMalloc" for a tensor from ``hbm_empty`` (its first
+    byte), "torch" otherwise."""
+    c = _HBM_BLOCKS.get(t.data_ptr())
+    return "torch" if c is None else ("contiguous" if c else "hipMalloc")
+
+
 def _require_cuda(t: torch.Tensor, name: str):
     if not t.is_cuda:
         raise ValueError(f"{name} must be a ROCm device tensor (got {t.device})")
@@ -76,13 +140,13 @@ def pack_tokens(embs: Union[torch.Tensor, Sequence[torch.Tensor]], device,
         n, L, D = embs.shape
         if D != DIM or L > ld:
             raise ValueError(f"doc embeddings must be [n, L<={ld}, {DIM}] (got {tuple(embs.shape)})")
-        tokens = torch.zeros((n, ld, DIM), dtype=dtype, device=device)
+        tokens = hbm_zeros((n, ld, DIM), dtype, device)
         tokens[:, :L] = embs.to(device=device, dtype=dtype)
         doclens = torch.full((n,), L, dtype=torch.int32, device=device)
         return tokens, doclens
     embs = list(embs)
     n = len(embs)
-    tokens = torch.zeros((n, ld, DIM), dtype=dtype, device=device)
+    tokens = hbm_zeros((n, ld, DIM), dtype, device)
     lens = []
     for i, e in enumerate(embs):
         e = e if e.dim() == 2 else e.unsqueeze(0)
@@ -104,7 +168,7 @@ def quantize_mxfp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         x, dt = x.float(), _lib.DTYPE_F32
     x = x.contiguous()
     rows = x.numel() // DIM
-    buf = torch.empty(rows * (DIM + 2), dtype=torch.uint8, device=x.device)
+    buf = hbm_empty((rows * (DIM + 2),), torch.uint8, x.device)
     q, sc = buf[: rows * DIM], buf[rows * DIM:]
     _lib.check(_lib.lib().cbv2_quantize_mxfp8(x.data_ptr(), dt, rows, q.data_ptr(), sc.data_ptr(),
                                               _stream_ptr(x.device)))
@@ -183,8 +247,8 @@ class ColbertIndex:
             raise ValueError(f"tokens_f32 must be f32 [n, ld, {DIM}], ld in {LONG_LDS} (got {tokens_f32.dtype} "
                              f"{tuple(tokens_f32.shape)})")
         x = tokens_f32.contiguous()
-        hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-        lo = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        hi = hbm_empty(x.shape, torch.bfloat16, x.device)     # the array every scan streams
+        lo = hbm_empty(x.shape, torch.bfloat16, x.device)
         bounds = torch.zeros(2, dtype=torch.float32, device=x.device)
         _require_cuda(doclens, "doclens")
         if doclens.dtype != torch.int32 or doclens.shape != (x.shape[0],):
@@ -276,8 +340,8 @@ class ColbertIndex:
         if begin < 0 or m < 0 or end > n:
             raise ValueError(f"doc range [{begin}, {end}) outside [0, {n})")
         fp8 = dt == _lib.DTYPE_MXFP8
-        tokens = torch.empty((m, ld, DIM), dtype=torch.uint8 if fp8 else torch.bfloat16, device=device)
-        scales = torch.empty((m, ld, 2), dtype=torch.uint8, device=device) if fp8 else None
+        tokens = hbm_empty((m, ld, DIM), torch.uint8 if fp8 else torch.bfloat16, device)
+        scales = hbm_empty((m, ld, 2), torch.uint8, device) if fp8 else None
         doclens = torch.empty((m,), dtype=torch.int32, device=device)
         with torch.cuda.device(device):
             _lib.check(_lib.lib().cbv2_index_file_read(
@@ -291,7 +355,7 @@ class ColbertIndex:
             if index_file_layout(path + ".resid")[1:] != (n, id_base, ld) or \
                     b.get("hi") != file_fingerprint(path) or b.get("resid") != file_fingerprint(path + ".resid"):
                 raise ValueError(f"{path}.resid / .bounds.json were not written with {path}")
-            resid = torch.empty((m, ld, DIM), dtype=torch.bfloat16, device=device)
+            resid = hbm_empty((m, ld, DIM), torch.bfloat16, device)
             dl2 = torch.empty((m,), dtype=torch.int32, device=device)
             with torch.cuda.device(device):
                 _lib.check(_lib.lib().cbv2_index_file_read(
@@ -592,19 +656,19 @@ class IndexBuilder:
         self.pos = 0
         self.doclens = torch.zeros((self.n,), dtype=torch.int32, device=self.device)
         if dtype == "fp8":     # padding rows: e4m3 zeros, scale 2^0 (never scored)
-            self.tokens = torch.zeros((self.n, self.ld, DIM), dtype=torch.uint8, device=self.device)
-            self.scales = torch.full((self.n, self.ld, 2), 127, dtype=torch.uint8, device=self.device)
+            self.tokens = hbm_zeros((self.n, self.ld, DIM), torch.uint8, self.device)
+            self.scales = hbm_empty((self.n, self.ld, 2), torch.uint8, self.device).fill_(127)
         else:
-            self.tokens = torch.zeros((self.n, self.ld, DIM), dtype=torch.bfloat16, device=self.device)
+            self.tokens = hbm_zeros((self.n, self.ld, DIM), torch.bfloat16, self.device)
             self.scales = None
         if dtype == "fp32":
-            self.residual = torch.zeros((self.n, self.ld, DIM), dtype=torch.bfloat16, device=self.device)
+            self.residual = hbm_zeros((self.n, self.ld, DIM), torch.bfloat16, self.device)
             self.bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
 
     def _relayout(self, ld: int) -> None:
         """Grow every doc to ld token slots (padding rows zero, never scored)."""
         def grown(x, fill=0):
-            y = torch.full((self.n, ld, x.shape[2]), fill, dtype=x.dtype, device=self.device)
+            y = hbm_empty((self.n, ld, x.shape[2]), x.dtype, self.device).fill_(fill)
             y[: self.pos, : self.ld] = x[: self.pos]
             return y
         self.tokens = grown(self.tokens)

@@ -80,8 +80,12 @@ def make_shard(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray, devic
                sigma: float = 0.1, dtype: torch.dtype = torch.bfloat16) -> Tuple[torch.Tensor, torch.Tensor]:
     """Docs [begin, end) of the synthetic corpus: (``dtype`` [n, 128, 128], int32 doclens [n]) on ``device``
     (bf16 = the fp32 draw rounded, so both dtypes describe the same corpus)."""
+    from .index import hbm_empty
     n = end - begin
-    tokens = torch.empty((n, LD, DIM), dtype=dtype, device=device)
+    # the index array (bf16 / MXFP8) in contiguous HBM like every index build;
+    # an fp32 source (split into an fp32-faithful index) in torch's allocator
+    tokens = (torch.empty((n, LD, DIM), dtype=dtype, device=device) if dtype == torch.float32
+              else hbm_empty((n, LD, DIM), dtype, device))
     doclens = torch.full((n,), LD, dtype=torch.int32, device=device)
     for lo, hi, t in iter_shard(begin, end, Q, planted, device, seed, sigma, dtype):
         tokens[lo - begin: hi - begin] = t
@@ -94,10 +98,10 @@ def make_shard_mxfp8(begin: int, end: int, Q: torch.Tensor, planted: np.ndarray,
     bf16 tokens, exactly as ``ColbertIndex.mxfp8(make_shard(...))`` would):
     (e4m3 uint8 [n, 128, 128], E8M0 uint8 [n, 128, 2], int32 doclens [n]).
     Peak extra memory is one generator chunk, so 10M docs (167 GB) fit one HBM."""
-    from .index import quantize_mxfp8
+    from .index import hbm_empty, quantize_mxfp8
     n = end - begin
-    q = torch.empty((n, LD, DIM), dtype=torch.uint8, device=device)
-    sc = torch.empty((n, LD, 2), dtype=torch.uint8, device=device)
+    q = hbm_empty((n, LD, DIM), torch.uint8, device)
+    sc = hbm_empty((n, LD, 2), torch.uint8, device)
     doclens = torch.full((n,), LD, dtype=torch.int32, device=device)
     for lo, hi, t in iter_shard(begin, end, Q, planted, device, seed, sigma, torch.bfloat16):
         qq, ss = quantize_mxfp8(t)

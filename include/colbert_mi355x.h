@@ -84,6 +84,18 @@ int cbv2_index_create(int device, const void* tokens, int32_t dtype, int64_t n, 
                       int32_t d, const int32_t* doclens, int64_t id_base, cbv2_index** out);
 int cbv2_index_destroy(cbv2_index* index);
 
+/* Index memory placement (no reference counterpart).  cbv2_hbm_alloc: `bytes`
+ * of device memory on `device`, PHYSICALLY CONTIGUOUS when the driver can
+ * provide it (hipExtMallocWithFlags(hipDeviceMallocContiguous); *contiguous =
+ * 1), else plain hipMalloc (0).  Large index buffers (the token arrays every
+ * scan streams) belong there: the B = 1 streaming scan over 1M docs (32.8 GB)
+ * ran 4.63-4.67 ms from contiguous allocations and 4.75-4.99 ms from plain
+ * hipMalloc ones of the same process (tools/probes/alloc_probe.cpp) -- the
+ * translation of a streamed range is cheaper when it is one contiguous
+ * physical range.  Free with cbv2_hbm_free (synchronous, like hipFree).    */
+int cbv2_hbm_alloc(int device, size_t bytes, void** out, int32_t* contiguous);
+int cbv2_hbm_free(int device, void* p);
+
 /* Scan timing (measurement only; no reference counterpart -- the reference
  * prints wall-clock stage timings, local_rag_complete.py:905-933).  While
  * enabled, every MaxSim scan launch of this handle (cbv2_score / cbv2_search /
@@ -119,6 +131,15 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        top-k, whose minimum faithful score lb bounds the
  *                        k-th from below, and bands T >= lb - beta (0: the
  *                        wider T >= T_k - 2 beta).  Identical results.
+ *  CBV2_OPT_BAND_FUSED   1: cbv2_search_f32 on at most 8 queries (128-slot
+ *                        docs) collects the band and rescores it in ONE
+ *                        launch (0: a collect launch, then a rescoring
+ *                        launch).  Identical results.
+ *  CBV2_OPT_RESCORE_SPLIT 1: the fp32-faithful rescorings (the bf16 top-k, the
+ *                        band of <= 8 queries, rerank candidates, the
+ *                        full-scan fallback) score one (query, doc) pair per
+ *                        workgroup, the doc's rows split over its 4 waves (0:
+ *                        one pair per wave).  Identical results.
  *  CBV2_OPT_TOPK_BMAX    1: cbv2_search's unfused MaxSim scan (rows of >= 65,536
  *                        and <= 1,572,864 docs, k <= 1024) also folds the max of
  *                        every 64-doc block, and ONE select launch reads only
@@ -134,6 +155,8 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_BAND_DOC_MAJOR 3
 #define CBV2_OPT_BAND_LOWER_BOUND 4
 #define CBV2_OPT_TOPK_BMAX 5
+#define CBV2_OPT_BAND_FUSED 6
+#define CBV2_OPT_RESCORE_SPLIT 7
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

@@ -267,3 +267,61 @@ def test_band_select_wide_bands_ties(dev, copies):
         assert (i.cpu().numpy() == np.arange(300, 400)[None, :]).all()
         exact = orc.maxsim(Q.numpy(), docs[300:301].numpy(), doclens[300:301].numpy())[0, 0]
         np.testing.assert_allclose(s.cpu().numpy(), exact, atol=ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("B,copies", [(1, 0), (5, 0), (8, 0), (1, 3000), (3, 3000)])
+def test_band_fused_equals_separate_launches(dev, B, copies):
+    """Batches of at most 8 queries collect and rescore their band in ONE
+    launch (band_collect_rescore_kernel, CBV2_OPT_BAND_FUSED): scores, ids and
+    band sizes equal the collect-then-rescore launches bit for bit -- also
+    when 3,000 tied copies put more hits in one workgroup than its LDS list
+    holds (the overflow hits are rescored as they come) and when the band
+    overflows cap (the full faithful scan takes the row)."""
+    docs, doclens, Q = make_case(101 + B, 20000, B, 32)
+    if copies:
+        docs[5000:5000 + copies] = docs[97 % 20000]          # query 0's planted doc, copied: ties
+        doclens[5000:5000 + copies] = 128
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=11)
+    Qd = Q.to(dev)
+    for cap in (16384, 64):
+        ix.set_option(_lib.OPT_BAND_FUSED, 1)
+        s1, i1 = ix._search_f32(Qd.contiguous(), B, 32, 100, cap=cap)
+        b1 = ix.last_band.clone()
+        ix.set_option(_lib.OPT_BAND_FUSED, 0)
+        s0, i0 = ix._search_f32(Qd.contiguous(), B, 32, 100, cap=cap)
+        b0 = ix.last_band.clone()
+        assert torch.equal(i1, i0) and torch.equal(s1, s0), cap
+        assert torch.equal(b1, b0), (cap, b1, b0)
+    ix.set_option(_lib.OPT_BAND_FUSED, 1)
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    assert_ranking_consistent(i1.cpu().numpy(), exact, ATOL, id_base=11)
+
+
+@pytest.mark.parametrize("B,ld", [(1, 128), (5, 128), (12, 128), (3, 256)])
+def test_rescore_split_equals_one_wave_per_pair(dev, B, ld):
+    """One pair per workgroup, the doc's rows split over its 4 waves
+    (rescore_split_kernel, CBV2_OPT_RESCORE_SPLIT) vs one pair per wave
+    (rescore_x3_kernel): search (bf16 top-k rescoring, band, fallback), rerank
+    and the full faithful scores equal bit for bit; ragged and empty docs, and
+    docs past 128 tokens (ld 256: the 128-token blocks carried)."""
+    docs, doclens, Q = make_case(301 + B + ld, 6000, B, 32)
+    if ld > 128:
+        docs = torch.cat([docs, torch.flip(docs, dims=(1,))], dim=1).contiguous()
+        doclens = torch.randint(0, ld + 1, doclens.shape, generator=torch.Generator().manual_seed(ld),
+                                dtype=torch.int32)
+    doclens[::17] = 0
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=5)
+    Qd = Q.to(dev)
+    cand = torch.randint(0, 6010, (B, 50), generator=torch.Generator().manual_seed(B), dtype=torch.int32).to(dev)
+    got = {}
+    for split in (1, 0):
+        ix.set_option(_lib.OPT_RESCORE_SPLIT, split)
+        s, i = ix.search(Qd, 100)
+        sc, si = ix._search_f32(Qd.contiguous(), B, 32, 100, cap=100)        # forces the full-scan fallback
+        rs, ri, rp = ix.rerank(Qd, cand, 10)
+        got[split] = [x.clone() for x in (s, i, sc, si, rs, ri, rp, ix.score(Qd), ix.rerank(Qd, cand, 0))]
+    ix.set_option(_lib.OPT_RESCORE_SPLIT, 1)
+    for a, b, name in zip(got[1], got[0], ("s", "i", "sc", "si", "rs", "ri", "rp", "score", "raw")):
+        assert torch.equal(a, b), name
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    np.testing.assert_allclose(got[1][7].cpu().numpy(), exact, atol=ATOL, rtol=0)
