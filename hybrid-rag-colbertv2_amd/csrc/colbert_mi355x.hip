@@ -1213,7 +1213,7 @@ template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = f
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
-    int ld, uint32_t* __restrict__ bm, int64_t bm_ld) {
+    int ld, uint32_t* __restrict__ bm, int64_t bm_ld, uint32_t* __restrict__ sb, int64_t sb_ld) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[WAVES * SLOTS * 4096];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1271,8 +1271,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
 #pragma unroll
   for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QW + q, B, lq, lane, qf[q]);
   float sc[QW];
+  uint32_t smax[QW];   // running superblock key (bm != nullptr)
 #pragma unroll
-  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f, smax[q] = 0u;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the query fragments: out of the ring's count
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) issue_next();
@@ -1346,8 +1347,130 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
           uint32_t u = lane < cnt ? f2u(sc[q]) : 0u;
 #pragma unroll
           for (int off = 1; off < 64; off <<= 1) u = max(u, (uint32_t)__shfl_xor((int)u, off));
-          if (lane == 0 && qi < B) bm[(size_t)qi * bm_ld + ((d_begin + i0) >> 6)] = u;
+          const int64_t gi = (d_begin + i0) >> 6;   // this 64-doc block; chunks are whole superblocks
+          smax[q] = max(smax[q], u);
+          if (lane == 0 && qi < B) bm[(size_t)qi * bm_ld + gi] = u;
+          if ((gi & 3) == 3 || i == nd - 1) {
+            if (lane == 0 && qi < B) sb[(size_t)qi * sb_ld + (gi >> 2)] = smax[q];
+            smax[q] = 0u;
+          }
         }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Paired streaming scan (mid batches, B = 3..8; lab variants 22-24): the B <= 2
+// streaming scan's LDS-DMA ring, SHARED by the 2 waves of a 128-thread
+// workgroup, each wave scoring its own QW queries on every tile -- so the
+// corpus is streamed once per 2*QW queries while the SIMD interleaves two
+// waves' MFMA chains (one wave per SIMD with all of a mid batch's queries
+// cannot hide them: lab variants 18/19).  Both waves walk the same (doc,
+// tile) sequence; wave h fetches pieces 2h, 2h + 1 of each tile (rows 8h ..
+// 8h + 7), waits for its own pieces, and an s_barrier publishes the whole tile
+// to both.  Tile k lives in slot k % SLOTS; after the barrier of tile t both
+// waves have finished reading tile t - 1 (each reads a tile completely before
+// computing it), so tile t + SLOTS - 1 is issued into that slot.  Same tiles,
+// masks, max order and epilogue as the streaming scan: bit-identical scores.
+// Four such workgroups per CU (32 KiB of LDS each) = 2 waves per SIMD.
+template <int QW, int AUX, int SLOTS = kStreamSlots>
+__global__ __launch_bounds__(128, 2) void maxsim_scan_pair_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
+    const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
+    int ld) {
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[SLOTS * 4096];
+  const int lane = threadIdx.x & 63;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  constexpr int QPB = 2 * QW;
+  const int nq_groups = (B + QPB - 1) / QPB;
+  const int qg = (int)(blockIdx.x % nq_groups);
+  const int64_t chunk = blockIdx.x / nq_groups;
+  const int64_t d_begin = chunk * chunk_docs;
+  const int64_t d_end = (d_begin + chunk_docs < n) ? d_begin + chunk_docs : n;
+  if (d_begin >= d_end) return;  // workgroup-uniform
+  const int nd = (int)(d_end - d_begin);
+  const size_t doc_bytes = (size_t)ld * kRowBytes;
+  const int32_t* dls = doclens + d_begin;
+  auto ntiles = [&](int d) -> int {
+    int dl = sload_len(dls + d);
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    return (dl + 15) >> 4;
+  };
+  uint32_t src_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int t = 4 * (2 * h + j) + g;
+    src_off[j] = (uint32_t)(t * kRowBytes + 16 * (c ^ swz16(t)));
+  }
+  int idoc = 0;
+  int itile = 0, intl = ntiles(0);
+  while (intl == 0 && ++idoc < nd) intl = ntiles(idoc);
+  int issued = 0;
+  const uint8_t* tbase = tokens + (size_t)d_begin * doc_bytes;
+  auto issue_next = [&]() {
+    if (idoc >= nd) return;
+    const uint8_t* base = tbase + (size_t)idoc * doc_bytes + (size_t)itile * 16 * kRowBytes;
+    uint8_t* dst = ring + (issued % SLOTS) * 4096;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + src_off[j]), (lds_void_t*)(dst + (2 * h + j) * 1024), 16,
+                                       0, AUX);
+    ++issued;
+    if (++itile >= intl) {
+      itile = 0;
+      intl = 0;
+      while (intl == 0 && ++idoc < nd) intl = ntiles(idoc);
+    }
+  };
+  bf16x8 qf[QW][2][4];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QPB + h * QW + q, B, lq, lane, qf[q]);
+  float sc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) sc[q] = 0.0f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the query fragments: out of the ring's count
+#pragma unroll
+  for (int k = 0; k < SLOTS - 1; ++k) issue_next();
+  int consumed = 0;
+  for (int i = 0; i < nd; ++i) {
+    int dl = sload_len(dls + i);
+    dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    const int nt = (dl + 15) >> 4;
+    float m[QW][2];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
+    for (int t = 0; t < nt; ++t) {
+      // SLOTS - 1 tiles in flight: this tile's 2 pieces are the oldest
+      if (issued - consumed >= SLOTS - 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (SLOTS - 2)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();   // both waves' pieces of the tile have landed
+      bf16x8 a[4];
+      const uint8_t* row = ring + (consumed % SLOTS) * 4096 + c * kRowBytes;
+      const int sw = swz16(c);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) a[s4] = *reinterpret_cast<const bf16x8*>(row + 16 * ((4 * g + s4) ^ sw));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ++consumed;
+      issue_next();   // into the slot of tile consumed - 2, read by both waves before this barrier
+      const f32x4 init = (dl >= 16 * t + 16) ? f32x4{} : row_mask_init16(16 * t + 4 * g, dl);
+      tile16<QW>(a, qf, init, m);
+    }
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float v = reduce16(m[q][0], m[q][1], lane, lq);
+      sc[q] = (lane == (i & 63)) ? v : sc[q];
+    }
+    if ((i & 63) == 63 || i == nd - 1) {
+      const int i0 = i & ~63;
+      const int cnt = i - i0 + 1;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const int qi = qg * QPB + h * QW + q;
+        if (qi < B && lane < cnt) out[(size_t)qi * ld_out + d_begin + i0 + lane] = sc[q];
       }
     }
   }
@@ -2597,17 +2720,29 @@ __global__ __launch_bounds__(kTkThreads) void topk_select_kernel(const float* __
 // ---------------------------------------------------------------------------
 constexpr int kBmCand = 4096;          // gathered ranking keys (32 KiB)
 constexpr int kBmQual = 2048;          // qualifying blocks
-constexpr int kBmMaxBlocks = 24576;    // block keys in LDS (96 KiB): rows of n <= 1,572,864
+constexpr int kBmMaxBlocks = 24576;    // rows of n <= 1,572,864 (superblock keys in LDS: 24 KiB)
 constexpr int kBmRankMax = 512;        // gathered keys ranked by counting (else bitonic)
 constexpr size_t kBmFixedLds = kBmCand * 8 + 2048 * 4 + kBmQual * 4 + 64;
 inline int64_t bm_blocks(int64_t n) { return (n + 63) >> 6; }   // 64-doc blocks of a row
+inline int64_t bm_supers(int64_t n) { return (n + 255) >> 8; }  // 256-doc superblocks (4 blocks) of a row
+// Workspace of the block-max top-k: block keys [B][nb], then superblock keys [B][ns].
+inline uint32_t* bm_super_keys(uint32_t* bm, int32_t B, int64_t n) { return bm + (size_t)B * bm_blocks(n); }
 
 // 16 lanes per 64-doc block (a float4 each), 4 blocks per wave-load, 4 loads
 // in flight per lane: a wave covers 16 blocks, a workgroup 64.  Rows that do
 // not start 16-B aligned (n % 4 != 0) load their floats one by one.
+// sb (superblock keys, row stride sb_ld): the max of each 4 consecutive block
+// keys = one 256-doc superblock (a wave's 4 rows of one load step).
+__device__ __forceinline__ uint32_t umax_over_rows(uint32_t v) {   // max over lanes l, l^16, l^32, l^48
+  auto t = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = max(t[0], t[1]);
+  t = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return max(t[0], t[1]);
+}
 constexpr int kBmBlocksPerWg = 64;
 __global__ __launch_bounds__(256) void block_max_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
-                                                        uint32_t* __restrict__ bm, int64_t bm_ld) {
+                                                        uint32_t* __restrict__ bm, int64_t bm_ld,
+                                                        uint32_t* __restrict__ sb, int64_t sb_ld) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.y;
   const int64_t nb = (n + 63) >> 6;
@@ -2641,35 +2776,42 @@ __global__ __launch_bounds__(256) void block_max_kernel(const float* __restrict_
     v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
     const int64_t blk = b0 + 4 * u + r;
     if (c == 0 && blk < nb) bm[(size_t)row * bm_ld + blk] = v;
+    const uint32_t s4 = umax_over_rows(v);   // blocks b0 + 4u .. + 3 (b0 is a multiple of 16)
+    if (lane == 0 && b0 + 4 * u < nb) sb[(size_t)row * sb_ld + (b0 >> 2) + u] = s4;
   }
 }
 
 __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
                                                                int k, int64_t id_base, const uint32_t* __restrict__ bm,
-                                                               int64_t bm_ld, float* __restrict__ out_s,
+                                                               int64_t bm_ld, const uint32_t* __restrict__ sb,
+                                                               int64_t sb_ld, float* __restrict__ out_s,
                                                                int32_t* __restrict__ out_i) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   uint64_t* const sel = reinterpret_cast<uint64_t*>(bm_dyn);   // [kBmCand]
   uint32_t* const hist = reinterpret_cast<uint32_t*>(sel + kBmCand);   // [2048]
   uint32_t* const qual = hist + 2048;                              // [kBmQual]
   uint32_t* const misc = qual + kBmQual;                           // [16]
-  uint32_t* const keys = misc + 16;                                // [nb]
+  uint32_t* const keys = misc + 16;                                // [ns] superblock keys
   const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6;
   const int row = blockIdx.x;
   const int nb = (int)((n + 63) >> 6);
+  const int ns = (int)((n + 255) >> 8);
   const float* x = scores + (size_t)row * ld;
   const uint32_t* brow = bm + (size_t)row * bm_ld;
+  const uint32_t* srow = sb + (size_t)row * sb_ld;
   const int kk = (int)((int64_t)k < n ? k : n);
-  for (int i = tid; i < nb; i += nth) keys[i] = brow[i];
+  for (int i = tid; i < ns; i += nth) keys[i] = srow[i];
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
-  // 1. t = the kk-th largest block key, to its top 22 bits (two 11-bit digits)
-  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < nb ? kk : nb);
+  // 1. t = the kk-th largest SUPERBLOCK key, to its top 22 bits (two 11-bit
+  //    digits): kk superblocks have a max >= t, so the kk-th largest score is
+  //    >= t, and every doc >= t lies in a 64-doc block whose key is >= t
+  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < ns ? kk : ns);
   for (int p = 0; p < 2; ++p) {
     const int shift = 21 - 11 * p;
     for (int b = tid; b < 2048; b += nth) hist[b] = 0;
     __syncthreads();
-    for (int i = tid; i < nb; i += nth) {
+    for (int i = tid; i < ns; i += nth) {
       const uint32_t u = keys[i];
       hist_add(hist, (u >> shift) & 2047u, (u & mask) == prefix);
     }
@@ -2682,12 +2824,14 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
     __syncthreads();
   }
   const uint32_t t = prefix;
-  // 2. the blocks whose max reaches t, then their docs >= t
-  for (int i = tid; i < nb; i += nth)
-    if (keys[i] >= t) {
+  // 2. the 64-doc blocks (of the superblocks >= t) whose max reaches t, then their docs >= t
+  for (int i = tid; i < 4 * ns; i += nth) {
+    const int sbk = i >> 2, j = i;
+    if (j < nb && keys[sbk] >= t && brow[j] >= t) {
       const uint32_t pos = atomicAdd(&misc[0], 1u);
-      if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)i;
+      if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)j;
     }
+  }
   __syncthreads();
   const uint32_t nqual = misc[0];
   if (nqual <= (uint32_t)kBmQual) {
@@ -3332,6 +3476,50 @@ __global__ __launch_bounds__(256, 2) void rescore_split_kernel(
   }
 }
 
+// The faithful search's full-scan fallback in ONE launch (rows whose band
+// overflowed its capacity, status < 0; every other row's workgroups exit at
+// once): the rows' faithful scores of every doc into T (rescore_split_kernel's
+// pairs), then the LAST workgroup of a row to finish -- a per-row counter
+// (done[b], reset by the query split), agent-scope fences around it -- runs
+// the exact top-k of the row (topk_exact_row + the bitonic sort, as
+// topk_rows_kernel, with 256 threads).  k <= kTopkMax.
+template <bool LONG = false>
+__global__ __launch_bounds__(256, 2) void fallback_split_kernel(
+    const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
+    int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
+    float* __restrict__ T, const int32_t* __restrict__ status, int ld, int32_t* __restrict__ done, int k,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i) {
+  __shared__ float s_m[4][32];
+  __shared__ uint64_t sel[kTopkMax];
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+  __shared__ int s_last;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  if (status[b] >= 0) return;   // block-uniform: the band held the row's top-k
+  bf16x8 qh[2][4], ql[2][4];
+  load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+  load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+  const int lmax = LONG ? ld : kLd;
+  float* row = T + (size_t)b * n;
+  for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {   // block-uniform
+    int dl = doclens[c];
+    dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
+    const float v = faithful_doc_split<LONG>(hi, lo, c, ld, dl, qh, ql, lane, wave, lq, s_m);
+    if (threadIdx.x == 0) row[c] = v;
+  }
+  __threadfence();   // this workgroup's scores, visible device-wide before it is counted
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(done + b, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();   // every workgroup's scores of the row are in
+  const int kk = (int)((int64_t)k < n ? k : n);
+  topk_exact_row(row, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
+  sort_and_write(sel, kk, k, id_base, out_s + (size_t)b * k, out_i + (size_t)b * k);
+}
+
 // ---------------------------------------------------------------------------
 // Doc-major band rescoring.  The bands of a batch overlap (at B=256, 1M docs,
 // ~6.1k band docs per query: 1.56M (query, doc) pairs over ~0.8M distinct
@@ -3527,6 +3715,69 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
   }
 }
 
+// Doc-major band rescoring with the doc split over the workgroup (128-slot
+// docs, CBV2_OPT_BAND_DOC_MAJOR = 3): one band doc per workgroup, wave w
+// holding row tiles 2w, 2w + 1 of hi and lo in VGPRs for all of the doc's
+// pairs; per pair the query's split fragments (L2-resident) and the
+// faithful_doc_split reduction (column maxima -> LDS -> max of 4 -> sum):
+// the same bits as every other faithful rescoring.  ~160 VGPRs (3 waves per
+// SIMD) where the one-wave-per-doc kernel holds a whole half doc (1 per SIMD).
+__global__ __launch_bounds__(256, 2) void rescore_docs_split_kernel(
+    const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens,
+    const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int B, int lq,
+    const int32_t* __restrict__ act, const int32_t* __restrict__ act_off, const int32_t* __restrict__ act_cnt,
+    const int32_t* __restrict__ ctr, const int32_t* __restrict__ pair_b, const int32_t* __restrict__ pair_c,
+    float* __restrict__ F, int cap) {
+  __shared__ float s_m[4][32];
+  const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n_act = ctr[1];
+  for (int a = blockIdx.x; a < n_act; a += gridDim.x) {   // one doc per workgroup (block-uniform)
+    const int64_t d = act[a];
+    const int o = act_off[a], cnt = act_cnt[a];
+    int dl = doclens[d];
+    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
+    const size_t at = (size_t)d * kLd * kRowBytes;
+    bf16x8 ah[2][4], al[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int rt = 2 * wave + t;
+      if (16 * rt < dl) {
+        gbl_afrag16(hi + at, rt, lane, ah[t]);
+        gbl_afrag16(lo + at, rt, lane, al[t]);
+      }
+    }
+    for (int p = 0; p < cnt; ++p) {
+      const int b = pair_b[o + p];
+      bf16x8 qh[2][4], ql[2][4];
+      load_qfrag16(qhi, b, B, lq, lane, qh);
+      load_qfrag16(qlo, b, B, lq, lane, ql);
+      float m[2] = {neg_inf(), neg_inf()};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int rt = 2 * wave + t;
+        if (16 * rt < dl) {
+          const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
+          tile16_x3(ah[t], al[t], qh, ql, init, m);
+        }
+      }
+      const float w0 = fold16_max(fold32_max(m[0])), w1 = fold16_max(fold32_max(m[1]));
+      if (lane < 16) {
+        s_m[wave][lane] = w0;
+        s_m[wave][16 + lane] = w1;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        const float m0 = fmaxf(fmaxf(s_m[0][c16], s_m[1][c16]), fmaxf(s_m[2][c16], s_m[3][c16]));
+        const float m1 = fmaxf(fmaxf(s_m[0][16 + c16], s_m[1][16 + c16]), fmaxf(s_m[2][16 + c16], s_m[3][16 + c16]));
+        const float v = dpp_row_sum16((c16 < lq ? m0 : 0.0f) + (16 + c16 < lq ? m1 : 0.0f));
+        if (lane == 0) F[(size_t)b * cap + pair_c[o + p]] = v;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // The band's threshold for row b: the exact lower bound of the k-th faithful
 // score minus beta(b) -- from the caller (lb, floats: the sharded path's
 // global bound) or from the atomic-min of the bf16 top-k's faithful scores
@@ -3706,7 +3957,8 @@ __global__ __launch_bounds__(kTkThreads) void union_kth_kernel(const float* __re
 // status[b] = band size when certified, -1 when the band overflowed cap.
 constexpr int kBandCapMax = 16384;
 constexpr int kBandPairMaxB = 8;       // batches up to this rescore the band pair by pair (search_f32_phase2)
-constexpr int kBandSelMax = 512;       // keys ranked by counting (the band, or its keys reaching the k-th score)
+constexpr int kBandSelMax = 512;       // keys ranked by counting after the radix select (those reaching the k-th score)
+constexpr int kBandCountMax = 2048;    // a band of at most this many keys is ranked by counting directly
 __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __restrict__ F,
                                                                  const int32_t* __restrict__ cand,
                                                                  const int32_t* __restrict__ count, int cap, int k,
@@ -3728,7 +3980,7 @@ __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __
   int32_t* oi = out_i + (size_t)b * k;
   const uint64_t* src = keys;
   int m = cnt;
-  if (cnt > kBandSelMax) {
+  if (cnt > kBandCountMax) {
     // the kk-th largest score (the keys' top 32 bits) by radix select over
     // 11/11/10-bit digits, then the keys that reach it (the top-kk and its
     // score ties) into sel
@@ -3760,7 +4012,7 @@ __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __
     m = (int)misc[0];
     src = sel;
   }
-  if (m <= kBandSelMax) {   // keys are unique (distinct docs): rank = #greater, the sort's order
+  if (src == keys ? m <= kBandCountMax : m <= kBandSelMax) {   // keys are unique (distinct docs): rank = #greater
     for (int i = tid; i < m; i += nth) {
       const uint64_t key = src[i];
       int r = 0;
@@ -3951,7 +4203,11 @@ struct cbv2_index {
   int topk_bmax = 1;         // CBV2_OPT_TOPK_BMAX (1: block-max top-k where eligible, 0: sampled filter + select)
   int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
   bool band_lower_bound = true;  // CBV2_OPT_BAND_LOWER_BOUND
-  bool band_fused = true;        // CBV2_OPT_BAND_FUSED (B <= 8: collect + rescore in one launch)
+  // CBV2_OPT_BAND_FUSED (B <= 8: collect + rescore in one launch): off -- the
+  // band collect (7.4 us) + the split rescoring (one band doc per workgroup)
+  // beat the fused launch (39 us at 1M docs, B=1: its workgroups score their
+  // few hits one after another; profiles/r04d_*)
+  bool band_fused = false;
   bool rescore_split = true;     // CBV2_OPT_RESCORE_SPLIT (one pair per workgroup, rows over 4 waves)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
@@ -4060,7 +4316,8 @@ enum ScanVariant {
   kScan16W4Q8 = 5, kScan16W8Q2 = 6, kScan16W8Q3 = 7, kScan16W4Q2 = 8,
   kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
   kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17, kScanStreamQ4 = 18,
-  kScanStreamQ8 = 19, kScanStreamQ1Tw2 = 20, kScanStreamQ2Tw2 = 21,
+  kScanStreamQ8 = 19, kScanStreamQ1Tw2 = 20, kScanStreamQ2Tw2 = 21, kScanPairQ1 = 22, kScanPairQ2 = 23,
+  kScanPairQ4 = 24,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -4287,8 +4544,27 @@ int launch_direct(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
 // Streaming scans (variants 14-16; 14 / 15 are the B = 1 / 2 production
 // scans of every bf16 index, long documents included): one 4-wave workgroup
 // per CU (128 KiB of LDS rings), chunks for kDirectOversub x the resident waves.
-// bm (nullable): fold the block maxima into the scan (chunks rounded up to a
-// multiple of the 64-doc block; row stride bm_blocks(n)).
+// The paired streaming scan (lab variants 22-24): 4 two-wave workgroups per CU
+// (2 waves per SIMD), chunks for kDirectOversub x the resident workgroups.
+template <int QW>
+int launch_pair(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st) {
+  if (ix->dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "pair scan: bf16 index only");
+  const int nq_groups = (B + 2 * QW - 1) / (2 * QW);
+  const int64_t target_wgs = 4LL * cu_count(ix->device) * kDirectOversub;
+  int64_t n_chunks = target_wgs / nq_groups;
+  if (n_chunks > ix->n) n_chunks = ix->n;
+  if (n_chunks < 1) n_chunks = 1;
+  const int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
+  n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
+  const int64_t grid = (int64_t)nq_groups * n_chunks;
+  if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
+  hipLaunchKernelGGL((maxsim_scan_pair_kernel<QW, 2>), dim3((unsigned)grid), dim3(128), 0, st, ix->tokens,
+                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld);
+  return launch_check("maxsim_scan_pair_kernel");
+}
+
+// bm (nullable): fold the block and superblock maxima into the scan (chunks
+// rounded up to whole 256-doc superblocks; layout of bm_ws_bytes).
 template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
 int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                   uint32_t* bm = nullptr) {
@@ -4299,13 +4575,14 @@ int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
   if (n_chunks > ix->n) n_chunks = ix->n;
   if (n_chunks < 1) n_chunks = 1;
   int64_t chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
-  if (bm != nullptr) chunk_docs = (chunk_docs + 63) & ~(int64_t)63;
+  if (bm != nullptr) chunk_docs = (chunk_docs + 255) & ~(int64_t)255;   // whole superblocks
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
   hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS, TW2>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
                      ix->tokens,
-                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld, bm, bm_blocks(ix->n));
+                     ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld, bm, bm_blocks(ix->n),
+                     bm ? bm_super_keys(bm, B, ix->n) : nullptr, bm_supers(ix->n));
   return launch_check("maxsim_scan_stream_kernel");
 }
 
@@ -4381,6 +4658,12 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_stream<1, 2, 4, kStreamSlots, true>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ2Tw2:
       return launch_stream<2, 2, 4, kStreamSlots, true>(ix, Q, B, lq, out, ld_out, st);
+    case kScanPairQ1:       // lab: two waves sharing one tile ring, 1 / 2 / 4 queries each
+      return launch_pair<1>(ix, Q, B, lq, out, ld_out, st);
+    case kScanPairQ2:
+      return launch_pair<2>(ix, Q, B, lq, out, ld_out, st);
+    case kScanPairQ4:
+      return launch_pair<4>(ix, Q, B, lq, out, ld_out, st);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
@@ -4631,7 +4914,9 @@ bool bmax_eligible(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) {
   return ix->topk_bmax != 0 && scorer == CBV2_SCORER_MAXSIM && ix->ld == kLd && ix->n >= kSampledMinN &&
          bm_blocks(ix->n) <= kBmMaxBlocks && k <= kTopkMax && B <= 65535 && fused_slots(ix, scorer, B, k) == 0;
 }
-size_t bm_ws_bytes(int32_t B, int64_t n) { return ((size_t)B * (size_t)bm_blocks(n) * 4 + 255) & ~(size_t)255; }
+size_t bm_ws_bytes(int32_t B, int64_t n) {
+  return ((size_t)B * (size_t)(bm_blocks(n) + bm_supers(n)) * 4 + 255) & ~(size_t)255;
+}
 
 // blocks_ready: bm already holds the block maxima (folded into the scan)
 int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, uint32_t* bm,
@@ -4639,18 +4924,19 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   static std::atomic<bool> attr_set[64] = {};
   if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
     CBV2_HIP(hipFuncSetAttribute((const void*)topk_bmax_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)(kBmFixedLds + (size_t)kBmMaxBlocks * 4)));
+                                 (int)(kBmFixedLds + (size_t)(kBmMaxBlocks / 4) * 4)));
     if (dev >= 0 && dev < 64) attr_set[dev].store(true, std::memory_order_relaxed);
   }
-  const int64_t nb = bm_blocks(n);
+  const int64_t nb = bm_blocks(n), ns = bm_supers(n);
+  uint32_t* sb = bm_super_keys(bm, B, n);
   if (!blocks_ready) {
     hipLaunchKernelGGL(block_max_kernel, dim3((unsigned)((nb + kBmBlocksPerWg - 1) / kBmBlocksPerWg), (unsigned)B),
-                       dim3(256), 0, st, scores, n, ld, bm, nb);
+                       dim3(256), 0, st, scores, n, ld, bm, nb, sb, ns);
     if (int rc = launch_check("block_max_kernel")) return rc;
   }
-  const size_t lds = kBmFixedLds + (size_t)nb * 4;
+  const size_t lds = kBmFixedLds + (size_t)ns * 4;
   hipLaunchKernelGGL(topk_bmax_kernel, dim3((unsigned)B), dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm,
-                     bm_blocks(n), out_s, out_i);
+                     nb, sb, ns, out_s, out_i);
   return launch_check("topk_bmax_kernel");
 }
 
@@ -5445,12 +5731,19 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
     hipLaunchKernelGGL(band_scatter_kernel, dim3(gc, (unsigned)B), dim3(256), 0, st, w.cand, w.count, cap,
                        ix->id_base, ix->n, w.dcnt, w.doff, w.pair_b, w.pair_c);
     if ((rc = launch_check("band_scatter_kernel"))) return rc;
-    const unsigned gr = (unsigned)(2 * cu_count(ix->device) * 4);   // 4 waves each; grid-stride over docs
-    auto kern = ix->band_doc_major == 2 ? (ix->ld != kLd ? rescore_docs_kernel<true, true> : rescore_docs_kernel<true>)
-                                        : (ix->ld != kLd ? rescore_docs_kernel<false, true> : rescore_docs_kernel<false>);
-    hipLaunchKernelGGL(kern, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, w.qhi, w.qlo, B, lq,
-                       w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap, (int)ix->ld);
-    if ((rc = launch_check("rescore_docs_kernel"))) return rc;
+    if (ix->band_doc_major == 3 && ix->ld == kLd) {   // the doc split over the workgroup
+      const unsigned gs = (unsigned)(3 * cu_count(ix->device) * 4);   // ~3 workgroups per CU resident, x4
+      hipLaunchKernelGGL(rescore_docs_split_kernel, dim3(gs), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
+                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
+      if ((rc = launch_check("rescore_docs_split_kernel"))) return rc;
+    } else {
+      const unsigned gr = (unsigned)(2 * cu_count(ix->device) * 4);   // 4 waves each; grid-stride over docs
+      auto kern = ix->band_doc_major == 2 ? (ix->ld != kLd ? rescore_docs_kernel<true, true> : rescore_docs_kernel<true>)
+                                          : (ix->ld != kLd ? rescore_docs_kernel<false, true> : rescore_docs_kernel<false>);
+      hipLaunchKernelGGL(kern, dim3(gr), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, w.qhi, w.qlo, B, lq,
+                         w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap, (int)ix->ld);
+      if ((rc = launch_check("rescore_docs_kernel"))) return rc;
+    }
   } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
                                    B <= kBandPairMaxB ? 1 : 0))) {
     return rc;
@@ -5460,6 +5753,13 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
   if ((rc = launch_check("band_select_kernel"))) return rc;
   // rows whose band overflowed cap (status -1): the full faithful scan over
   // every doc and an exact top-k, on the device (other rows exit at once)
+  if (ix->rescore_split && k <= kTopkMax) {   // scan + top-k in one launch (last workgroup per row)
+    const unsigned gx = (unsigned)(ix->n < kRsSplitGrid ? ix->n : kRsSplitGrid);
+    hipLaunchKernelGGL(ix->ld != kLd ? fallback_split_kernel<true> : fallback_split_kernel<false>, dim3(gx, (unsigned)B),
+                       dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w.qhi, w.qlo, lq,
+                       w.T, out_status, (int)ix->ld, w.done, k, out_scores, out_ids);
+    return launch_check("fallback_split_kernel");
+  }
   if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st, out_status))) return rc;
   if (k > kTopkMax)
     return topk_multi(w.T, B, ix->n, ix->n, k, ix->id_base, nullptr, 0, out_scores, out_ids, nullptr, st, out_status);

@@ -153,17 +153,18 @@ def test_faithful_shards_merge_equal_unsharded(dev):
     assert torch.equal(mi, fi) and torch.equal(ms, fs)
 
 
-@pytest.mark.parametrize("N,dups", [(6000, 1), (3000, 9)])
-def test_band_doc_major_equals_pair_major(dev, N, dups):
+@pytest.mark.parametrize("N,dups,mode", [(6000, 1, 1), (3000, 9, 1), (6000, 1, 3), (3000, 9, 3)])
+def test_band_doc_major_equals_pair_major(dev, N, dups, mode):
     """Doc-major band rescoring (pairs grouped by doc, each band doc's tiles
     read once per batch; batches of more than 8 queries) returns the
     pair-by-pair rescoring's results bit for bit.  dups > 1 repeats queries,
     so every band doc has > 4 pairs (several passes of one wave over the
-    doc)."""
+    doc).  mode 3: the doc split over the workgroup (rescore_docs_split_kernel)."""
     docs, doclens, Q = make_case(N + dups, N, 12, 32)
     if dups > 1:
         Q = torch.cat([Q[:1].expand(dups, -1, -1), Q[1:]]).contiguous()
     ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=5)
+    ix.set_option(_lib.OPT_BAND_DOC_MAJOR, mode)
     s1, i1 = ix.search(Q.to(dev), 100)
     b1 = ix.last_band.clone()
     ix.set_option(_lib.OPT_BAND_DOC_MAJOR, 0)

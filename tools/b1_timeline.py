@@ -55,8 +55,9 @@ def run(a):
         torch.cuda.synchronize()
         if it >= 5:
             lat.append((time.perf_counter() - t) * 1e3)
+    from hybrid_rag_colbertv2_amd.index import hbm_placement
     print(json.dumps({"docs": n, "dtype": a.dtype, "iters": a.iters, "p50_ms": round(statistics.median(lat), 4),
-                      "min_ms": round(min(lat), 4)}), flush=True)
+                      "min_ms": round(min(lat), 4), "placement": hbm_placement(ix.tokens)}), flush=True)
 
 
 def short(name):
