@@ -3155,6 +3155,59 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_raw_kernel(
   if (lane == 0) raw[(size_t)b * C + c] = v;
 }
 
+// bf16 rerank of small batches with one (query, candidate) per WORKGROUP: the
+// doc's 128-token blocks split over the 4 waves (wave w: row tiles 2w, 2w + 1),
+// each wave's column maxima max'ed in LDS and summed by wave 0 as reduce16
+// does -- max is exact, so the bits equal rerank_one_bf16's (one wave walking
+// all 8 tiles), at one 8 KiB HBM round trip per wave instead of 32 KiB.
+__global__ __launch_bounds__(256, 2) void rerank_split_kernel(
+    const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
+    const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, float* __restrict__ raw, int ld) {
+  __shared__ float s_m[4][32];
+  const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y, c = blockIdx.x;
+  const int32_t id = cand[(size_t)b * C + c];
+  const int64_t loc = (int64_t)id - id_base;
+  if (id < 0 || loc < 0 || loc >= n) {   // block-uniform
+    if (threadIdx.x == 0) raw[(size_t)b * C + c] = neg_inf();
+    return;
+  }
+  bf16x8 qf[1][2][4];
+  load_qfrag16(Q, b, b + 1, lq, lane, qf[0]);
+  int dl = doclens[loc];
+  float m[1][2] = {{neg_inf(), neg_inf()}};
+  for (int blk = 0; blk == 0 || kLd * blk < dl; ++blk) {
+    const uint8_t* dbase = tokens + (size_t)loc * (size_t)ld * kRowBytes + (size_t)blk * kDocBytes;
+    bf16x8 af[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)   // the first block's loads do not wait for the doc length
+      if (blk == 0 || 16 * (2 * wave + t) < dl - kLd * blk) gbl_afrag16(dbase, 2 * wave + t, lane, af[t]);
+    if (blk == 0) dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
+    const int dlb = dl - kLd * blk;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int rt = 2 * wave + t;
+      if (16 * rt < dlb) {
+        const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
+        tile16<1>(af[t], qf, init, m);
+      }
+    }
+  }
+  const float w0 = fold16_max(fold32_max(m[0][0])), w1 = fold16_max(fold32_max(m[0][1]));
+  if (lane < 16) {
+    s_m[wave][lane] = w0;
+    s_m[wave][16 + lane] = w1;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const float m0 = fmaxf(fmaxf(s_m[0][c16], s_m[1][c16]), fmaxf(s_m[2][c16], s_m[3][c16]));
+    const float m1 = fmaxf(fmaxf(s_m[0][16 + c16], s_m[1][16 + c16]), fmaxf(s_m[2][16 + c16], s_m[3][16 + c16]));
+    const float v = dpp_row_sum16((c16 < lq ? m0 : 0.0f) + (16 + c16 < lq ? m1 : 0.0f));
+    if (lane == 0) raw[(size_t)b * C + c] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // fp32-faithful path (an index built from fp32 embeddings, as the reference
 // stores them: local_rag_complete.py:735-746).  Each fp32 token x is split
@@ -3393,6 +3446,8 @@ __global__ __launch_bounds__(256, 2) void rescore_x3_kernel(
 // The split pair's score (called by every thread of the workgroup; the result
 // is valid in wave 0): waves' row maxima -> column maxima -> LDS -> max of
 // the 4 -> reduce16's sum.
+// dl: the doc's raw doclens entry (clamped here, after the first block's
+// tile loads are issued: those do not wait for it).
 template <bool LONG>
 __device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo,
                                                     int64_t loc, int ld, int dl, const bf16x8 (&qh)[2][4],
@@ -3402,17 +3457,20 @@ __device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ 
   const int lmax = LONG ? ld : kLd;
   float m[2] = {neg_inf(), neg_inf()};
   for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {
-    const int dlb = dl - kLd * blk;
     const size_t at = ((size_t)loc * lmax + (size_t)kLd * blk) * kRowBytes;
     bf16x8 ah[2][4], al[2][4];
+    // the first block's tiles are loaded whatever the doc length (its slots
+    // exist; padding rows are loaded but never computed)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int rt = 2 * wave + t;
-      if (16 * rt < dlb) {
+      if (blk == 0 || 16 * rt < dl - kLd * blk) {
         gbl_afrag16(hi + at, rt, lane, ah[t]);
         gbl_afrag16(lo + at, rt, lane, al[t]);
       }
     }
+    if (blk == 0) dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
+    const int dlb = dl - kLd * blk;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int rt = 2 * wave + t;
@@ -3459,16 +3517,12 @@ __global__ __launch_bounds__(256, 2) void rescore_split_kernel(
   bf16x8 qh[2][4], ql[2][4];
   load_qfrag16(qhi, b, b + 1, lq, lane, qh);
   load_qfrag16(qlo, b, b + 1, lq, lane, ql);
-  const int lmax = LONG ? ld : kLd;
   for (int64_t c = blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
     const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
     const int64_t loc = id - id_base;
     float v = neg_inf();
-    if (id >= 0 && loc >= 0 && loc < n) {                    // block-uniform
-      int dl = doclens[loc];
-      dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
-      v = faithful_doc_split<LONG>(hi, lo, loc, ld, dl, qh, ql, lane, wave, lq, s_m);
-    }
+    if (id >= 0 && loc >= 0 && loc < n)                      // block-uniform
+      v = faithful_doc_split<LONG>(hi, lo, loc, ld, doclens[loc], qh, ql, lane, wave, lq, s_m);
     if (threadIdx.x == 0) {
       out[(size_t)b * ld_out + c] = v;
       if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
@@ -3501,12 +3555,9 @@ __global__ __launch_bounds__(256, 2) void fallback_split_kernel(
   bf16x8 qh[2][4], ql[2][4];
   load_qfrag16(qhi, b, b + 1, lq, lane, qh);
   load_qfrag16(qlo, b, b + 1, lq, lane, ql);
-  const int lmax = LONG ? ld : kLd;
   float* row = T + (size_t)b * n;
   for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {   // block-uniform
-    int dl = doclens[c];
-    dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
-    const float v = faithful_doc_split<LONG>(hi, lo, c, ld, dl, qh, ql, lane, wave, lq, s_m);
+    const float v = faithful_doc_split<LONG>(hi, lo, c, ld, doclens[c], qh, ql, lane, wave, lq, s_m);
     if (threadIdx.x == 0) row[c] = v;
   }
   __threadfence();   // this workgroup's scores, visible device-wide before it is counted
@@ -3909,9 +3960,7 @@ __global__ __launch_bounds__(256, 2) void band_collect_rescore_kernel(
   load_qfrag16(qlo, b, b + 1, lq, lane, ql);
   for (int j = 0; j < nl && base + j < cap; ++j) {   // block-uniform
     const int64_t loc = s_loc[j];
-    int dl = doclens[loc];
-    dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-    const float v = faithful_doc_split<false>(hi, lo, loc, kLd, dl, qh, ql, lane, wave, lq, s_m);
+    const float v = faithful_doc_split<false>(hi, lo, loc, kLd, doclens[loc], qh, ql, lane, wave, lq, s_m);
     if (threadIdx.x == 0) {
       cand[(size_t)b * cap + base + j] = (int32_t)(id_base + loc);
       F[(size_t)b * cap + base + j] = v;
@@ -3958,7 +4007,10 @@ __global__ __launch_bounds__(kTkThreads) void union_kth_kernel(const float* __re
 constexpr int kBandCapMax = 16384;
 constexpr int kBandPairMaxB = 8;       // batches up to this rescore the band pair by pair (search_f32_phase2)
 constexpr int kBandSelMax = 512;       // keys ranked by counting after the radix select (those reaching the k-th score)
-constexpr int kBandCountMax = 2048;    // a band of at most this many keys is ranked by counting directly
+// a band of at most this many keys is ranked by counting directly (each key
+// counted against every other from LDS: 107 us for an 880-key band at 1M docs,
+// B=1, vs 14 us through the radix select; profiles/r04e_*)
+constexpr int kBandCountMax = 128;
 __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __restrict__ F,
                                                                  const int32_t* __restrict__ cand,
                                                                  const int32_t* __restrict__ count, int cap, int k,
@@ -5530,7 +5582,11 @@ static int rerank_impl(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, con
   if (B <= kRrSplitMaxB && (k == 0 || (!big && ws != nullptr && ws_bytes >= raw_bytes))) {
     float* raw = k == 0 ? out_scores : (float*)ws;
     const dim3 grid((unsigned)((C + kRrWaves - 1) / kRrWaves), (unsigned)B);
-    if (f8)
+    if (!f8 && ix->rescore_split) {   // one candidate per workgroup, its rows over the 4 waves
+      hipLaunchKernelGGL(rerank_split_kernel, dim3((unsigned)C, (unsigned)B), dim3(256), 0, st, ix->tokens,
+                         ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, raw, (int)ix->ld);
+      if ((rc = launch_check("rerank_split_kernel"))) return rc;
+    } else if (f8)
       hipLaunchKernelGGL(rerank_raw_kernel<true>, grid, dim3(kRrWaves * 64), 0, st, ix->tokens, ix->scales,
                          ix->doclens, ix->n, ix->id_base, Qb, Qs, lq, cand, C, raw, (int)ix->ld);
     else

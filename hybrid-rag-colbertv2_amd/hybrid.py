@@ -391,8 +391,11 @@ class OneTripRetriever:
         self.device = index.device
         self._ws = None
         self._host = None
+        self._sized = None        # (B, lq, kb) -> (ws pointer, bytes): the sizes of the last call
 
     def _buffers(self, B: int, lq: int, kb: int):
+        if self._sized is not None and self._sized[0] == (B, lq, kb):
+            return self._sized[1]           # the latency path: no size queries per call
         L = _lib.lib()
         need = int(L.cbv2_retrieve_workspace_bytes(self.index._h, self.comm, B, lq, self.k, kb, self.C))
         if need == 0:
@@ -408,14 +411,20 @@ class OneTripRetriever:
                 torch.cuda.current_stream(self.device).synchronize()
             self._host = torch.empty((hneed,), dtype=torch.uint8, pin_memory=True)
         off = (-self._ws.data_ptr()) % 256                 # 256-B aligned start
-        return self._ws.data_ptr() + off, self._ws.numel() - off
+        out = (self._ws.data_ptr() + off, self._ws.numel() - off)
+        self._sized = ((B, lq, kb), out)
+        return out
 
     def __call__(self, Q: torch.Tensor, lexical=None):
         from .index import LQ_MAX, _stream_ptr
         L = _lib.lib()
         if Q.dim() == 3 and Q.shape[1] > LQ_MAX and self.comm is None:
             return self._stages(Q, lexical)     # long queries: the index sums blocks of <= 32 tokens
-        _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
+        if (Q.dim() == 3 and Q.is_contiguous() and Q.device == self.device and 1 <= Q.shape[1] <= LQ_MAX
+                and Q.shape[2] == 128 and Q.dtype == self._qdtype()):   # the index's query layout: no conversion
+            _keep, qptr, qdt, B, lq = Q, Q.data_ptr(), self._qabi, int(Q.shape[0]), int(Q.shape[1])
+        else:
+            _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
         kb_cap = self.lexical_k if callable(lexical) else (0 if lexical is None else int(np.shape(lexical)[1]))
         ws, wsb = self._buffers(B, lq, kb_cap)
         st = _stream_ptr(self.device)
@@ -444,6 +453,15 @@ class OneTripRetriever:
             self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
             out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), st))
         return out_s, out_i, out_p
+
+    def _qdtype(self):
+        """The torch dtype a query of this index is passed as without conversion
+        (None for MXFP8: quantised per call)."""
+        if getattr(self, "_qdt_cache", None) is None:
+            ix = self.index
+            self._qdt_cache = (torch.float32 if ix.faithful else None if ix.fp8 else torch.bfloat16,)
+            self._qabi = _lib.DTYPE_F32 if ix.faithful else _lib.DTYPE_BF16
+        return self._qdt_cache[0]
 
     def _stages(self, Q: torch.Tensor, lexical):
         """The same stages called one by one (queries of more than 32 tokens)."""

@@ -36,7 +36,7 @@ def run(a):
     del terms, off
     qt, qo = synth.bm25_queries(256)
     bm_one = lambda: lex.search(qt[:qo[1]], qo[:2], 100)   # noqa: E731
-    f32 = a.dtype == "fp32"
+    f32 = a.dtype in ("fp32", "both")
     tokens, doclens = synth.make_shard(0, n, Qf, planted, dev, seed=0,
                                        dtype=torch.float32 if f32 else torch.bfloat16)
     ix = (ColbertIndex.faithful_f32(tokens, doclens) if f32 else
@@ -44,20 +44,25 @@ def run(a):
     del tokens
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
-    Q1 = Qf[:1].to(dev, torch.float32 if f32 else torch.bfloat16).contiguous()
-    one = OneTripRetriever(ix)
-    lat = []
+    legs = {a.dtype if a.dtype != "both" else "fp32":
+            (OneTripRetriever(ix), Qf[:1].to(dev, torch.float32 if f32 else torch.bfloat16).contiguous())}
+    if a.dtype == "both":   # a bf16 handle over the faithful index's hi: the same memory, interleaved
+        legs["bf16"] = (OneTripRetriever(ColbertIndex(ix.tokens, ix.doclens)),
+                        Qf[:1].to(dev, torch.bfloat16).contiguous())
+    lat = {k: [] for k in legs}
     for it in range(a.iters + 5):
-        torch.cuda.synchronize()
-        time.sleep(0.002)          # the GPU idles between queries, as in the bench's latency loop
-        t = time.perf_counter()
-        one(Q1, bm_one)
-        torch.cuda.synchronize()
-        if it >= 5:
-            lat.append((time.perf_counter() - t) * 1e3)
+        for name, (one, Q1) in legs.items():
+            torch.cuda.synchronize()
+            time.sleep(0.002)          # the GPU idles between queries, as in the bench's latency loop
+            t = time.perf_counter()
+            one(Q1, bm_one)
+            torch.cuda.synchronize()
+            if it >= 5:
+                lat[name].append((time.perf_counter() - t) * 1e3)
     from hybrid_rag_colbertv2_amd.index import hbm_placement
-    print(json.dumps({"docs": n, "dtype": a.dtype, "iters": a.iters, "p50_ms": round(statistics.median(lat), 4),
-                      "min_ms": round(min(lat), 4), "placement": hbm_placement(ix.tokens)}), flush=True)
+    for name, v in lat.items():
+        print(json.dumps({"docs": n, "dtype": name, "iters": a.iters, "p50_ms": round(statistics.median(v), 4),
+                          "min_ms": round(min(v), 4), "placement": hbm_placement(ix.tokens)}), flush=True)
 
 
 def short(name):
@@ -84,7 +89,7 @@ def parse(d, scan_key):
         cur.append(e)
     if cur:
         groups.append(cur)
-    per = []
+    per_kind = {}
     for g in groups:
         if not any(scan_key in e[2] for e in g):
             continue
@@ -92,10 +97,17 @@ def parse(d, scan_key):
         for (a, b, nm) in g:
             rows.append((nm, (b - a) / 1e3, max(0, a - prev) / 1e3))
             prev = max(prev, b)
-        per.append((rows, (prev - g[0][0]) / 1e3))
-    if not per:
+        kind = "fp32-faithful" if any("split_query" in e[2] for e in g) else "bf16 / other"
+        per_kind.setdefault(kind, []).append((rows, (prev - g[0][0]) / 1e3))
+    if not per_kind:
         print("no iterations found")
         return
+    for kind, per in per_kind.items():
+        print(f"[{kind}]")
+        _fold(per, scan_key)
+
+
+def _fold(per, scan_key):
     L = statistics.mode(len(r) for r, _ in per)
     same = [p for p in per if len(p[0]) == L]
     print(f"{len(per)} iterations ({len(same)} with the modal {L} events); medians:")
@@ -118,7 +130,8 @@ def parse(d, scan_key):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=1_000_000)
-    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp8", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp8", "fp32", "both"],
+                    help="both: the faithful index and a bf16 handle over its hi, interleaved in one process")
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--parse", default=None, help="a rocprofv3 output directory to fold")
     ap.add_argument("--scan", default="maxsim_scan", help="substring naming the scan kernel")
