@@ -3292,8 +3292,9 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 // Query split: one wave per query, 4 rows at a time.  beta[b] bounds
 // |T - S| for every doc: sum_i ||q_i|| E + ||q_i - qhi_i|| M + slack (||q_i|| + ||q_i - qhi_i||) M
 // with E = max ||x - hi||, M = max ||hi|| of the index.  A search's split also
-// resets the row's band state (each nullable): count[b] = 0 (the band
-// collect's counter), lbu[b] = ~0 (the atomic-min of the bf16 top-k's
+// resets the row's band state (each nullable): count[b] = count0 (the band
+// collect's counter; k when the band's first k slots are the bf16 top-k
+// already rescored by phase 1), lbu[b] = ~0 (the atomic-min of the bf16 top-k's
 // faithful scores, order-preserving bits) and done[b] = 0 (the fallback's
 // finished-workgroup counter) -- one launch fewer than separate memsets.
 __global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict__ Q, int lq,
@@ -3301,7 +3302,7 @@ __global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict
                                                          float E, float M, float* __restrict__ beta,
                                                          int32_t* __restrict__ count = nullptr,
                                                          uint32_t* __restrict__ lbu = nullptr,
-                                                         int32_t* __restrict__ done = nullptr) {
+                                                         int32_t* __restrict__ done = nullptr, int count0 = 0) {
   const int b = blockIdx.x, lane = threadIdx.x, grp = lane >> 4, sub = lane & 15;
   float acc = 0.0f;
   for (int r = grp; r < lq; r += 4) {
@@ -3316,7 +3317,7 @@ __global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict
   for (int off = 16; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
   if (lane == 0) {
     beta[b] = acc * kBoundUp;
-    if (count != nullptr) count[b] = 0;
+    if (count != nullptr) count[b] = count0;
     if (lbu != nullptr) lbu[b] = 0xffffffffu;
     if (done != nullptr) done[b] = 0;
   }
@@ -3448,22 +3449,24 @@ __global__ __launch_bounds__(256, 2) void rescore_x3_kernel(
 // the 4 -> reduce16's sum.
 // dl: the doc's raw doclens entry (clamped here, after the first block's
 // tile loads are issued: those do not wait for it).
-template <bool LONG>
+// NW waves per doc (4: 2 row tiles each; 2: 4 row tiles each).
+template <bool LONG, int NW = 4>
 __device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo,
                                                     int64_t loc, int ld, int dl, const bf16x8 (&qh)[2][4],
                                                     const bf16x8 (&ql)[2][4], int lane, int wave, int lq,
                                                     float (&s_m)[4][32]) {
+  constexpr int TPW = 8 / NW;   // row tiles per wave
   const int g = lane >> 4, c16 = lane & 15;
   const int lmax = LONG ? ld : kLd;
   float m[2] = {neg_inf(), neg_inf()};
   for (int blk = 0; blk == 0 || (LONG && kLd * blk < dl); ++blk) {
     const size_t at = ((size_t)loc * lmax + (size_t)kLd * blk) * kRowBytes;
-    bf16x8 ah[2][4], al[2][4];
+    bf16x8 ah[TPW][4], al[TPW][4];
     // the first block's tiles are loaded whatever the doc length (its slots
     // exist; padding rows are loaded but never computed)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int rt = 2 * wave + t;
+    for (int t = 0; t < TPW; ++t) {
+      const int rt = TPW * wave + t;
       if (blk == 0 || 16 * rt < dl - kLd * blk) {
         gbl_afrag16(hi + at, rt, lane, ah[t]);
         gbl_afrag16(lo + at, rt, lane, al[t]);
@@ -3472,8 +3475,8 @@ __device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ 
     if (blk == 0) dl = dl < 0 ? 0 : (dl > lmax ? lmax : dl);
     const int dlb = dl - kLd * blk;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int rt = 2 * wave + t;
+    for (int t = 0; t < TPW; ++t) {
+      const int rt = TPW * wave + t;
       if (16 * rt < dlb) {
         const f32x4 init = (dlb >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dlb);
         tile16_x3(ah[t], al[t], qh, ql, init, m);
@@ -3488,21 +3491,25 @@ __device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ 
   __syncthreads();
   float v = 0.0f;
   if (wave == 0) {
-    const float m0 = fmaxf(fmaxf(s_m[0][c16], s_m[1][c16]), fmaxf(s_m[2][c16], s_m[3][c16]));
-    const float m1 = fmaxf(fmaxf(s_m[0][16 + c16], s_m[1][16 + c16]), fmaxf(s_m[2][16 + c16], s_m[3][16 + c16]));
+    float m0 = s_m[0][c16], m1 = s_m[0][16 + c16];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      m0 = fmaxf(m0, s_m[w][c16]);
+      m1 = fmaxf(m1, s_m[w][16 + c16]);
+    }
     v = dpp_row_sum16((c16 < lq ? m0 : 0.0f) + (16 + c16 < lq ? m1 : 0.0f));
   }
   __syncthreads();   // s_m is rewritten by the next pair
   return v;
 }
 
-template <bool LONG = false>
-__global__ __launch_bounds__(256, 2) void rescore_split_kernel(
+template <bool LONG = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
     float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld,
-    uint32_t* __restrict__ lb_min) {
+    uint32_t* __restrict__ lb_min, int64_t c0) {
   __shared__ float s_m[4][32];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -3513,16 +3520,16 @@ __global__ __launch_bounds__(256, 2) void rescore_split_kernel(
     const int64_t cb = count[b];
     lim = cb < lim ? cb : lim;
   }
-  if ((int64_t)blockIdx.x >= lim) return;  // block-uniform
+  if (c0 + (int64_t)blockIdx.x >= lim) return;  // block-uniform
   bf16x8 qh[2][4], ql[2][4];
   load_qfrag16(qhi, b, b + 1, lq, lane, qh);
   load_qfrag16(qlo, b, b + 1, lq, lane, ql);
-  for (int64_t c = blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
+  for (int64_t c = c0 + blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
     const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
     const int64_t loc = id - id_base;
     float v = neg_inf();
     if (id >= 0 && loc >= 0 && loc < n)                      // block-uniform
-      v = faithful_doc_split<LONG>(hi, lo, loc, ld, doclens[loc], qh, ql, lane, wave, lq, s_m);
+      v = faithful_doc_split<LONG, NW>(hi, lo, loc, ld, doclens[loc], qh, ql, lane, wave, lq, s_m);
     if (threadIdx.x == 0) {
       out[(size_t)b * ld_out + c] = v;
       if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
@@ -3573,9 +3580,9 @@ __global__ __launch_bounds__(256, 2) void fallback_split_kernel(
 
 // ---------------------------------------------------------------------------
 // Doc-major band rescoring.  The bands of a batch overlap (at B=256, 1M docs,
-// ~6.1k band docs per query: 1.56M (query, doc) pairs over ~0.8M distinct
-// docs), so rescoring pair by pair gathers most band docs' hi+lo (64 KiB)
-// twice.  Instead the pairs are grouped by doc (counting sort: per-doc counts,
+// ~0.9k band docs per query with the two-pass band: 0.23M (query, doc) pairs
+// over ~0.2M distinct docs), so rescoring pair by pair would gather the shared
+// band docs' hi+lo (64 KiB) more than once.  Instead the pairs are grouped by doc (counting sort: per-doc counts,
 // wave-aggregated segment offsets, scatter) and one wave rescored every pair
 // of a doc with the doc's tiles loaded once per half, the queries' fragments
 // (16 KiB each, L2-resident) streamed per pair.  Same arithmetic and max
@@ -3584,52 +3591,91 @@ __global__ __launch_bounds__(256, 2) void fallback_split_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void band_count_kernel(const int32_t* __restrict__ cand,
                                                          const int32_t* __restrict__ count, int cap,
-                                                         int64_t id_base, int64_t n, int32_t* __restrict__ dcnt) {
+                                                         int64_t id_base, int64_t n, int32_t* __restrict__ dcnt,
+                                                         int c0) {
   const int b = blockIdx.y;
   const int tot = count[b];
   if (tot > cap) return;   // overflow row: full scan later
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < tot; c += gridDim.x * blockDim.x) {
+  for (int c = c0 + blockIdx.x * blockDim.x + threadIdx.x; c < tot; c += gridDim.x * blockDim.x) {
     const int64_t d = (int64_t)cand[(size_t)b * cap + c] - id_base;
     if (d >= 0 && d < n) atomicAdd(dcnt + d, 1);
   }
 }
 
 // Per doc with pairs: a segment [doff, doff + cnt) of the pair list and an
-// entry in the active list; one atomic per wave for each.  ctr[0] = pairs,
-// ctr[1] = active docs.
+// entry in the active list.  Each workgroup owns a contiguous range of docs:
+// pass 1 sums the range (one atomic per counter per WORKGROUP -- one per wave
+// serialised ~30k atomics on two addresses, 0.36 ms at B=256), pass 2 walks it
+// in 256-doc tiles with a block-wide exclusive scan.  Segment order across
+// workgroups is arbitrary; every pair's (b, c) travels with it, so the scores
+// land in the same places.  ctr[0] = pairs, ctr[1] = active docs.
 __global__ __launch_bounds__(256) void band_offsets_kernel(const int32_t* __restrict__ dcnt, int64_t n,
                                                            int32_t* __restrict__ doff, int32_t* __restrict__ act,
                                                            int32_t* __restrict__ act_off,
                                                            int32_t* __restrict__ act_cnt, int32_t* __restrict__ ctr) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t d0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63LL; d0 < n;
-       d0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t d = d0 + lane;
+  __shared__ int s_p[4], s_a[4];
+  __shared__ int s_base[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t tiles = (n + 255) >> 8;
+  const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * per;
+  const int64_t t1 = t0 + per < tiles ? t0 + per : tiles;
+  if (t0 >= t1) return;   // block-uniform
+  int sp = 0, sa = 0;
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t d = (t << 8) + tid;
+    const int c = d < n ? dcnt[d] : 0;
+    sp += c;
+    sa += c > 0 ? 1 : 0;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sp += __shfl_xor(sp, off);
+    sa += __shfl_xor(sa, off);
+  }
+  if (lane == 0) {
+    s_p[wave] = sp;
+    s_a[wave] = sa;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int tp = s_p[0] + s_p[1] + s_p[2] + s_p[3], ta = s_a[0] + s_a[1] + s_a[2] + s_a[3];
+    s_base[0] = tp > 0 ? atomicAdd(ctr, tp) : 0;
+    s_base[1] = ta > 0 ? atomicAdd(ctr + 1, ta) : 0;
+  }
+  __syncthreads();
+  int pb = s_base[0], ab = s_base[1];
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t d = (t << 8) + tid;
     const int c = d < n ? dcnt[d] : 0;
     int incl = c;   // inclusive prefix sum over the wave
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const int t = __shfl_up(incl, off);
-      if (lane >= off) incl += t;
+      const int v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
     }
-    const int total = __shfl(incl, 63);
     const uint64_t am = __ballot(c > 0);
-    if (am == 0) continue;   // wave-uniform
-    int pbase = 0, abase = 0;
-    if (lane == 0) {
-      pbase = atomicAdd(ctr, total);
-      abase = atomicAdd(ctr + 1, __popcll(am));
+    __syncthreads();   // the previous tile's s_p / s_a reads are done
+    if (lane == 63) {
+      s_p[wave] = incl;
+      s_a[wave] = __popcll(am);
     }
-    pbase = __shfl(pbase, 0);
-    abase = __shfl(abase, 0);
+    __syncthreads();
+    int wp = 0, wa = 0;
+    for (int w = 0; w < wave; ++w) {
+      wp += s_p[w];
+      wa += s_a[w];
+    }
     if (c > 0) {
-      const int o = pbase + incl - c;
-      const int a = abase + __popcll(am & ((1ull << lane) - 1ull));
+      const int o = pb + wp + incl - c;
+      const int a = ab + wa + __popcll(am & ((1ull << lane) - 1ull));
       doff[d] = o;
       act[a] = (int32_t)d;
       act_off[a] = o;
       act_cnt[a] = c;
     }
+    pb += s_p[0] + s_p[1] + s_p[2] + s_p[3];
+    ab += s_a[0] + s_a[1] + s_a[2] + s_a[3];
   }
 }
 
@@ -3637,11 +3683,12 @@ __global__ __launch_bounds__(256) void band_scatter_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ count, int cap,
                                                            int64_t id_base, int64_t n, int32_t* __restrict__ dcnt,
                                                            const int32_t* __restrict__ doff,
-                                                           int32_t* __restrict__ pair_b, int32_t* __restrict__ pair_c) {
+                                                           int32_t* __restrict__ pair_b, int32_t* __restrict__ pair_c,
+                                                           int c0) {
   const int b = blockIdx.y;
   const int tot = count[b];
   if (tot > cap) return;
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < tot; c += gridDim.x * blockDim.x) {
+  for (int c = c0 + blockIdx.x * blockDim.x + threadIdx.x; c < tot; c += gridDim.x * blockDim.x) {
     const int64_t d = (int64_t)cand[(size_t)b * cap + c] - id_base;
     if (d < 0 || d >= n) continue;
     const int pos = doff[d] + atomicSub(dcnt + d, 1) - 1;   // leaves dcnt at 0
@@ -3767,37 +3814,45 @@ __global__ __launch_bounds__(256) void rescore_docs_kernel(
 }
 
 // Doc-major band rescoring with the doc split over the workgroup (128-slot
-// docs, CBV2_OPT_BAND_DOC_MAJOR = 3): one band doc per workgroup, wave w
-// holding row tiles 2w, 2w + 1 of hi and lo in VGPRs for all of the doc's
-// pairs; per pair the query's split fragments (L2-resident) and the
-// faithful_doc_split reduction (column maxima -> LDS -> max of 4 -> sum):
-// the same bits as every other faithful rescoring.  ~160 VGPRs (3 waves per
-// SIMD) where the one-wave-per-doc kernel holds a whole half doc (1 per SIMD).
-__global__ __launch_bounds__(256, 2) void rescore_docs_split_kernel(
+// docs): one band doc per workgroup of NW waves, wave w holding row tiles
+// [w * 8/NW, (w + 1) * 8/NW) of hi and lo in VGPRs for all of the doc's pairs;
+// per pair the query's split fragments (L2-resident) and the
+// faithful_doc_split reduction (column maxima -> LDS -> max over the waves ->
+// sum): the same bits as every other faithful rescoring.  NW = 4
+// (CBV2_OPT_BAND_DOC_MAJOR = 3): ~170 VGPRs; NW = 2 (= 4): a half doc per
+// wave, both halves in flight at once, 2 waves per SIMD -- where the
+// one-wave-per-doc kernel (mode 1) walks the halves in turn at 1 wave per
+// SIMD (254 VGPRs + accumulators).  The doc's tiles are loaded before its
+// length is known (its 128 slots exist; rows past the length never enter a
+// product), the next doc's list entry while this one computes.
+template <int NW>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void rescore_docs_split_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens,
     const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int B, int lq,
     const int32_t* __restrict__ act, const int32_t* __restrict__ act_off, const int32_t* __restrict__ act_cnt,
     const int32_t* __restrict__ ctr, const int32_t* __restrict__ pair_b, const int32_t* __restrict__ pair_c,
     float* __restrict__ F, int cap) {
-  __shared__ float s_m[4][32];
+  constexpr int TPW = 8 / NW;   // row tiles per wave
+  __shared__ float s_m[NW][32];
   const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n_act = ctr[1];
-  for (int a = blockIdx.x; a < n_act; a += gridDim.x) {   // one doc per workgroup (block-uniform)
-    const int64_t d = act[a];
+  int a = blockIdx.x;
+  if (a >= n_act) return;   // block-uniform
+  int64_t d = act[a];
+  for (; a < n_act; a += gridDim.x) {   // one doc per workgroup (block-uniform)
+    const size_t at = (size_t)d * kLd * kRowBytes;
+    bf16x8 ah[TPW][4], al[TPW][4];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      gbl_afrag16(hi + at, TPW * wave + t, lane, ah[t]);
+      gbl_afrag16(lo + at, TPW * wave + t, lane, al[t]);
+    }
     const int o = act_off[a], cnt = act_cnt[a];
     int dl = doclens[d];
     dl = dl < 0 ? 0 : (dl > kLd ? kLd : dl);
-    const size_t at = (size_t)d * kLd * kRowBytes;
-    bf16x8 ah[2][4], al[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int rt = 2 * wave + t;
-      if (16 * rt < dl) {
-        gbl_afrag16(hi + at, rt, lane, ah[t]);
-        gbl_afrag16(lo + at, rt, lane, al[t]);
-      }
-    }
+    const int an = a + (int)gridDim.x;
+    const int64_t d_next = an < n_act ? act[an] : 0;
     for (int p = 0; p < cnt; ++p) {
       const int b = pair_b[o + p];
       bf16x8 qh[2][4], ql[2][4];
@@ -3805,8 +3860,8 @@ __global__ __launch_bounds__(256, 2) void rescore_docs_split_kernel(
       load_qfrag16(qlo, b, B, lq, lane, ql);
       float m[2] = {neg_inf(), neg_inf()};
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int rt = 2 * wave + t;
+      for (int t = 0; t < TPW; ++t) {
+        const int rt = TPW * wave + t;
         if (16 * rt < dl) {
           const f32x4 init = (dl >= 16 * rt + 16) ? f32x4{} : row_mask_init16(16 * rt + 4 * g, dl);
           tile16_x3(ah[t], al[t], qh, ql, init, m);
@@ -3819,13 +3874,18 @@ __global__ __launch_bounds__(256, 2) void rescore_docs_split_kernel(
       }
       __syncthreads();
       if (wave == 0) {
-        const float m0 = fmaxf(fmaxf(s_m[0][c16], s_m[1][c16]), fmaxf(s_m[2][c16], s_m[3][c16]));
-        const float m1 = fmaxf(fmaxf(s_m[0][16 + c16], s_m[1][16 + c16]), fmaxf(s_m[2][16 + c16], s_m[3][16 + c16]));
+        float m0 = s_m[0][c16], m1 = s_m[0][16 + c16];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+          m0 = fmaxf(m0, s_m[w][c16]);
+          m1 = fmaxf(m1, s_m[w][16 + c16]);
+        }
         const float v = dpp_row_sum16((c16 < lq ? m0 : 0.0f) + (16 + c16 < lq ? m1 : 0.0f));
         if (lane == 0) F[(size_t)b * cap + pair_c[o + p]] = v;
       }
       __syncthreads();
     }
+    d = d_next;
   }
 }
 
@@ -3856,7 +3916,8 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
                                                            int cap, int32_t* __restrict__ cand,
                                                            int32_t* __restrict__ count,
                                                            const float* __restrict__ lb,
-                                                           const uint32_t* __restrict__ lbu) {
+                                                           const uint32_t* __restrict__ lbu,
+                                                           const int32_t* __restrict__ topk_i) {
   __shared__ int32_t s_ids[kBandLds];
   __shared__ int s_n, s_base;
   const int b = blockIdx.y, lane = threadIdx.x & 63;
@@ -3865,6 +3926,16 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
   const float thr = band_threshold(b, lb, lbu, topk_s, k, beta);
   const float* row = T + (size_t)b * n;
   int32_t* crow = cand + (size_t)b * cap;
+  // topk_i (nullable): the band's slots [0, k) are the bf16 top-k (every one
+  // of them is in the band: T_j >= F_j - beta >= lb - beta), already rescored
+  // by phase 1 and count[b] started at k; the docs at or above the k-th key
+  // are left out here
+  uint64_t kth = 0;
+  if (topk_i != nullptr) {
+    kth = rank_key(topk_s[(size_t)b * k + k - 1], (uint32_t)((int64_t)topk_i[(size_t)b * k + k - 1] - id_base));
+    if (blockIdx.x == 0)
+      for (int j = threadIdx.x; j < k; j += blockDim.x) crow[j] = topk_i[(size_t)b * k + j];
+  }
   constexpr int U = 8;  // 8 coalesced loads in flight per thread, then the ballots
   const int64_t step = (int64_t)gridDim.x * blockDim.x * U;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U; i0 < n; i0 += step) {  // uniform trip count per wave
@@ -3877,7 +3948,7 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x + threadIdx.x;
-      const bool take = i < n && v[u] >= thr;
+      const bool take = i < n && v[u] >= thr && (topk_i == nullptr || rank_key(v[u], (uint32_t)i) < kth);
       const uint64_t mask = __ballot(take);
       if (mask == 0) continue;
       const int nh = __popcll(mask);
@@ -4011,12 +4082,17 @@ constexpr int kBandSelMax = 512;       // keys ranked by counting after the radi
 // counted against every other from LDS: 107 us for an 880-key band at 1M docs,
 // B=1, vs 14 us through the radix select; profiles/r04e_*)
 constexpr int kBandCountMax = 128;
+// lb / lbu (nullable, as band_threshold): a lower bound of the row's k-th
+// score; when at least kk band keys reach it and no more than kBandSelMax
+// do, those keys alone are ranked (the top-kk is among them) -- no radix pass.
 __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __restrict__ F,
                                                                  const int32_t* __restrict__ cand,
                                                                  const int32_t* __restrict__ count, int cap, int k,
                                                                  int64_t id_base, float* __restrict__ out_s,
                                                                  int32_t* __restrict__ out_i,
-                                                                 int32_t* __restrict__ status) {
+                                                                 int32_t* __restrict__ status,
+                                                                 const float* __restrict__ lb,
+                                                                 const uint32_t* __restrict__ lbu) {
   __shared__ uint64_t keys[kBandCapMax];
   __shared__ uint64_t sel[kBandSelMax];
   __shared__ uint32_t hist[2048];
@@ -4032,7 +4108,25 @@ __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __
   int32_t* oi = out_i + (size_t)b * k;
   const uint64_t* src = keys;
   int m = cnt;
-  if (cnt > kBandCountMax) {
+  const int kk0 = k < cnt ? k : cnt;
+  if (cnt > kBandCountMax && (lb != nullptr || lbu != nullptr)) {
+    // the keys whose score reaches the k-th score's lower bound
+    const uint32_t ulb = f2u(lbu != nullptr ? u2f(lbu[b]) : lb[b]);
+    for (int i = tid; i < cnt; i += nth)
+      if ((uint32_t)(keys[i] >> 32) >= ulb) {
+        const uint32_t pos = atomicAdd(&misc[0], 1u);
+        if (pos < (uint32_t)kBandSelMax) sel[pos] = keys[i];
+      }
+    __syncthreads();
+    if (misc[0] >= (uint32_t)kk0 && misc[0] <= (uint32_t)kBandSelMax) {
+      src = sel;
+      m = (int)misc[0];
+    }
+    __syncthreads();
+    if (tid == 0) misc[0] = 0;
+    __syncthreads();
+  }
+  if (src == keys && cnt > kBandCountMax) {
     // the kk-th largest score (the keys' top 32 bits) by radix select over
     // 11/11/10-bit digits, then the keys that reach it (the top-kk and its
     // score ties) into sel
@@ -4261,6 +4355,7 @@ struct cbv2_index {
   // few hits one after another; profiles/r04d_*)
   bool band_fused = false;
   bool rescore_split = true;     // CBV2_OPT_RESCORE_SPLIT (one pair per workgroup, rows over 4 waves)
+  bool band_reuse = true;        // CBV2_OPT_BAND_REUSE (the band's first k slots: phase 1's top-k scores)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -5218,9 +5313,9 @@ int check_f32(cbv2_index* ix, int op, const float* Q, int32_t B, int32_t lq, int
 }
 
 // (a SEARCH workspace's split also resets the rows' band state: count, lb, done)
-int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st) {
+int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st, int count0 = 0) {
   hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(64), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
-                     ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done);
+                     ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0);
   return launch_check("split_query_kernel");
 }
 
@@ -5230,15 +5325,21 @@ constexpr int64_t kRsSmallPairs = 4096;
 constexpr int64_t kRsSplitGrid = 1024;   // workgroups per row of a split rescoring launch (grid-stride beyond)
 int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t* cand, const int32_t* count,
                    int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
-                   const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr) {
-  if (limit <= 0) return CBV2_OK;
-  if (ix->rescore_split) {   // one pair per workgroup (its doc split over the 4 waves)
-    const unsigned gx = (unsigned)(limit < kRsSplitGrid ? limit : kRsSplitGrid);
-    hipLaunchKernelGGL(ix->ld != kLd ? rescore_split_kernel<true> : rescore_split_kernel<false>, dim3(gx, (unsigned)B),
-                       dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w->qhi, w->qlo, lq,
-                       cand, count, limit, ld_c, out, ld_out, only_neg, (int)ix->ld, lb_min);
+                   const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr, int64_t c0 = 0) {
+  if (limit <= c0) return CBV2_OK;
+  if (ix->rescore_split) {   // one pair per workgroup (its doc split over 4 waves, or 2 for launches past
+                             // the chip's resident 4-wave workgroups: one round of 2-wave ones instead of two)
+    const int64_t span = limit - c0;   // (pairs [c0, min(count, limit)) of a row)
+    const unsigned gx = (unsigned)(span < kRsSplitGrid ? span : kRsSplitGrid);
+    const bool two = (int64_t)gx * B > 3LL * cu_count(ix->device);
+    auto kern = ix->ld != kLd ? (two ? rescore_split_kernel<true, 2> : rescore_split_kernel<true, 4>)
+                              : (two ? rescore_split_kernel<false, 2> : rescore_split_kernel<false, 4>);
+    hipLaunchKernelGGL(kern, dim3(gx, (unsigned)B), dim3(two ? 128 : 256), 0, st, ix->tokens, ix->resid, ix->doclens,
+                       ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out, only_neg,
+                       (int)ix->ld, lb_min, c0);
     return launch_check("rescore_split_kernel");
   }
+  if (c0 != 0) return fail(CBV2_EUNSUPPORTED, "pair offset needs the split rescoring");
   if (pw <= 0) pw = (int64_t)B * limit <= kRsSmallPairs ? 1 : kRsPerWave;
   const int64_t per_wg = 4LL * pw;
   int64_t gx = (limit + per_wg - 1) / per_wg;
@@ -5526,6 +5627,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
     case CBV2_OPT_RESCORE_SPLIT:
       ix->rescore_split = value != 0;
       return CBV2_OK;
+    case CBV2_OPT_BAND_REUSE:
+      ix->band_reuse = value != 0;
+      return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);
   }
@@ -5707,6 +5811,13 @@ namespace {
 // itself); fk_out (nullable): those k faithful scores themselves, [B][k].
 // Returns 1 when the whole search is already done (k beyond any band: the
 // full faithful scan ran, status -1 everywhere).
+// The two-pass band (lbu) reuses phase 1's faithful scores of the bf16 top-k
+// as its first k slots instead of rescoring those docs again (they are always
+// in the band): the split rescoring, not the fused latency launch, n >= k.
+bool band_reuses_topk(const cbv2_index* ix, int32_t B, int32_t k) {
+  return ix->band_reuse && ix->rescore_split && ix->n >= k && !(B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused);
+}
+
 int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w,
                       float* out_scores, int32_t* out_ids, int32_t* out_status, bool want_lb, hipStream_t st,
                       float* fk_out = nullptr) {
@@ -5716,7 +5827,7 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     if ((rc = topk_impl_empty(B, k, out_scores, out_ids, st))) return rc;
     return 1;
   }
-  if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
+  if ((rc = split_queries(ix, Q, B, lq, &w, st, want_lb && band_reuses_topk(ix, B, k) ? k : 0))) return rc;
   if (k > kBandCapMax) {   // no band can hold k: every row takes the full faithful scan (status -1)
     CBV2_HIP(hipMemsetAsync(out_status, 0xff, (size_t)B * sizeof(int32_t), st));
     if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st))) return rc;
@@ -5750,7 +5861,9 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
                            const float* lb, const uint32_t* lbu, float* out_scores, int32_t* out_ids,
                            int32_t* out_status, hipStream_t st) {
   int rc;
-  // (count[b] was reset by the query split of phase 1)
+  // (count[b] was reset by the query split of phase 1: to k with the reuse)
+  const bool reuse = lbu != nullptr && band_reuses_topk(ix, B, k);
+  const int c0 = reuse ? k : 0;
   int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
   const int64_t max_splits = (ix->n + 8191) / 8192;
   splits = splits < max_splits ? splits : max_splits;
@@ -5764,7 +5877,8 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
     if ((rc = launch_check("band_collect_rescore_kernel"))) return rc;
   } else {
     hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
-                       out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb, lbu);
+                       out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb, lbu,
+                       reuse ? out_ids : nullptr);
     if ((rc = launch_check("band_collect_kernel"))) return rc;
   }
   // pairs grouped by doc (each band doc's tiles read once per batch) pay when
@@ -5778,19 +5892,22 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
     CBV2_HIP(hipMemsetAsync(w.dctr, 0, 2 * sizeof(int32_t), st));
     const unsigned gc = (unsigned)std::min<int64_t>((cap + 255) / 256, 16);
     hipLaunchKernelGGL(band_count_kernel, dim3(gc, (unsigned)B), dim3(256), 0, st, w.cand, w.count, cap, ix->id_base,
-                       ix->n, w.dcnt);
+                       ix->n, w.dcnt, c0);
     if ((rc = launch_check("band_count_kernel"))) return rc;
-    const unsigned go = (unsigned)std::min<int64_t>((ix->n + 255) / 256, 4096);
+    const unsigned go = (unsigned)std::min<int64_t>((ix->n + 255) / 256, 1024);
     hipLaunchKernelGGL(band_offsets_kernel, dim3(go), dim3(256), 0, st, w.dcnt, ix->n, w.doff, w.act, w.act_off,
                        w.act_cnt, w.dctr);
     if ((rc = launch_check("band_offsets_kernel"))) return rc;
     hipLaunchKernelGGL(band_scatter_kernel, dim3(gc, (unsigned)B), dim3(256), 0, st, w.cand, w.count, cap,
-                       ix->id_base, ix->n, w.dcnt, w.doff, w.pair_b, w.pair_c);
+                       ix->id_base, ix->n, w.dcnt, w.doff, w.pair_b, w.pair_c, c0);
     if ((rc = launch_check("band_scatter_kernel"))) return rc;
-    if (ix->band_doc_major == 3 && ix->ld == kLd) {   // the doc split over the workgroup
-      const unsigned gs = (unsigned)(3 * cu_count(ix->device) * 4);   // ~3 workgroups per CU resident, x4
-      hipLaunchKernelGGL(rescore_docs_split_kernel, dim3(gs), dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens,
-                         w.qhi, w.qlo, B, lq, w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
+    if ((ix->band_doc_major == 3 || ix->band_doc_major == 4) && ix->ld == kLd) {   // the doc split over the workgroup
+      const bool two = ix->band_doc_major == 4;
+      // resident workgroups per CU (2 waves per SIMD), x4; grid-stride beyond
+      const unsigned gs = (unsigned)((two ? 4 : 3) * cu_count(ix->device) * 4);
+      hipLaunchKernelGGL(two ? rescore_docs_split_kernel<2> : rescore_docs_split_kernel<4>, dim3(gs),
+                         dim3(two ? 128 : 256), 0, st, ix->tokens, ix->resid, ix->doclens, w.qhi, w.qlo, B, lq, w.act,
+                         w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap);
       if ((rc = launch_check("rescore_docs_split_kernel"))) return rc;
     } else {
       const unsigned gr = (unsigned)(2 * cu_count(ix->device) * 4);   // 4 waves each; grid-stride over docs
@@ -5801,16 +5918,19 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
       if ((rc = launch_check("rescore_docs_kernel"))) return rc;
     }
   } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
-                                   B <= kBandPairMaxB ? 1 : 0))) {
+                                   B <= kBandPairMaxB ? 1 : 0, nullptr, c0))) {
     return rc;
   }
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
-                     ix->id_base, out_scores, out_ids, out_status);
+                     ix->id_base, out_scores, out_ids, out_status, lb, lbu);
   if ((rc = launch_check("band_select_kernel"))) return rc;
   // rows whose band overflowed cap (status -1): the full faithful scan over
   // every doc and an exact top-k, on the device (other rows exit at once)
   if (ix->rescore_split && k <= kTopkMax) {   // scan + top-k in one launch (last workgroup per row)
-    const unsigned gx = (unsigned)(ix->n < kRsSplitGrid ? ix->n : kRsSplitGrid);
+    // (a grid of this size is dispatched whether or not a row overflowed: it
+    // stays small -- an overflowing row then takes a few ms)
+    const int64_t fb = std::max<int64_t>(64, 512 / B);
+    const unsigned gx = (unsigned)(ix->n < fb ? ix->n : fb);
     hipLaunchKernelGGL(ix->ld != kLd ? fallback_split_kernel<true> : fallback_split_kernel<false>, dim3(gx, (unsigned)B),
                        dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w.qhi, w.qlo, lq,
                        w.T, out_status, (int)ix->ld, w.done, k, out_scores, out_ids);

@@ -126,7 +126,10 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        of more than 8 queries grouped by doc (each band doc
  *                        read once per batch; 0: pair by pair; smaller
  *                        batches always go pair by pair, one band doc per
- *                        wave).  Identical results either way.
+ *                        wave).  Doc-major kernels: 1 one wave per doc, its
+ *                        halves in turn; 2 the same, pair-outer; 3 / 4 one
+ *                        doc per workgroup of 4 / 2 waves (128-slot docs;
+ *                        others take 1).  Identical results either way.
  *  CBV2_OPT_BAND_LOWER_BOUND 1: cbv2_search_f32 first rescores the bf16
  *                        top-k, whose minimum faithful score lb bounds the
  *                        k-th from below, and bands T >= lb - beta (0: the
@@ -140,6 +143,11 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        full-scan fallback) score one (query, doc) pair per
  *                        workgroup, the doc's rows split over its 4 waves (0:
  *                        one pair per wave).  Identical results.
+ *  CBV2_OPT_BAND_REUSE   1: the two-pass band of cbv2_search_f32 keeps the
+ *                        faithful scores phase 1 computed for the bf16 top-k
+ *                        (its lower bound) as its first k entries and rescores
+ *                        only the rest (0: the whole band).  Needs
+ *                        CBV2_OPT_RESCORE_SPLIT.  Identical results.
  *  CBV2_OPT_TOPK_BMAX    1: cbv2_search's unfused MaxSim scan (rows of >= 65,536
  *                        and <= 1,572,864 docs, k <= 1024) also folds the max of
  *                        every 64-doc block, and ONE select launch reads only
@@ -157,6 +165,7 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_TOPK_BMAX 5
 #define CBV2_OPT_BAND_FUSED 6
 #define CBV2_OPT_RESCORE_SPLIT 7
+#define CBV2_OPT_BAND_REUSE 8
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

@@ -153,13 +153,14 @@ def test_faithful_shards_merge_equal_unsharded(dev):
     assert torch.equal(mi, fi) and torch.equal(ms, fs)
 
 
-@pytest.mark.parametrize("N,dups,mode", [(6000, 1, 1), (3000, 9, 1), (6000, 1, 3), (3000, 9, 3)])
+@pytest.mark.parametrize("N,dups,mode", [(6000, 1, 1), (3000, 9, 1), (6000, 1, 3), (3000, 9, 3), (6000, 1, 4), (3000, 9, 4)])
 def test_band_doc_major_equals_pair_major(dev, N, dups, mode):
     """Doc-major band rescoring (pairs grouped by doc, each band doc's tiles
     read once per batch; batches of more than 8 queries) returns the
     pair-by-pair rescoring's results bit for bit.  dups > 1 repeats queries,
     so every band doc has > 4 pairs (several passes of one wave over the
-    doc).  mode 3: the doc split over the workgroup (rescore_docs_split_kernel)."""
+    doc).  modes 3 / 4: the doc split over a workgroup of 4 / 2 waves
+    (rescore_docs_split_kernel)."""
     docs, doclens, Q = make_case(N + dups, N, 12, 32)
     if dups > 1:
         Q = torch.cat([Q[:1].expand(dups, -1, -1), Q[1:]]).contiguous()
@@ -326,3 +327,35 @@ def test_rescore_split_equals_one_wave_per_pair(dev, B, ld):
         assert torch.equal(a, b), name
     exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
     np.testing.assert_allclose(got[1][7].cpu().numpy(), exact, atol=ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("B,mode", [(1, 1), (6, 1), (12, 1), (12, 3), (12, 4), (12, 0)])
+def test_band_reuse_equals_full_band(dev, B, mode):
+    """CBV2_OPT_BAND_REUSE: the two-pass band keeps phase 1's faithful scores of
+    the bf16 top-k as its first k slots (band_collect leaves out every doc at
+    or above the k-th key) and rescores only the rest -- pair by pair (B <= 8),
+    doc-major (modes 1, 3) or pair by pair at any B (mode 0).  Top-k, scores
+    and band sizes equal the full band's bit for bit, with exact copies of row
+    0's k-th doc (k = 40, 100) at other ids: T ties straddling the k-th key."""
+    docs, doclens, Q = make_case(911 + B + mode, 5000, B, 32)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=3)
+    _, i0 = ix.search(Q.to(dev), 100)
+    for j, r in enumerate((39, 99)):              # copies right after the original's key: ties at the k-th
+        src = int(i0[0, r]) - 3
+        docs[4990 + j], doclens[4990 + j] = docs[src], doclens[src]
+    del ix
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=3)
+    ix.set_option(_lib.OPT_BAND_DOC_MAJOR, mode)
+    Qd = Q.to(dev)
+    got = {}
+    for k in (40, 100):
+        for reuse in (1, 0):
+            ix.set_option(_lib.OPT_BAND_REUSE, reuse)
+            s, i = ix.search(Qd, k)
+            got[(k, reuse)] = (s.clone(), i.clone(), ix.last_band.clone())
+        for a, b, name in zip(got[(k, 1)], got[(k, 0)], ("s", "i", "band")):
+            assert torch.equal(a, b), (k, name)
+    ix.set_option(_lib.OPT_BAND_REUSE, 1)
+    ix.set_option(_lib.OPT_BAND_DOC_MAJOR, 1)
+    exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
+    assert_ranking_consistent(got[(100, 1)][1].cpu().numpy(), exact, ATOL, id_base=3)
