@@ -1209,7 +1209,9 @@ __device__ __forceinline__ int sload_len(const int32_t* p) {
 // a wave writes its scores 64 docs at a time, which with chunks of a multiple
 // of 64 docs (the launcher's rounding) are exactly one block: one wave max and
 // one store per block, and the separate block-max launch is skipped.
-template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
+// PF (lab): the next tile's fragments are read from the ring while this
+// tile's MFMAs run (the LDS read latency off the critical path).
+template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false, bool PF = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out, int64_t chunk_docs,
@@ -1279,6 +1281,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
   for (int k = 0; k < SLOTS; ++k) issue_next();
 
   int consumed = 0;
+  // PF: the ring's next tile, read ahead (c: this lane's row of the tile)
+  auto read_tile = [&](bf16x8 (&a)[4]) {
+    if (issued - consumed >= SLOTS)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SLOTS - 1)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint8_t* row = ring + (consumed & (SLOTS - 1)) * 4096 + c * kRowBytes;
+    const int sw = swz16(c);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) a[s4] = *reinterpret_cast<const bf16x8*>(row + 16 * ((4 * g + s4) ^ sw));
+  };
+  bf16x8 a_cur[4];
+  if (PF && issued > 0) {
+    read_tile(a_cur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ++consumed;
+    issue_next();
+  }
   for (int i = 0; i < nd; ++i) {
     int dl = sload_len(dls + i);
     dl = dl < 0 ? 0 : (dl > ld ? ld : dl);
@@ -1287,6 +1307,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_stream_kernel(
 #pragma unroll
     for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     for (int t = 0; t < nt; ++t) {
+      if (PF) {
+        bf16x8 a_nx[4];
+        const bool more = consumed < issued;   // the ring holds a later tile (issued ahead of every read)
+        if (more) read_tile(a_nx);
+        const f32x4 init = (dl >= 16 * t + 16) ? f32x4{} : row_mask_init16(16 * t + 4 * g, dl);
+        tile16<QW>(a_cur, qf, init, m);
+        if (more) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // its slot is read: refill it
+          ++consumed;
+          issue_next();
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) a_cur[s4] = a_nx[s4];
+        }
+        continue;
+      }
       if (TW2 && t + 1 < nt) {
         if (issued - consumed >= SLOTS)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SLOTS - 2)) : "memory");
@@ -4464,7 +4499,8 @@ enum ScanVariant {
   kScanDirectQ1 = 9, kScanDirectQ2 = 10, kScan16x4W8 = 11, kScan16x4W4 = 12, kScan16x4W4Q2 = 13,
   kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17, kScanStreamQ4 = 18,
   kScanStreamQ8 = 19, kScanStreamQ1Tw2 = 20, kScanStreamQ2Tw2 = 21, kScanPairQ1 = 22, kScanPairQ2 = 23,
-  kScanPairQ4 = 24,
+  kScanPairQ4 = 24, kScanStreamQ4Pf = 25, kScanStreamQ1Pf = 26, kScanStreamQ2Pf = 27, kScan16x4W4Q1 = 28,
+  kScan16x4W4Q1Occ3 = 29,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -4712,7 +4748,7 @@ int launch_pair(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
 
 // bm (nullable): fold the block and superblock maxima into the scan (chunks
 // rounded up to whole 256-doc superblocks; layout of bm_ws_bytes).
-template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false>
+template <int QW, int AUX, int WAVES = 4, int SLOTS = kStreamSlots, bool TW2 = false, bool PF = false>
 int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                   uint32_t* bm = nullptr) {
   if (ix->dtype != CBV2_DTYPE_BF16) return fail(CBV2_EUNSUPPORTED, "stream scan: bf16 index only");
@@ -4726,7 +4762,7 @@ int launch_stream(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, 
   n_chunks = (ix->n + chunk_docs - 1) / chunk_docs;
   const int64_t grid = ((int64_t)nq_groups * n_chunks + WAVES - 1) / WAVES;
   if (grid > 0x7fffffff) return fail(CBV2_EUNSUPPORTED, "scan grid too large");
-  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS, TW2>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
+  hipLaunchKernelGGL((maxsim_scan_stream_kernel<QW, AUX, WAVES, SLOTS, TW2, PF>), dim3((unsigned)grid), dim3(WAVES * 64), 0, st,
                      ix->tokens,
                      ix->doclens, ix->n, Q, B, lq, out, ld_out, chunk_docs, (int)ix->ld, bm, bm_blocks(ix->n),
                      bm ? bm_super_keys(bm, B, ix->n) : nullptr, bm_supers(ix->n));
@@ -4811,6 +4847,18 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_pair<2>(ix, Q, B, lq, out, ld_out, st);
     case kScanPairQ4:
       return launch_pair<4>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ4Pf:   // lab: the next tile's fragments read under this tile's MFMAs
+      return launch_stream<4, 2, 4, kStreamSlots, false, true>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ1Pf:
+      return launch_stream<1, 2, 4, kStreamSlots, false, true>(ix, Q, B, lq, out, ld_out, st);
+    case kScanStreamQ2Pf:
+      return launch_stream<2, 2, 4, kStreamSlots, false, true>(ix, Q, B, lq, out, ld_out, st);
+    case kScan16x4W4Q1:     // lab: 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
+      return launch_scan16x4<4, 1, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
+    case kScan16x4W4Q1Occ3:
+      return launch_scan16x4<4, 1, 3, 2, 2, false, 32, 3>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB,
+                                                          kScanTaskDocs, nullptr, ctr_ws);
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
