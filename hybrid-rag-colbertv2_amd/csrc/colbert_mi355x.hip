@@ -800,9 +800,12 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // A wave waits only for what it reads or overwrites, so the partner waves
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
+// AUX: the doc stream's cache policy (0 cached: the query groups of a chunk
+// share its tiles through L2; 2 non-temporal, for a launch of ONE query
+// group, where every byte is read once).
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
           bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd,
-          int MORDER = 0>
+          int MORDER = 0, int AUX = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
@@ -914,7 +917,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
         d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
         const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
-                                         0, 0);
+                                         0, AUX);
       };
       auto issue = [&](int it, int buf) {
         if (!loader || (PROBE == 2 && it >= NBUF)) return;   // PROBE 2 (INVALID): no streaming after the first fill
@@ -3952,7 +3955,8 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
                                                            int32_t* __restrict__ count,
                                                            const float* __restrict__ lb,
                                                            const uint32_t* __restrict__ lbu,
-                                                           const int32_t* __restrict__ topk_i) {
+                                                           const int32_t* __restrict__ topk_i,
+                                                           const uint32_t* __restrict__ bm) {
   __shared__ int32_t s_ids[kBandLds];
   __shared__ int s_n, s_base;
   const int b = blockIdx.y, lane = threadIdx.x & 63;
@@ -3971,34 +3975,67 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
     if (blockIdx.x == 0)
       for (int j = threadIdx.x; j < k; j += blockDim.x) crow[j] = topk_i[(size_t)b * k + j];
   }
-  constexpr int U = 8;  // 8 coalesced loads in flight per thread, then the ballots
-  const int64_t step = (int64_t)gridDim.x * blockDim.x * U;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U; i0 < n; i0 += step) {  // uniform trip count per wave
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * blockDim.x + threadIdx.x;
-      v[u] = i < n ? row[i] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * blockDim.x + threadIdx.x;
-      const bool take = i < n && v[u] >= thr && (topk_i == nullptr || rank_key(v[u], (uint32_t)i) < kth);
-      const uint64_t mask = __ballot(take);
-      if (mask == 0) continue;
-      const int nh = __popcll(mask);
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&s_n, nh);
-      base = __shfl(base, 0);
-      const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-      if (take) {
-        if (pos < kBandLds) {
-          s_ids[pos] = (int32_t)(id_base + i);
-        } else {  // LDS list full (a very wide band): straight to the global list
-          const int gp = atomicAdd(count + b, 1);
-          if (gp < cap) crow[gp] = (int32_t)(id_base + i);
-        }
+  // doc i (this lane's) with score v: appended when in the band (wave-uniform call)
+  auto offer = [&](int64_t i, float v) {
+    const bool take = i < n && v >= thr && (topk_i == nullptr || rank_key(v, (uint32_t)i) < kth);
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) return;
+    const int nh = __popcll(mask);
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&s_n, nh);
+    base = __shfl(base, 0);
+    const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+    if (take) {
+      if (pos < kBandLds) {
+        s_ids[pos] = (int32_t)(id_base + i);
+      } else {  // LDS list full (a very wide band): straight to the global list
+        const int gp = atomicAdd(count + b, 1);
+        if (gp < cap) crow[gp] = (int32_t)(id_base + i);
       }
+    }
+  };
+  if (bm != nullptr) {
+    // bm (nullable): the row's 64-doc block maxima of the block-max top-k
+    // (keys f2u(max), [B][ceil(n / 64)]) -- a block whose key is below the
+    // threshold holds no band doc and its scores are never read: ~1 block in
+    // 18 at 1M docs (883 band docs / query), instead of the whole 4 MB row
+    const int64_t nb = (n + 63) >> 6;
+    const uint32_t* krow = bm + (size_t)b * nb;
+    const uint32_t uthr = f2u(thr);
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int64_t g0 = ((int64_t)blockIdx.x * nw + wave) * 64; g0 < nb; g0 += (int64_t)gridDim.x * nw * 64) {
+      const int64_t kb = g0 + lane;   // one block key per lane
+      uint64_t qual = __ballot(kb < nb && krow[kb] >= uthr);
+      while (qual != 0) {             // wave-uniform; up to 4 qualifying blocks' scores in flight
+        int64_t blk[4];
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          blk[u] = -1;
+          if (qual != 0) {
+            blk[u] = g0 + (__ffsll((long long)qual) - 1);
+            qual &= qual - 1;
+          }
+          const int64_t i = blk[u] >= 0 ? (blk[u] << 6) + lane : n;
+          v[u] = i < n ? row[i] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (blk[u] >= 0) offer((blk[u] << 6) + lane, v[u]);
+      }
+    }
+  } else {
+    constexpr int U = 8;  // 8 coalesced loads in flight per thread, then the ballots
+    const int64_t step = (int64_t)gridDim.x * blockDim.x * U;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U; i0 < n; i0 += step) {  // uniform trip count per wave
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * blockDim.x + threadIdx.x;
+        v[u] = i < n ? row[i] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) offer(i0 + (int64_t)u * blockDim.x + threadIdx.x, v[u]);
     }
   }
   __syncthreads();
@@ -4391,6 +4428,7 @@ struct cbv2_index {
   bool band_fused = false;
   bool rescore_split = true;     // CBV2_OPT_RESCORE_SPLIT (one pair per workgroup, rows over 4 waves)
   bool band_reuse = true;        // CBV2_OPT_BAND_REUSE (the band's first k slots: phase 1's top-k scores)
+  bool band_block_skip = true;   // CBV2_OPT_BAND_BLOCK_SKIP (the collect reads only blocks whose max reaches it)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -4500,7 +4538,7 @@ enum ScanVariant {
   kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17, kScanStreamQ4 = 18,
   kScanStreamQ8 = 19, kScanStreamQ1Tw2 = 20, kScanStreamQ2Tw2 = 21, kScanPairQ1 = 22, kScanPairQ2 = 23,
   kScanPairQ4 = 24, kScanStreamQ4Pf = 25, kScanStreamQ1Pf = 26, kScanStreamQ2Pf = 27, kScan16x4W4Q1 = 28,
-  kScan16x4W4Q1Occ3 = 29,
+  kScan16x4W8Q1 = 30, kScan16x4W8Q1x2 = 31, kScan16x4W4Q1Nt = 33, kScan16x4W4Q2Nt = 34,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -4544,9 +4582,15 @@ int pick_shape(const ShapeCost (&c)[N], int B) {
   }
   return best;
 }
-// bf16: 4 waves x 2 queries (5.5 ms per group; B=8 alone 6.3), 4 x 4 (9.6;
-// B=16 alone 10.6), 8 x 4 (17.4; B=256 = 8 groups 139 ms)
-constexpr ShapeCost kBf16Shapes[] = {{8, 5.5f, kScan16x4W4Q2}, {16, 9.6f, kScan16x4W4}, {32, 17.4f, kScan16x4W8}};
+// bf16: 4 waves x 1 query (round 4: 4.6 ms per group -- B = 3-4 without the
+// 4 x 2 shape's padded query slots, which at 82 % MFMA-busy cost it the
+// clock, and with the non-temporal doc stream of a one-group launch: 1M docs,
+// same process, B=4 5.98 (4 x 2) -> 4.92 (4 x 1) -> 4.62 ms (4 x 1, nt), B=3
+// 4.91 -> 4.62; profiles/r04m_lab_midbatch.log, r04n_lab_midbatch.log), 4 x 2
+// (6.1; nt for B = 5-8: B=8 6.39 -> 6.34), 4 x 4 (9.6; B=16 alone 10.6), 8 x 4
+// (17.4; B=256 = 8 groups 139 ms)
+constexpr ShapeCost kBf16Shapes[] = {
+    {4, 4.6f, kScan16x4W4Q1}, {8, 6.1f, kScan16x4W4Q2}, {16, 9.6f, kScan16x4W4}, {32, 17.4f, kScan16x4W8}};
 
 template <int WAVES, int QW, int PER_CU, typename Kern>
 int launch_scan(Kern kern, cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out,
@@ -4673,7 +4717,8 @@ int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
 }
 
 template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
-          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd, int MORDER = 0>
+          int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd, int MORDER = 0,
+          int AUX = 0>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
                     int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
@@ -4687,7 +4732,8 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD, MORDER>),
+  hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD, MORDER,
+                                             AUX>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
                      ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -4853,12 +4899,25 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_stream<1, 2, 4, kStreamSlots, false, true>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ2Pf:
       return launch_stream<2, 2, 4, kStreamSlots, false, true>(ix, Q, B, lq, out, ld_out, st);
-    case kScan16x4W4Q1:     // lab: 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
+    case kScan16x4W4Q1Nt:   // lab: 4 x 1 / 4 x 2 with the non-temporal doc stream (one query group per launch)
+      return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+          ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
+    case kScan16x4W4Q2Nt:
+      return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+          ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
+    case kScan16x4W8Q1:     // lab: 8 queries per workgroup, one per wave (2 waves per SIMD)
+      return launch_scan16x4<8, 1, 1, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
+    case kScan16x4W8Q1x2:   // lab: the same, two workgroups per CU
+      return launch_scan16x4<8, 1, 2, 2, 2, false, 32, 4>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB,
+                                                          kScanTaskDocs, nullptr, ctr_ws);
+    case kScan16x4W4Q1:     // 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
+      if (B <= 4)           // one query group: every doc byte is read once (non-temporal)
+        return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
       return launch_scan16x4<4, 1, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
                                                    nullptr, ctr_ws);
-    case kScan16x4W4Q1Occ3:
-      return launch_scan16x4<4, 1, 3, 2, 2, false, 32, 3>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB,
-                                                          kScanTaskDocs, nullptr, ctr_ws);
+
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
@@ -4884,6 +4943,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs,
                                                    nullptr, ctr_ws);
     case kScan16x4W4Q2:   // 8 queries per workgroup (2 per wave)
+      if (B <= 8)         // one query group: non-temporal doc stream
+        return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
       return launch_scan16x4<4, 2, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
                                                    nullptr, ctr_ws);
     default:
@@ -5678,6 +5740,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
     case CBV2_OPT_BAND_REUSE:
       ix->band_reuse = value != 0;
       return CBV2_OK;
+    case CBV2_OPT_BAND_BLOCK_SKIP:
+      ix->band_block_skip = value != 0;
+      return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);
   }
@@ -5924,9 +5989,11 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
                        lq, cap, w.cand, w.F, w.count);
     if ((rc = launch_check("band_collect_rescore_kernel"))) return rc;
   } else {
+    // phase 1's block-max select left the rows' 64-doc block keys in w.tk
+    const bool bkeys = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k) && ix->band_block_skip;
     hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
                        out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb, lbu,
-                       reuse ? out_ids : nullptr);
+                       reuse ? out_ids : nullptr, bkeys ? reinterpret_cast<const uint32_t*>(w.tk) : nullptr);
     if ((rc = launch_check("band_collect_kernel"))) return rc;
   }
   // pairs grouped by doc (each band doc's tiles read once per batch) pay when

@@ -148,6 +148,10 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        (its lower bound) as its first k entries and rescores
  *                        only the rest (0: the whole band).  Needs
  *                        CBV2_OPT_RESCORE_SPLIT.  Identical results.
+ *  CBV2_OPT_BAND_BLOCK_SKIP 1: the band collect of cbv2_search_f32 reads only
+ *                        the 64-doc blocks whose maximum (left by the
+ *                        block-max top-k) reaches the band threshold (0: the
+ *                        whole score row).  Identical results.
  *  CBV2_OPT_TOPK_BMAX    1: cbv2_search's unfused MaxSim scan (rows of >= 65,536
  *                        and <= 1,572,864 docs, k <= 1024) also folds the max of
  *                        every 64-doc block, and ONE select launch reads only
@@ -166,6 +170,7 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_BAND_FUSED 6
 #define CBV2_OPT_RESCORE_SPLIT 7
 #define CBV2_OPT_BAND_REUSE 8
+#define CBV2_OPT_BAND_BLOCK_SKIP 9
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

@@ -359,3 +359,44 @@ def test_band_reuse_equals_full_band(dev, B, mode):
     ix.set_option(_lib.OPT_BAND_DOC_MAJOR, 1)
     exact = orc.maxsim(Q.numpy(), docs.numpy(), doclens.numpy())
     assert_ranking_consistent(got[(100, 1)][1].cpu().numpy(), exact, ATOL, id_base=3)
+
+
+@pytest.fixture(scope="module")
+def bmax_corpus(dev):
+    """70,000 docs of the bench's synthetic corpus (fp32, 10 planted per query):
+    past the block-max top-k's 65,536-doc threshold, so phase 1 leaves 64-doc
+    block keys for the band collect."""
+    from hybrid_rag_colbertv2_amd import synth
+    n, B = 70_000, 12
+    Qf = synth.make_queries(B, 32, seed=5)
+    planted = synth.planted_ids(B, n, 10, seed=6)
+    x, dl = synth.make_shard(0, n, Qf, planted, dev, seed=3, dtype=torch.float32)
+    dl[::7] = torch.randint(0, 129, dl[::7].shape, device=dev, dtype=torch.int32)   # ragged and empty docs
+    ix = ColbertIndex.faithful_f32(x, dl, id_base=9)
+    del x
+    torch.cuda.empty_cache()
+    return ix, Qf.to(dev)
+
+
+@pytest.mark.parametrize("B", [1, 3, 12])
+def test_band_block_skip_equals_full_row(dev, bmax_corpus, B):
+    """CBV2_OPT_BAND_BLOCK_SKIP: the band collect reads only the 64-doc blocks
+    whose maximum reaches the threshold (the block-max top-k's keys).  Top-k,
+    scores and band sizes equal the whole-row collect's bit for bit, with and
+    without the phase-1 reuse, pair-by-pair (B <= 8) and doc-major (B = 12)."""
+    ix, Q = bmax_corpus
+    Qb = Q[:B].contiguous()
+    got = {}
+    for reuse in (1, 0):
+        ix.set_option(_lib.OPT_BAND_REUSE, reuse)
+        for skip in (1, 0):
+            ix.set_option(_lib.OPT_BAND_BLOCK_SKIP, skip)
+            s, i = ix.search(Qb, 100)
+            got[(reuse, skip)] = (s.clone(), i.clone(), ix.last_band.clone())
+    ix.set_option(_lib.OPT_BAND_REUSE, 1)
+    ix.set_option(_lib.OPT_BAND_BLOCK_SKIP, 1)
+    ref = got[(0, 0)]
+    assert (ref[2] > 100).all()                    # a real band beyond the top-k
+    for key, val in got.items():
+        for a, b, name in zip(val, ref, ("s", "i", "band")):
+            assert torch.equal(a, b), (key, name)
