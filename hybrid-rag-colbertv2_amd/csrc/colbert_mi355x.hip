@@ -800,6 +800,10 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // A wave waits only for what it reads or overwrites, so the partner waves
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
+#ifndef CBV2_SCAN_QSKIP
+#define CBV2_SCAN_QSKIP 1   // lab A/B builds set 0
+#endif
+constexpr bool kScanQSkip = CBV2_SCAN_QSKIP != 0;
 // AUX: the doc stream's cache policy (0 cached: the query groups of a chunk
 // share its tiles through L2; 2 non-temporal, for a launch of ONE query
 // group, where every byte is read once).
@@ -1009,6 +1013,26 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           ++ph_n;
         }
         const bool full = TPI * j + TPI <= dl_min;
+        // small shapes (QW <= 2, the B <= 8 launches): a wave's padded query
+        // slots (queries >= B) skip their MFMAs -- at B = 5 on the 4 x 2 shape
+        // 3 of 8 -- which at these batches, HBM- and power-bound, buy clock;
+        // the live queries' chains are the same instructions in the same order
+        const int nlive = QW <= 2 ? max(0, min(QW, B - (qg * QPB + wave * QW))) : QW;
+        if constexpr (kScanQSkip && QW <= 2 && !SPREAD && MORDER == 0) {
+          if (full) {
+            if (nlive == QW)
+              iter4_full<QW, D, NT, NoTileHook, PROBE>(buf, lane, qf, m);
+            else if (QW == 2 && nlive == 1)
+              iter4_full<1, D, NT, NoTileHook, PROBE>(buf, lane, reinterpret_cast<const bf16x8(&)[1][2][4]>(qf[0]),
+                                                    reinterpret_cast<float(&)[1][2]>(m[0]));
+          } else if (TPI * j < dl_max) {
+            if (nlive == QW)
+              iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
+            else if (QW == 2 && nlive == 1)
+              iter4_ragged<1, NT>(buf, lane, j, dl_g, dl_max, reinterpret_cast<const bf16x8(&)[1][2][4]>(qf[0]),
+                                  reinterpret_cast<float(&)[1][2]>(m[0]));
+          }
+        } else {
         if constexpr (SPREAD && NBUF == 2) {
           static_assert(NT >= kPiecesPerWave, "one piece per tile");
           if (it + 1 < nit && !full) issue(it + 1, nslot);   // ragged or empty iteration: all at once
@@ -1029,6 +1053,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           }
         } else if (TPI * j < dl_max)
           iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
+        }
         if (j == IPG - 1) {
           // doc 4G+g's score in every lane of group g; lane c of the 64-doc block
           // register keeps doc group c, so lane (c, g) holds doc 4c+g of the block
@@ -4587,8 +4612,9 @@ int pick_shape(const ShapeCost (&c)[N], int B) {
 // clock, and with the non-temporal doc stream of a one-group launch: 1M docs,
 // same process, B=4 5.98 (4 x 2) -> 4.92 (4 x 1) -> 4.62 ms (4 x 1, nt), B=3
 // 4.91 -> 4.62; profiles/r04m_lab_midbatch.log, r04n_lab_midbatch.log), 4 x 2
-// (6.1; nt for B = 5-8: B=8 6.39 -> 6.34), 4 x 4 (9.6; B=16 alone 10.6), 8 x 4
-// (17.4; B=256 = 8 groups 139 ms)
+// (6.1; nt for B = 5-8: B=8 6.39 -> 6.34; padded query slots skip their MFMAs:
+// B=5 5.92 -> 5.53, B=6 6.15 -> 5.81, profiles/r04p_lab_qskip.log), 4 x 4
+// (9.6; B=16 alone 10.6), 8 x 4 (17.4; B=256 = 8 groups 139 ms)
 constexpr ShapeCost kBf16Shapes[] = {
     {4, 4.6f, kScan16x4W4Q1}, {8, 6.1f, kScan16x4W4Q2}, {16, 9.6f, kScan16x4W4}, {32, 17.4f, kScan16x4W8}};
 
