@@ -3360,26 +3360,35 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 // already rescored by phase 1), lbu[b] = ~0 (the atomic-min of the bf16 top-k's
 // faithful scores, order-preserving bits) and done[b] = 0 (the fallback's
 // finished-workgroup counter) -- one launch fewer than separate memsets.
-__global__ __launch_bounds__(64) void split_query_kernel(const float* __restrict__ Q, int lq,
-                                                         uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
-                                                         float E, float M, float* __restrict__ beta,
-                                                         int32_t* __restrict__ count = nullptr,
-                                                         uint32_t* __restrict__ lbu = nullptr,
-                                                         int32_t* __restrict__ done = nullptr, int count0 = 0) {
-  const int b = blockIdx.x, lane = threadIdx.x, grp = lane >> 4, sub = lane & 15;
-  float acc = 0.0f;
-  for (int r = grp; r < lq; r += 4) {
+__global__ __launch_bounds__(512) void split_query_kernel(const float* __restrict__ Q, int lq,
+                                                          uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
+                                                          float E, float M, float* __restrict__ beta,
+                                                          int32_t* __restrict__ count = nullptr,
+                                                          uint32_t* __restrict__ lbu = nullptr,
+                                                          int32_t* __restrict__ done = nullptr, int count0 = 0) {
+  // one 16-lane group per query token (lq <= 32: one pass, no loop -- the B=1
+  // latency path waits on this launch); the per-token bound terms are summed
+  // in the order of the round-3 one-wave kernel (4 strided partial sums, then
+  // pairwise), so beta keeps its bits
+  __shared__ float s_t[kLqMax];
+  const int b = blockIdx.x, tid = threadIdx.x, r = tid >> 4, sub = tid & 15;
+  if (r < lq) {
     const size_t row = (size_t)b * lq + r;
     float xx, rr, hh;
     split_row8(Q + row * kDim, qhi + row * kDim, qlo + row * kDim, sub, xx, rr, hh);
     const float nq = sqrtf(xx) * kBoundUp, eq = sqrtf(rr) * kBoundUp;
-    acc += nq * E + eq * M + kAccSlack * (nq + eq) * M;
+    const float t = nq * E + eq * M + kAccSlack * (nq + eq) * M;
+    if (sub == 0) s_t[r] = t;
   }
-  acc = sub == 0 ? acc : 0.0f;
+  __syncthreads();
+  if (tid == 0) {
+    float a[4];
 #pragma unroll
-  for (int off = 16; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
-  if (lane == 0) {
-    beta[b] = acc * kBoundUp;
+    for (int g = 0; g < 4; ++g) {
+      a[g] = 0.0f;
+      for (int rr = g; rr < lq; rr += 4) a[g] += s_t[rr];
+    }
+    beta[b] = ((a[0] + a[1]) + (a[2] + a[3])) * kBoundUp;
     if (count != nullptr) count[b] = count0;
     if (lbu != nullptr) lbu[b] = 0xffffffffu;
     if (done != nullptr) done[b] = 0;
@@ -3572,7 +3581,8 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
     float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld,
-    uint32_t* __restrict__ lb_min, int64_t c0) {
+    uint32_t* __restrict__ lb_min, int64_t c0, float* __restrict__ fb_T = nullptr, int32_t* __restrict__ fb_done = nullptr,
+    int fb_k = 0, float* __restrict__ fb_s = nullptr, int32_t* __restrict__ fb_i = nullptr) {
   __shared__ float s_m[4][32];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -3582,6 +3592,33 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
   if (count != nullptr) {
     const int64_t cb = count[b];
     lim = cb < lim ? cb : lim;
+    if (fb_T != nullptr && cb > limit) {   // block-uniform: the row's band overflowed its capacity
+      // the full-scan fallback in this launch (fallback_split_kernel's work:
+      // every doc's faithful score into fb_T, then the row's last workgroup
+      // runs the exact top-k into fb_s / fb_i; band_select leaves such rows)
+      __shared__ uint64_t sel[kTopkMax];
+      __shared__ uint32_t hist[2048];
+      __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+      __shared__ int s_last;
+      bf16x8 qh[2][4], ql[2][4];
+      load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+      load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+      float* row = fb_T + (size_t)b * n;
+      for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {   // block-uniform
+        const float v = faithful_doc_split<LONG, NW>(hi, lo, c, ld, doclens[c], qh, ql, lane, wave, lq, s_m);
+        if (threadIdx.x == 0) row[c] = v;
+      }
+      __threadfence();   // this workgroup's scores, visible device-wide before it is counted
+      __syncthreads();
+      if (threadIdx.x == 0) s_last = atomicAdd(fb_done + b, 1) == (int)gridDim.x - 1;
+      __syncthreads();
+      if (!s_last) return;
+      __threadfence();   // every workgroup's scores of the row are in
+      const int kk = (int)((int64_t)fb_k < n ? fb_k : n);
+      topk_exact_row(row, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
+      sort_and_write(sel, kk, fb_k, id_base, fb_s + (size_t)b * fb_k, fb_i + (size_t)b * fb_k);
+      return;
+    }
   }
   if (c0 + (int64_t)blockIdx.x >= lim) return;  // block-uniform
   bf16x8 qh[2][4], ql[2][4];
@@ -4197,6 +4234,10 @@ __global__ __launch_bounds__(kTkThreads) void band_select_kernel(const float* __
   const int b = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
   const int total = count[b];
   const int cnt = total < cap ? total : cap;
+  if (total > cap) {   // block-uniform: the band overflowed -- the fallback writes this row
+    if (tid == 0) status[b] = -1;
+    return;
+  }
   for (int t = tid; t < cnt; t += nth)
     keys[t] = rank_key(F[(size_t)b * cap + t], (uint32_t)((int64_t)cand[(size_t)b * cap + t] - id_base));
   if (tid < 8) misc[tid] = 0;
@@ -5450,7 +5491,7 @@ int check_f32(cbv2_index* ix, int op, const float* Q, int32_t B, int32_t lq, int
 
 // (a SEARCH workspace's split also resets the rows' band state: count, lb, done)
 int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st, int count0 = 0) {
-  hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(64), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
+  hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(512), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
                      ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0);
   return launch_check("split_query_kernel");
 }
@@ -5461,21 +5502,24 @@ constexpr int64_t kRsSmallPairs = 4096;
 constexpr int64_t kRsSplitGrid = 1024;   // workgroups per row of a split rescoring launch (grid-stride beyond)
 int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t* cand, const int32_t* count,
                    int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
-                   const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr, int64_t c0 = 0) {
-  if (limit <= c0) return CBV2_OK;
+                   const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr, int64_t c0 = 0,
+                   float* fb_T = nullptr, int32_t* fb_done = nullptr, int fb_k = 0, float* fb_s = nullptr,
+                   int32_t* fb_i = nullptr) {
+  if (limit <= c0 && fb_T == nullptr) return CBV2_OK;
   if (ix->rescore_split) {   // one pair per workgroup (its doc split over 4 waves, or 2 for launches past
                              // the chip's resident 4-wave workgroups: one round of 2-wave ones instead of two)
-    const int64_t span = limit - c0;   // (pairs [c0, min(count, limit)) of a row)
+    int64_t span = limit - c0;   // (pairs [c0, min(count, limit)) of a row)
+    if (fb_T != nullptr) span = std::max<int64_t>(span, std::min<int64_t>(ix->n, 256));   // the fallback's grid
     const unsigned gx = (unsigned)(span < kRsSplitGrid ? span : kRsSplitGrid);
     const bool two = (int64_t)gx * B > 3LL * cu_count(ix->device);
     auto kern = ix->ld != kLd ? (two ? rescore_split_kernel<true, 2> : rescore_split_kernel<true, 4>)
                               : (two ? rescore_split_kernel<false, 2> : rescore_split_kernel<false, 4>);
     hipLaunchKernelGGL(kern, dim3(gx, (unsigned)B), dim3(two ? 128 : 256), 0, st, ix->tokens, ix->resid, ix->doclens,
                        ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out, only_neg,
-                       (int)ix->ld, lb_min, c0);
+                       (int)ix->ld, lb_min, c0, fb_T, fb_done, fb_k, fb_s, fb_i);
     return launch_check("rescore_split_kernel");
   }
-  if (c0 != 0) return fail(CBV2_EUNSUPPORTED, "pair offset needs the split rescoring");
+  if (c0 != 0 || fb_T != nullptr) return fail(CBV2_EUNSUPPORTED, "pair offset / fallback need the split rescoring");
   if (pw <= 0) pw = (int64_t)B * limit <= kRsSmallPairs ? 1 : kRsPerWave;
   const int64_t per_wg = 4LL * pw;
   int64_t gx = (limit + per_wg - 1) / per_wg;
@@ -6003,6 +6047,11 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
   // (count[b] was reset by the query split of phase 1: to k with the reuse)
   const bool reuse = lbu != nullptr && band_reuses_topk(ix, B, k);
   const int c0 = reuse ? k : 0;
+  // the band goes pair by pair (not fused with the collect, not doc-major):
+  // its rescoring launch also runs the overflow fallback (no separate launch)
+  const bool pair_path = !(B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused) &&
+                         !(ix->band_doc_major && B > kBandPairMaxB);
+  const bool fb_fused = pair_path && ix->rescore_split && k <= kTopkMax;
   int64_t splits = (8LL * cu_count(ix->device) + B - 1) / B;    // ~8 workgroups per CU
   const int64_t max_splits = (ix->n + 8191) / 8192;
   splits = splits < max_splits ? splits : max_splits;
@@ -6059,18 +6108,21 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
       if ((rc = launch_check("rescore_docs_kernel"))) return rc;
     }
   } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
-                                   B <= kBandPairMaxB ? 1 : 0, nullptr, c0))) {
+                                   B <= kBandPairMaxB ? 1 : 0, nullptr, c0, fb_fused ? w.T : nullptr,
+                                   fb_fused ? w.done : nullptr, k, out_scores, out_ids))) {
     return rc;
   }
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
                      ix->id_base, out_scores, out_ids, out_status, lb, lbu);
   if ((rc = launch_check("band_select_kernel"))) return rc;
   // rows whose band overflowed cap (status -1): the full faithful scan over
-  // every doc and an exact top-k, on the device (other rows exit at once)
+  // every doc and an exact top-k, on the device (other rows exit at once);
+  // pair-by-pair bands did it inside their rescoring launch already
+  if (fb_fused) return CBV2_OK;
   if (ix->rescore_split && k <= kTopkMax) {   // scan + top-k in one launch (last workgroup per row)
     // (a grid of this size is dispatched whether or not a row overflowed: it
     // stays small -- an overflowing row then takes a few ms)
-    const int64_t fb = std::max<int64_t>(64, 512 / B);
+    const int64_t fb = std::max<int64_t>(64, 256 / B);
     const unsigned gx = (unsigned)(ix->n < fb ? ix->n : fb);
     hipLaunchKernelGGL(ix->ld != kLd ? fallback_split_kernel<true> : fallback_split_kernel<false>, dim3(gx, (unsigned)B),
                        dim3(256), 0, st, ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w.qhi, w.qlo, lq,
