@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 #include <stdio.h>
 #include <string.h>
@@ -1017,21 +1018,24 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
         // slots (queries >= B) skip their MFMAs -- at B = 5 on the 4 x 2 shape
         // 3 of 8 -- which at these batches, HBM- and power-bound, buy clock;
         // the live queries' chains are the same instructions in the same order
-        const int nlive = QW <= 2 ? max(0, min(QW, B - (qg * QPB + wave * QW))) : QW;
-        if constexpr (kScanQSkip && QW <= 2 && !SPREAD && MORDER == 0) {
-          if (full) {
-            if (nlive == QW)
-              iter4_full<QW, D, NT, NoTileHook, PROBE>(buf, lane, qf, m);
-            else if (QW == 2 && nlive == 1)
-              iter4_full<1, D, NT, NoTileHook, PROBE>(buf, lane, reinterpret_cast<const bf16x8(&)[1][2][4]>(qf[0]),
-                                                    reinterpret_cast<float(&)[1][2]>(m[0]));
-          } else if (TPI * j < dl_max) {
-            if (nlive == QW)
-              iter4_ragged<QW, NT>(buf, lane, j, dl_g, dl_max, qf, m);
-            else if (QW == 2 && nlive == 1)
-              iter4_ragged<1, NT>(buf, lane, j, dl_g, dl_max, reinterpret_cast<const bf16x8(&)[1][2][4]>(qf[0]),
-                                  reinterpret_cast<float(&)[1][2]>(m[0]));
-          }
+        // (the 4 x 4 shape too, B = 9-16; never the 8 x 4 shape of large batches)
+        constexpr bool kSkipShape = QW <= 2 || (QW == 4 && WAVES == 4);
+        const int nlive = kSkipShape ? max(0, min(QW, B - (qg * QPB + wave * QW))) : QW;
+        if constexpr (kScanQSkip && kSkipShape && !SPREAD && MORDER == 0) {
+          // the first nlive query slots of the wave, as arrays of their own
+          auto live = [&](auto nq) {
+            constexpr int L = decltype(nq)::value;
+            auto& q = reinterpret_cast<const bf16x8(&)[L][2][4]>(qf[0]);
+            auto& mm = reinterpret_cast<float(&)[L][2]>(m[0]);
+            if (full)
+              iter4_full<L, D, NT, NoTileHook, PROBE>(buf, lane, q, mm);
+            else if (TPI * j < dl_max)
+              iter4_ragged<L, NT>(buf, lane, j, dl_g, dl_max, q, mm);
+          };
+          if (nlive == QW) live(std::integral_constant<int, QW>{});
+          else if (QW >= 4 && nlive == 3) live(std::integral_constant<int, (QW >= 4 ? 3 : 1)>{});
+          else if (QW >= 3 && nlive == 2) live(std::integral_constant<int, (QW >= 3 ? 2 : 1)>{});
+          else if (QW >= 2 && nlive == 1) live(std::integral_constant<int, 1>{});
         } else {
         if constexpr (SPREAD && NBUF == 2) {
           static_assert(NT >= kPiecesPerWave, "one piece per tile");
@@ -4604,7 +4608,7 @@ enum ScanVariant {
   kScanStreamQ1 = 14, kScanStreamQ2 = 15, kScanStreamQ1Cached = 16, kScanStreamQ1W8 = 17, kScanStreamQ4 = 18,
   kScanStreamQ8 = 19, kScanStreamQ1Tw2 = 20, kScanStreamQ2Tw2 = 21, kScanPairQ1 = 22, kScanPairQ2 = 23,
   kScanPairQ4 = 24, kScanStreamQ4Pf = 25, kScanStreamQ1Pf = 26, kScanStreamQ2Pf = 27, kScan16x4W4Q1 = 28,
-  kScan16x4W8Q1 = 30, kScan16x4W8Q1x2 = 31, kScan16x4W4Q1Nt = 33, kScan16x4W4Q2Nt = 34,
+  kScan16x4W8Q1 = 30, kScan16x4W8Q1x2 = 31, kScan16x4W4Q1Nt = 33, kScan16x4W4Q2Nt = 34, kScan16x4W4Nt = 35,
   kScanAuto = -1
 };
 // Measured (tools/scan_lab.py, 200k docs, B=256, one MI355X): 0: 54.8 %,
@@ -4655,7 +4659,9 @@ int pick_shape(const ShapeCost (&c)[N], int B) {
 // 4.91 -> 4.62; profiles/r04m_lab_midbatch.log, r04n_lab_midbatch.log), 4 x 2
 // (6.1; nt for B = 5-8: B=8 6.39 -> 6.34; padded query slots skip their MFMAs:
 // B=5 5.92 -> 5.53, B=6 6.15 -> 5.81, profiles/r04p_lab_qskip.log), 4 x 4
-// (9.6; B=16 alone 10.6), 8 x 4 (17.4; B=256 = 8 groups 139 ms)
+// (9.6; B=16 alone 10.6; nt and padded-slot skipping for B <= 16: B=9 9.61 ->
+// 8.60, B=12 10.05 -> 9.44, B=16 10.64 -> 10.56, profiles/r04s_lab.log), 8 x 4
+// (17.4; B=256 = 8 groups 139 ms)
 constexpr ShapeCost kBf16Shapes[] = {
     {4, 4.6f, kScan16x4W4Q1}, {8, 6.1f, kScan16x4W4Q2}, {16, 9.6f, kScan16x4W4}, {32, 17.4f, kScan16x4W8}};
 
@@ -4972,6 +4978,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16x4W4Q2Nt:
       return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
           ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
+    case kScan16x4W4Nt:     // lab: 4 x 4 with the non-temporal doc stream (B <= 16: one query group)
+      return launch_scan16x4<4, 4, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+          ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs, nullptr, ctr_ws);
     case kScan16x4W8Q1:     // lab: 8 queries per workgroup, one per wave (2 waves per SIMD)
       return launch_scan16x4<8, 1, 1, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
                                                    nullptr, ctr_ws);
@@ -5007,6 +5016,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac,
                                                                           kScanTaskDocs, nullptr, ctr_ws);
     case kScan16x4W4:
+      if (B <= 16)          // one query group: non-temporal doc stream
+        return launch_scan16x4<4, 4, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs, nullptr, ctr_ws);
       return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs,
                                                    nullptr, ctr_ws);
     case kScan16x4W4Q2:   // 8 queries per workgroup (2 per wave)
