@@ -4489,7 +4489,11 @@ struct cbv2_index {
   int fused_topk_mode = 0;   // its value (2: also the MXFP8 scan, A/B only)
   int dynamic_tail = 1;      // CBV2_OPT_DYNAMIC_TAIL (1: XCD-sliced tail, 2: one shared tail, 0: off)
   int topk_bmax = 1;         // CBV2_OPT_TOPK_BMAX (1: block-max top-k where eligible, 0: sampled filter + select)
-  int band_doc_major = 1;    // CBV2_OPT_BAND_DOC_MAJOR (2: pair-outer variant, A/B)
+  // CBV2_OPT_BAND_DOC_MAJOR: 0 pair by pair (round 4 default: with the split
+  // rescoring the pair-by-pair gather beats grouping by doc -- band 2.64 vs
+  // 2.78 ms at B=256, 0.72 vs 0.85 at 64, 0.22 vs 0.31 at 16, 1M docs,
+  // profiles/r04u_band_ab.jsonl); 1 / 2 / 3 / 4 doc-major kernels (A/B)
+  int band_doc_major = 0;
   bool band_lower_bound = true;  // CBV2_OPT_BAND_LOWER_BOUND
   // CBV2_OPT_BAND_FUSED (B <= 8: collect + rescore in one launch): off -- the
   // band collect (7.4 us) + the split rescoring (one band doc per workgroup)

@@ -122,14 +122,13 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
  *                        as dynamic tasks, in 8 XCD-local slices (2: one
  *                        shared tail; 0: static chunks only).
- *  CBV2_OPT_BAND_DOC_MAJOR 1: cbv2_search_f32 rescores the band of a batch
- *                        of more than 8 queries grouped by doc (each band doc
- *                        read once per batch; 0: pair by pair; smaller
- *                        batches always go pair by pair, one band doc per
- *                        wave).  Doc-major kernels: 1 one wave per doc, its
- *                        halves in turn; 2 the same, pair-outer; 3 / 4 one
- *                        doc per workgroup of 4 / 2 waves (128-slot docs;
- *                        others take 1).  Identical results either way.
+ *  CBV2_OPT_BAND_DOC_MAJOR 0 (default): cbv2_search_f32 rescores the band
+ *                        pair by pair (one (query, doc) pair per workgroup);
+ *                        1-4: a batch of more than 8 queries grouped by doc
+ *                        (each band doc read once per batch) -- 1 one wave
+ *                        per doc, its halves in turn; 2 the same, pair-outer;
+ *                        3 / 4 one doc per workgroup of 4 / 2 waves (128-slot
+ *                        docs; others take 1).  Identical results either way.
  *  CBV2_OPT_BAND_LOWER_BOUND 1: cbv2_search_f32 first rescores the bf16
  *                        top-k, whose minimum faithful score lb bounds the
  *                        k-th from below, and bands T >= lb - beta (0: the
