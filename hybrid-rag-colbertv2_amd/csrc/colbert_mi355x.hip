@@ -4503,6 +4503,7 @@ struct cbv2_index {
   bool rescore_split = true;     // CBV2_OPT_RESCORE_SPLIT (one pair per workgroup, rows over 4 waves)
   bool band_reuse = true;        // CBV2_OPT_BAND_REUSE (the band's first k slots: phase 1's top-k scores)
   bool band_block_skip = true;   // CBV2_OPT_BAND_BLOCK_SKIP (the collect reads only blocks whose max reaches it)
+  int rescore_grid = 0;          // CBV2_OPT_RESCORE_GRID (workgroups per row of a split rescoring; 0: 1024)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -5526,7 +5527,13 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
                              // the chip's resident 4-wave workgroups: one round of 2-wave ones instead of two)
     int64_t span = limit - c0;   // (pairs [c0, min(count, limit)) of a row)
     if (fb_T != nullptr) span = std::max<int64_t>(span, std::min<int64_t>(ix->n, 256));   // the fallback's grid
-    const unsigned gx = (unsigned)(span < kRsSplitGrid ? span : kRsSplitGrid);
+    // workgroups per row: ~4k per launch, 256..1024 per row -- a row's pairs
+    // beyond that grid-stride (band at 1M docs, grid 1024 / 512 / 256: B=256
+    // 2.76 / 2.64 / 2.57 ms, B=16 0.247 / 0.238 / 0.225, B=1 39 / 40 / 41 us;
+    // profiles/r04w_grid_ab.jsonl)
+    const int64_t grid_auto = std::min<int64_t>(kRsSplitGrid, std::max<int64_t>(256, 4096 / std::max(B, 1)));
+    const int64_t grid_max = ix->rescore_grid > 0 ? ix->rescore_grid : grid_auto;
+    const unsigned gx = (unsigned)(span < grid_max ? span : grid_max);
     const bool two = (int64_t)gx * B > 3LL * cu_count(ix->device);
     auto kern = ix->ld != kLd ? (two ? rescore_split_kernel<true, 2> : rescore_split_kernel<true, 4>)
                               : (two ? rescore_split_kernel<false, 2> : rescore_split_kernel<false, 4>);
@@ -5828,6 +5835,10 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
       return CBV2_OK;
     case CBV2_OPT_BAND_BLOCK_SKIP:
       ix->band_block_skip = value != 0;
+      return CBV2_OK;
+    case CBV2_OPT_RESCORE_GRID:
+      if (value < 0 || value > 65535) return fail(CBV2_EINVAL, "rescore grid must be in [0, 65535]");
+      ix->rescore_grid = (int)value;
       return CBV2_OK;
     default:
       return fail(CBV2_EINVAL, "unknown option %d", option);

@@ -151,6 +151,10 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        the 64-doc blocks whose maximum (left by the
  *                        block-max top-k) reaches the band threshold (0: the
  *                        whole score row).  Identical results.
+ *  CBV2_OPT_RESCORE_GRID  workgroups per row of a split rescoring launch (0:
+ *                        automatic, 4096 / B within [256, 1024]; rows with
+ *                        more pairs grid-stride).
+ *                        Identical results.
  *  CBV2_OPT_TOPK_BMAX    1: cbv2_search's unfused MaxSim scan (rows of >= 65,536
  *                        and <= 1,572,864 docs, k <= 1024) also folds the max of
  *                        every 64-doc block, and ONE select launch reads only
@@ -170,6 +174,7 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_RESCORE_SPLIT 7
 #define CBV2_OPT_BAND_REUSE 8
 #define CBV2_OPT_BAND_BLOCK_SKIP 9
+#define CBV2_OPT_RESCORE_GRID 10
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

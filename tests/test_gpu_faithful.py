@@ -400,3 +400,26 @@ def test_band_block_skip_equals_full_row(dev, bmax_corpus, B):
     for key, val in got.items():
         for a, b, name in zip(val, ref, ("s", "i", "band")):
             assert torch.equal(a, b), (key, name)
+
+
+@pytest.mark.parametrize("B", [1, 12])
+def test_rescore_grid_equals_default(dev, B):
+    """CBV2_OPT_RESCORE_GRID: fewer workgroups per row grid-stride over the
+    row's pairs (band, top-k rescoring, forced overflow fallback, rerank): the
+    same bits as the automatic grid."""
+    docs, doclens, Q = make_case(77 + B, 5000, B, 32)
+    ix = ColbertIndex.faithful_f32(docs.to(dev), doclens.to(dev), id_base=2)
+    Qd = Q.to(dev)
+    cand = torch.randint(0, 5002, (B, 50), generator=torch.Generator().manual_seed(B), dtype=torch.int32).to(dev)
+    got = {}
+    for grid in (0, 7, 64):
+        ix.set_option(_lib.OPT_RESCORE_GRID, grid)
+        s, i = ix.search(Qd, 100)
+        band = ix.last_band.clone()
+        sc, si = ix._search_f32(Qd.contiguous(), B, 32, 100, cap=100)     # forces the fallback
+        rs, ri, rp = ix.rerank(Qd, cand, 10)
+        got[grid] = [x.clone() for x in (s, i, band, sc, si, rs, ri, rp)]
+    ix.set_option(_lib.OPT_RESCORE_GRID, 0)
+    for grid in (7, 64):
+        for a, b, name in zip(got[grid], got[0], ("s", "i", "band", "sc", "si", "rs", "ri", "rp")):
+            assert torch.equal(a, b), (grid, name)
