@@ -4503,7 +4503,11 @@ struct cbv2_index {
   bool rescore_split = true;     // CBV2_OPT_RESCORE_SPLIT (one pair per workgroup, rows over 4 waves)
   bool band_reuse = true;        // CBV2_OPT_BAND_REUSE (the band's first k slots: phase 1's top-k scores)
   bool band_block_skip = true;   // CBV2_OPT_BAND_BLOCK_SKIP (the collect reads only blocks whose max reaches it)
-  int rescore_grid = 0;          // CBV2_OPT_RESCORE_GRID (workgroups per row of a split rescoring; 0: 1024)
+  int rescore_grid = 0;          // CBV2_OPT_RESCORE_GRID (workgroups per row of a split rescoring; 0: automatic)
+  // CBV2_OPT_DENSE_DOCS: the docs fill (nearly) all 128 token slots -- B <= 2
+  // then runs the 4 x 1 non-temporal scan (every slot streamed, 7.1 TB/s)
+  // instead of the streaming scan that skips empty tiles (6.9 TB/s)
+  bool dense_docs = false;
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -4923,7 +4927,8 @@ int scan_maxsim_long(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* ou
 // of the block-max top-k into their epilogue (scan_folds_bmax); other scans
 // ignore it.
 bool scan_folds_bmax(const cbv2_index* ix, int B) {
-  return ix->dtype == CBV2_DTYPE_BF16 && ix->ld == kLd && B <= kDirectMaxB && kDefaultScan == kScanAuto;
+  return ix->dtype == CBV2_DTYPE_BF16 && ix->ld == kLd && B <= kDirectMaxB && kDefaultScan == kScanAuto &&
+         !ix->dense_docs;
 }
 int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                 int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr, uint32_t* bm = nullptr) {
@@ -4937,7 +4942,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
                                                                                kScanDynFrac, kScanTaskDocs, nullptr,
                                                                                ctr_ws, ft);
   if (variant == kScanAuto) {
-    if (B <= kDirectMaxB)
+    // dense docs: B <= 2 takes the 4 x 1 shape below (bm == nullptr: its
+    // caller runs the block maxima, scan_folds_bmax)
+    if (B <= kDirectMaxB && !ix->dense_docs)
       return B == 1 ? launch_stream<1, 2>(ix, Q, B, lq, out, ld_out, st, bm)
                     : launch_stream<2, 2>(ix, Q, B, lq, out, ld_out, st, bm);
     variant = pick_shape(kBf16Shapes, B);
@@ -5835,6 +5842,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
       return CBV2_OK;
     case CBV2_OPT_BAND_BLOCK_SKIP:
       ix->band_block_skip = value != 0;
+      return CBV2_OK;
+    case CBV2_OPT_DENSE_DOCS:
+      ix->dense_docs = value != 0;
       return CBV2_OK;
     case CBV2_OPT_RESCORE_GRID:
       if (value < 0 || value > 65535) return fail(CBV2_EINVAL, "rescore grid must be in [0, 65535]");

@@ -155,6 +155,13 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        automatic, 4096 / B within [256, 1024]; rows with
  *                        more pairs grid-stride).
  *                        Identical results.
+ *  CBV2_OPT_DENSE_DOCS    1: the docs fill (nearly) all 128 token slots, so
+ *                        searches of B <= 2 stream every slot on the 4-wave
+ *                        x 1-query scan (non-temporal) instead of the
+ *                        streaming scan that skips empty 16-token tiles
+ *                        (0, the default; the Python ColbertIndex sets it
+ *                        when >= 98 % of the tiles hold tokens).  Identical
+ *                        results.
  *  CBV2_OPT_TOPK_BMAX    1: cbv2_search's unfused MaxSim scan (rows of >= 65,536
  *                        and <= 1,572,864 docs, k <= 1024) also folds the max of
  *                        every 64-doc block, and ONE select launch reads only
@@ -175,6 +182,7 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_BAND_REUSE 8
 #define CBV2_OPT_BAND_BLOCK_SKIP 9
 #define CBV2_OPT_RESCORE_GRID 10
+#define CBV2_OPT_DENSE_DOCS 11
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

@@ -521,3 +521,31 @@ def test_long_queries_sum_of_blocks(dev, lq, B):
         exp = orc.rerank_select(raw[b], 10)
         assert [int(x) for x in rp[b].cpu()] == [e[0] for e in exp], b
         assert [int(x) for x in ri[b].cpu()] == [int(cand[b, e[0]]) for e in exp], b
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_dense_docs_scan_equals_stream(dev, B):
+    """CBV2_OPT_DENSE_DOCS (set by ColbertIndex when >= 98 % of the 16-token
+    tiles hold tokens): B <= 2 streams every slot on the 4 x 1 doc-interleaved
+    scan instead of the tile-skipping streaming scan, the block-max top-k then
+    runs its own block maxima.  Scores and top-k equal the streaming scan's bit
+    for bit; a ragged index keeps the streaming scan."""
+    from hybrid_rag_colbertv2_amd import _lib, synth
+    n = 70_000                                    # past the block-max select's threshold
+    Qf = synth.make_queries(B, 32, seed=3)
+    planted = synth.planted_ids(B, n, 10, seed=4)
+    tok, dl = synth.make_shard(0, n, Qf, planted, dev, seed=5)
+    dl[::50] = 120                                 # 2 % of the docs one tile short: still dense
+    ix = ColbertIndex(tok, dl, id_base=11)
+    assert ix.dense_docs
+    Q = Qf.to(dev, torch.bfloat16)
+    got = {}
+    for dense in (1, 0):
+        ix.set_option(_lib.OPT_DENSE_DOCS, dense)
+        s, i = ix.search(Q, 100)
+        got[dense] = (s.clone(), i.clone(), ix.score(Q).clone())
+    for a, b in zip(got[1], got[0]):
+        assert torch.equal(a, b)
+    dl2 = dl.clone()
+    dl2[::3] = 40
+    assert not ColbertIndex(tok, dl2).dense_docs
