@@ -4978,6 +4978,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_pair<2>(ix, Q, B, lq, out, ld_out, st);
     case kScanPairQ4:
       return launch_pair<4>(ix, Q, B, lq, out, ld_out, st);
+    // lab, round 4, 1M docs, same process (profiles/r04l_lab_midbatch.log): the
+    // prefetching stream 5.78 vs 5.82 ms at B=4, 4.76 vs 4.78 at B=1 -- not
+    // kept; 8 waves x 1 query (30 / 31) 7.1-7.6 ms at B=5-8 vs 4 x 2's 6.1-6.4
     case kScanStreamQ4Pf:   // lab: the next tile's fragments read under this tile's MFMAs
       return launch_stream<4, 2, 4, kStreamSlots, false, true>(ix, Q, B, lq, out, ld_out, st);
     case kScanStreamQ1Pf:
