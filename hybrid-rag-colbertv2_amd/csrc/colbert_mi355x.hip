@@ -1920,7 +1920,7 @@ __device__ __forceinline__ void iter_f8x4_ragged(const uint8_t* buf, int lane, i
 // 0 .. WAVES/2 - 1 issue the DMA pieces (+0.2 %, within noise, 4 VGPR spills).
 template <int WAVES, int QW, int D = 1, int NBUF = 3, int TPI = 32, bool PF = false, int OCC = 2,   // D = 2 spills at QW = 8
           int FK = 0, int LD = kLd, bool PQS = false, bool PAIR = false, bool SPREAD2 = false, bool SPLIT = false,
-          bool QUAD = false, int PROBE = 0>
+          bool QUAD = false, int PROBE = 0, int AUX = 0>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
@@ -1995,13 +1995,13 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       const uint32_t off = (R % TPI) * kDim + 16 * ((lane & 7) ^ swz_f8<TPI>(R));
       const int d = clamp_doc(4 * G + 8 * piece / TPI);
       const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kDim + off;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + piece * 1024), 16, 0, AUX);
     }
     if (wave < kScaleDma) {  // scale bytes b = 256 * wave + 4L: row b/2 = TPI * doc + token
       const int R = (256 * wave + 4 * lane) / 2;
       const int d = clamp_doc(4 * G + R / TPI);
       const uint8_t* src = tscales + (size_t)(d_begin + d) * kScaleStride + (size_t)(j * TPI + R % TPI) * 2;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + kIterBytes + 256 * wave), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(sbuf + kIterBytes + 256 * wave), 4, 0, AUX);
     }
   };
   // vector-memory ops per wave per iteration (the vmcnt that leaves one iteration in flight)
@@ -2031,10 +2031,31 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
 #pragma unroll
       for (int q = 0; q < QW; ++q) m[q][0] = m[q][1] = neg_inf();
     }
-    if (TPI * j + TPI <= dl_min)
-      iter_f8x4_full<QW, D, TPI, PF, PQS, PROBE == 1 ? 1 : 0>(buf, lane, qa, qsv, m);
-    else if (TPI * j < dl_max)
-      iter_f8x4_ragged<QW, TPI, PQS>(buf, lane, j, dl_g, dl_max, qa, qsv, m);
+    // the 4-wave shapes of batches <= 16: a wave's padded query slots (>= B)
+    // skip their MFMAs, as in maxsim_scan16x4_kernel (same chains, same order)
+    constexpr bool kSkipF8 = kScanQSkip && WAVES == 4 && (QW <= 2 || QW == 4) && PROBE == 0 && FK == 0;
+    if constexpr (kSkipF8) {
+      const int nlive = max(0, min(QW, B - (qg * QPB + wave * QW)));
+      auto live = [&](auto nq) {
+        constexpr int L = decltype(nq)::value;
+        constexpr int DL = (2 * L) % (D + 1) == 0 ? D : 1;   // the accumulator ring must divide the chains
+        auto& q = reinterpret_cast<const i32x8(&)[L][2]>(qa[0]);
+        auto& mm = reinterpret_cast<float(&)[L][2]>(m[0]);
+        if (TPI * j + TPI <= dl_min)
+          iter_f8x4_full<L, DL, TPI, PF, PQS, 0>(buf, lane, q, qsv, mm);
+        else if (TPI * j < dl_max)
+          iter_f8x4_ragged<L, TPI, PQS>(buf, lane, j, dl_g, dl_max, q, qsv, mm);
+      };
+      if (nlive == QW) live(std::integral_constant<int, QW>{});
+      else if (QW >= 4 && nlive == 3) live(std::integral_constant<int, (QW >= 4 ? 3 : 1)>{});
+      else if (QW >= 3 && nlive == 2) live(std::integral_constant<int, (QW >= 3 ? 2 : 1)>{});
+      else if (QW >= 2 && nlive == 1) live(std::integral_constant<int, 1>{});
+    } else {
+      if (TPI * j + TPI <= dl_min)
+        iter_f8x4_full<QW, D, TPI, PF, PQS, PROBE == 1 ? 1 : 0>(buf, lane, qa, qsv, m);
+      else if (TPI * j < dl_max)
+        iter_f8x4_ragged<QW, TPI, PQS>(buf, lane, j, dl_g, dl_max, qa, qsv, m);
+    }
     if (j == IPG - 1) {
 #pragma unroll
       for (int q = 0; q < QW; ++q) {
@@ -5059,7 +5080,11 @@ constexpr int kF8SmallMaxB = 8;
 // CU (18.2; B=256 = 4 groups 72.5).  Against the 8 x 8 shape for every B > 8
 // (round 1): B=16 17.93 -> 5.81 ms, B=32 18.45 -> 10.77, B=48 19.63 -> 16.88
 // (lab r02ad), B=80 35.1 -> 26.2 (r02af).
-constexpr ShapeCost kF8Shapes[] = {{8, 3.0f, 9}, {16, 5.2f, 7}, {32, 9.5f, 8}, {64, 18.2f, 5}};
+// round 4: 24 = 4 waves x 1 query, non-temporal (B = 3-4: 3.14 -> 2.49 ms at
+// B=4, 2.79 -> 2.38 at B=3, 1M docs; the one-group launches of 9 and 7 stream
+// non-temporally and skip padded slots: B=5 3.50 -> 3.40, B=12 5.30 -> 5.08;
+// profiles/r04aa_lab_f8_midbatch.log)
+constexpr ShapeCost kF8Shapes[] = {{4, 2.45f, 24}, {8, 3.0f, 9}, {16, 5.2f, 7}, {32, 9.5f, 8}, {64, 18.2f, 5}};
 constexpr int kF8Waves = 8, kF8QW = 8;
 // Fold distance of the doc-interleaved f8 scans: a chain's row max is folded
 // 3 MFMAs after it issues (no MFMA -> VALU hazard pads: 122 -> 36 s_nop per
@@ -5083,7 +5108,7 @@ constexpr float kF8DynB8 = 0.3f;      // shape 9
 // launch-bounds occupancy hint (production: 8 waves x 8 queries, one per CU).
 template <int TPI, int NBUF, bool PF = false, int QW = kF8QW, int PER_CU = 1, int OCC = 2, int WAVES = kF8Waves,
           int FK = 0, int LD = kLd, int D = 1, bool PQS = false, bool PAIR = false, bool SPREAD2 = false,
-          bool SPLIT = false, bool QUAD = false, int PROBE = 0>
+          bool SPLIT = false, bool QUAD = false, int PROBE = 0, int AUX = 0>
 int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int lq, float* out, int64_t ld_out,
                 hipStream_t st, float dyn_frac, int task_docs, int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
   constexpr int QPB = WAVES * QW;
@@ -5096,7 +5121,8 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
-  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT, QUAD, PROBE>),
+  hipLaunchKernelGGL((maxsim_scan_f8x4_kernel<WAVES, QW, D, NBUF, TPI, PF, OCC, FK, LD, PQS, PAIR, SPREAD2, SPLIT, QUAD, PROBE,
+                                              AUX>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
                      sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
@@ -5205,12 +5231,23 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     // workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two per CU
     // (2 waves per SIMD from independent barrier domains); 9 = 2 queries per
     // wave, two per CU
-    case 7: return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
-                                                                            frac(kF8DynSmall), task_docs, ctr_ws);
+    case 7:
+      if (B <= 16)   // one query group: non-temporal doc stream
+        return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true, false, false, false, false, 0, 2>(
+            ix, Qb, Qs, B, lq, out, ld_out, st, frac(kF8DynSmall), task_docs, ctr_ws);
+      return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                     frac(kF8DynSmall), task_docs, ctr_ws);
     case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
                                                                             frac(kF8DynSmall), task_docs, ctr_ws);
-    case 9: return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
-                                                                            frac(kF8DynB8), task_docs, ctr_ws);
+    case 9:
+      if (B <= 8)    // one query group: non-temporal doc stream
+        return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true, false, false, false, false, 0, 2>(
+            ix, Qb, Qs, B, lq, out, ld_out, st, frac(kF8DynB8), task_docs, ctr_ws);
+      return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                     frac(kF8DynB8), task_docs, ctr_ws);
+    // 24 = 1 query per wave, two per CU (B = 3-4 without padded slots), non-temporal
+    case 24: return launch_f8x4<32, 3, true, 1, 2, 2, 4, 0, kLd, 1, true, false, false, false, false, 0, 2>(
+        ix, Qb, Qs, B, lq, out, ld_out, st, frac(kF8DynB8), task_docs, ctr_ws);
     // 12 = shape 5 before PAIR: one 32-token iteration per barrier, 3-deep ring
     case 12: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
