@@ -4526,8 +4526,9 @@ struct cbv2_index {
   bool band_block_skip = true;   // CBV2_OPT_BAND_BLOCK_SKIP (the collect reads only blocks whose max reaches it)
   int rescore_grid = 0;          // CBV2_OPT_RESCORE_GRID (workgroups per row of a split rescoring; 0: automatic)
   // CBV2_OPT_DENSE_DOCS: the docs fill (nearly) all 128 token slots -- B <= 2
-  // then runs the 4 x 1 non-temporal scan (every slot streamed, 7.1 TB/s)
-  // instead of the streaming scan that skips empty tiles (6.9 TB/s)
+  // then runs the 4 x 1 non-temporal scan (every slot streamed, 7.1 TB/s;
+  // MXFP8 its 4 x 1 shape) instead of the streaming scan that skips empty
+  // tiles (6.9 TB/s)
   bool dense_docs = false;
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
@@ -5190,8 +5191,10 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
     return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st,
                                                                       frac(kScanDynFrac), task_docs, ctr_ws, ft);
-  if (B > kF8DirectMaxB && shape == 0) shape = pick_shape(kF8Shapes, B);
+  // dense docs (CBV2_OPT_DENSE_DOCS): B <= 2 too on the 4 x 1 shape (every slot streamed)
+  if ((B > kF8DirectMaxB || ix->dense_docs) && shape == 0) shape = pick_shape(kF8Shapes, B);
   if (B <= kF8DirectMaxB && shape == 0) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
+  if (B <= kF8DirectMaxB && shape == 25) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<4, 16, false>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 21) return launch_f8_stream<16, 4, false>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   // lab: one tile per wait (the production 8 x 8 ring before TW2) / TW2 at 4 x 16

@@ -221,7 +221,7 @@ class ColbertIndex:
         # docs filling >= 98 % of their 16-token tiles: B <= 2 streams every
         # slot (CBV2_OPT_DENSE_DOCS); one small reduction at build time
         self.dense_docs = False
-        if not self.fp8 and self.ld == 128 and self.n > 0:
+        if self.ld == 128 and self.n > 0:
             tiles = int(((self.doclens.clamp(0, self.ld) + 15) // 16).sum().item())
             self.dense_docs = tiles >= 0.98 * self.n * (self.ld // 16)
             if self.dense_docs:

@@ -523,12 +523,12 @@ def test_long_queries_sum_of_blocks(dev, lq, B):
         assert [int(x) for x in ri[b].cpu()] == [int(cand[b, e[0]]) for e in exp], b
 
 
-@pytest.mark.parametrize("B", [1, 2])
-def test_dense_docs_scan_equals_stream(dev, B):
+@pytest.mark.parametrize("B,fp8", [(1, False), (2, False), (1, True), (2, True)])
+def test_dense_docs_scan_equals_stream(dev, B, fp8):
     """CBV2_OPT_DENSE_DOCS (set by ColbertIndex when >= 98 % of the 16-token
     tiles hold tokens): B <= 2 streams every slot on the 4 x 1 doc-interleaved
-    scan instead of the tile-skipping streaming scan, the block-max top-k then
-    runs its own block maxima.  Scores and top-k equal the streaming scan's bit
+    scan (bf16 or MXFP8) instead of the tile-skipping streaming scan, the
+    block-max top-k then runs its own block maxima.  Scores and top-k equal the streaming scan's bit
     for bit; a ragged index keeps the streaming scan."""
     from hybrid_rag_colbertv2_amd import _lib, synth
     n = 70_000                                    # past the block-max select's threshold
@@ -536,7 +536,7 @@ def test_dense_docs_scan_equals_stream(dev, B):
     planted = synth.planted_ids(B, n, 10, seed=4)
     tok, dl = synth.make_shard(0, n, Qf, planted, dev, seed=5)
     dl[::50] = 120                                 # 2 % of the docs one tile short: still dense
-    ix = ColbertIndex(tok, dl, id_base=11)
+    ix = ColbertIndex.mxfp8(tok, dl, id_base=11) if fp8 else ColbertIndex(tok, dl, id_base=11)
     assert ix.dense_docs
     Q = Qf.to(dev, torch.bfloat16)
     got = {}
@@ -548,4 +548,4 @@ def test_dense_docs_scan_equals_stream(dev, B):
         assert torch.equal(a, b)
     dl2 = dl.clone()
     dl2[::3] = 40
-    assert not ColbertIndex(tok, dl2).dense_docs
+    assert not (ColbertIndex.mxfp8(tok, dl2) if fp8 else ColbertIndex(tok, dl2)).dense_docs
