@@ -549,3 +549,31 @@ def test_dense_docs_scan_equals_stream(dev, B, fp8):
     dl2 = dl.clone()
     dl2[::3] = 40
     assert not (ColbertIndex.mxfp8(tok, dl2) if fp8 else ColbertIndex(tok, dl2)).dense_docs
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("dense", [False, True])
+@pytest.mark.parametrize("B", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 15, 16])
+def test_small_batch_shapes_match_oracle(dev, B, dense, fp8):
+    """Every small-batch scan shape (round 4): B <= 2 streaming scan (ragged)
+    or 4 x 1 non-temporal scan (dense docs), 4 x 1 for 3-4, 4 x 2 for 5-8 and
+    4 x 4 for 9-16 (one query group, non-temporal, padded query slots skipping
+    their MFMAs), bf16 and MXFP8 -- each row's scores equal the same query
+    scored alone (B = 1: another shape) bit for bit; bf16 against the oracle,
+    and padding rows with garbage never change a score."""
+    docs, doclens, Q = make_case(4000 + B + 97 * dense, 900, B, 32, ragged=not dense)
+    Qd = Q.to(dev)
+    ix = ColbertIndex.mxfp8(docs.to(dev), doclens.to(dev)) if fp8 else ColbertIndex(docs.to(dev), doclens.to(dev))
+    assert ix.dense_docs == dense
+    got = ix.score(Qd)
+    for b in sorted({0, B // 2, B - 1}):
+        assert torch.equal(got[b:b + 1], ix.score(Qd[b:b + 1].contiguous())), b
+    if fp8:
+        return
+    got = got.cpu()
+    ref = orc.maxsim(Q.float().numpy(), docs.float().numpy(), doclens.numpy())
+    np.testing.assert_allclose(got.numpy(), ref, atol=ATOL, rtol=0)
+    if not dense:
+        poisoned = docs.clone()
+        poisoned[torch.arange(128)[None, :] >= doclens[:, None].long()] = 100.0
+        assert torch.equal(ColbertIndex(poisoned.to(dev), doclens.to(dev)).score(Qd).cpu(), got)
