@@ -5557,7 +5557,43 @@ int check_f32(cbv2_index* ix, int op, const float* Q, int32_t B, int32_t lq, int
 }
 
 // (a SEARCH workspace's split also resets the rows' band state: count, lb, done)
+// Which queries each workspace's split (qhi / qlo) holds, for
+// cbv2_rerank_f32_after_search: the one-trip rerank reuses the split its
+// search left in the stage-2 workspace only while the last split enqueued
+// into that workspace is that search's (same index, Q pointer, B, lq);
+// otherwise it splits Q again.  Keyed by the qhi address; a small ring, so an
+// evicted entry only costs the re-split.
+struct SplitTag {
+  const void* qhi = nullptr;
+  const cbv2_index* ix = nullptr;
+  const float* Q = nullptr;
+  int B = 0, lq = 0;
+};
+constexpr int kSplitTags = 64;
+std::mutex g_split_mu;
+SplitTag g_split_tags[kSplitTags];
+int g_split_next = 0;
+
+void note_split(const cbv2_index* ix, const float* Q, int B, int lq, const void* qhi) {
+  std::lock_guard<std::mutex> lk(g_split_mu);
+  int slot = -1;
+  for (int i = 0; i < kSplitTags && slot < 0; ++i)
+    if (g_split_tags[i].qhi == qhi) slot = i;
+  if (slot < 0) slot = g_split_next++ % kSplitTags;
+  g_split_tags[slot] = SplitTag{qhi, ix, Q, B, lq};
+}
+
+bool split_holds(const cbv2_index* ix, const float* Q, int B, int lq, const void* qhi) {
+  std::lock_guard<std::mutex> lk(g_split_mu);
+  for (int i = 0; i < kSplitTags; ++i) {
+    const SplitTag& t = g_split_tags[i];
+    if (t.qhi == qhi) return t.ix == ix && t.Q == Q && t.B == B && t.lq == lq;
+  }
+  return false;
+}
+
 int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st, int count0 = 0) {
+  note_split(ix, Q, B, lq, w->qhi);
   hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(512), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
                      ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0);
   return launch_check("split_query_kernel");
@@ -6324,12 +6360,15 @@ int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const
 }
 
 // Internal (retrieve.cpp): cbv2_rerank_f32 for the queries a cbv2_search_f32
-// with the same (B, lq) and band capacity `cap` split into `search_ws` just
-// before on the same stream: the rerank reads that split (qhi / qlo) instead
-// of launching the query split again.  Same arithmetic, same results.
+// with the same (B, lq) and band capacity `cap` split into `search_ws` before
+// on the same stream: while that split is still the last one enqueued into
+// the workspace (split_holds: same index, Q, B, lq), the rerank reads it (qhi
+// / qlo) instead of launching the query split again; otherwise it splits Q
+// into its own workspace, as cbv2_rerank_f32 does.  Same arithmetic, same
+// results either way.
 int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t search_wsb, int32_t cap, int32_t B,
                                  int32_t lq, const int32_t* cand, int32_t C, int32_t k, void* ws, size_t wsb,
-                                 float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+                                 float* out_scores, int32_t* out_ids, int32_t* out_pos, const float* Q, void* stream) {
   CBV2_REQUIRE(cand != nullptr && C >= 1 && k >= 0 && out_scores != nullptr && (k == 0 || out_ids != nullptr),
                "bad candidates / outputs");
   CBV2_REQUIRE(ix != nullptr && ix->resid != nullptr, "not an fp32-faithful index");
@@ -6342,12 +6381,22 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
   CBV2_REQUIRE(ws != nullptr && wsb >= need && aligned16(ws), "workspace too small or misaligned (%zu < %zu)", wsb,
                need);
   f32_ws_layout(ix, CBV2_F32_RERANK, B, lq, C, (uint8_t*)ws, &w);
-  w.qhi = sw.qhi;
-  w.qlo = sw.qlo;
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
-  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, (hipStream_t)stream);
+  const hipStream_t st = (hipStream_t)stream;
+  if (split_holds(ix, Q, B, lq, sw.qhi)) {
+    w.qhi = sw.qhi;
+    w.qlo = sw.qlo;
+  } else {
+    CBV2_REQUIRE(Q != nullptr, "null queries");
+    int rc = split_queries(ix, Q, B, lq, &w, st);
+    if (rc) return rc;
+  }
+  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st);
 }
+
+// Internal (retrieve.cpp): the device an index lives on (-1: null index).
+int cbv2_index_device(const cbv2_index* ix) { return ix ? ix->device : -1; }
 
 size_t cbv2_topk_workspace_bytes(int32_t B, int64_t n) { return B >= 1 && n >= 1 ? topk_ws_bytes(B, n) : 0; }
 

@@ -19,6 +19,10 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "colbert_mi355x.h"
 
@@ -26,7 +30,8 @@ extern "C" int cbv2_set_error(int code, const char* msg);
 extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t search_wsb, int32_t cap,
                                             int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k, void* ws,
                                             size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
-                                            void* stream);
+                                            const float* Q, void* stream);
+extern "C" int cbv2_index_device(const cbv2_index* ix);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -46,32 +51,96 @@ int err(int code, const char* fmt, ...) {
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// The round trip's wait: an event after the D2H copy, polled by this thread
-// (hipEventQuery) for up to kSpinNs, then a blocking wait.  The stream work
-// ahead of the copy is one scan (~5 ms at B=1, 1M docs) or one batch; a
-// blocking hipStreamSynchronize wakes the host tens of microseconds after the
-// copy lands (measured: 26-39 us from the D2H copy's end to the next H2D
-// copy's start), a poll within about a microsecond.  One event per thread
-// and device, created once.
+// The round trip's wait: an event recorded after the D2H copy.  A blocking
+// wait wakes the host tens of microseconds after the copy lands (measured:
+// 26-39 us from the D2H copy's end to the next H2D copy's start), a poll
+// (hipEventQuery) within about a microsecond -- but a poll holds a core for
+// as long as the stream work ahead of the copy runs.  So only small batches
+// poll flat out: B <= kSpinMaxB (one scan of <= 8 queries: ~5-7 ms at 1M
+// docs, where a wake-up would be ~0.5 % of the latency), for at most kSpinNs,
+// then as below.
+// Larger batches (one B=256 scan: ~140 ms, whose host side runs the BM25
+// threads meanwhile) poll between sleeps of 1/32 of the time waited so far
+// (20 us .. 500 us): the thread wakes at most ~3 % (and 0.5 ms) after the
+// copy and is asleep otherwise.  (hipEventSynchronize is no substitute:
+// measured on the GPU box, a B=256 call over 200k docs burned its whole
+// 28 ms wait on a core even with a hipEventBlockingSync event.)
+//
+// Events come from a process-wide pool per device: taken for one wait and
+// returned after it, so the pool holds at most as many events as threads
+// ever waited at once (cbv2_retrieve_wait_events counts them), none leaks per
+// thread, and an event is always created on the device of the index whose
+// stream it is recorded on (the caller's current device may differ).
 constexpr long long kSpinNs = 50LL * 1000 * 1000;
-int wait_copy(hipStream_t st) {
-  thread_local hipEvent_t ev[64] = {};
-  int dev = 0;
-  RT_HIP(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return hipStreamSynchronize(st) == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "sync failed");
-  if (!ev[dev]) RT_HIP(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
-  RT_HIP(hipEventRecord(ev[dev], st));
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    const hipError_t q = hipEventQuery(ev[dev]);
-    if (q == hipSuccess) return CBV2_OK;
-    if (q != hipErrorNotReady) return err(CBV2_EHIP, "hipEventQuery (%d)", (int)q);
-    if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kSpinNs)
-      break;
+constexpr int32_t kSpinMaxB = 8;
+constexpr int kMaxDev = 64;
+
+struct EventPool {
+  std::mutex mu;
+  std::vector<hipEvent_t> free_ev[kMaxDev];
+  int64_t created = 0;
+};
+EventPool& pool() {
+  static EventPool* p = new EventPool;   // never destroyed: no teardown-order issue at exit
+  return *p;
+}
+
+int take_event(int dev, hipEvent_t* ev) {
+  EventPool& P = pool();
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto& v = P.free_ev[dev];
+    if (!v.empty()) {
+      *ev = v.back();
+      v.pop_back();
+      return CBV2_OK;
+    }
   }
-  RT_HIP(hipEventSynchronize(ev[dev]));
+  RT_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  std::lock_guard<std::mutex> lk(P.mu);
+  ++P.created;
   return CBV2_OK;
 }
+
+void give_event(int dev, hipEvent_t ev) {
+  EventPool& P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.free_ev[dev].push_back(ev);
+}
+
+// The caller has selected the index's device (DevSel below).
+int wait_copy(hipStream_t st, int dev, int32_t B) {
+  if (dev < 0 || dev >= kMaxDev) return hipStreamSynchronize(st) == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "sync failed");
+  hipEvent_t ev = nullptr;
+  if (int rc = take_event(dev, &ev)) return rc;
+  hipError_t e = hipEventRecord(ev, st);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (e == hipSuccess) {
+    e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) break;
+    e = hipSuccess;
+    const long long waited =
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (B > kSpinMaxB || waited > kSpinNs)   // a long wait: sleep between polls
+      std::this_thread::sleep_for(std::chrono::nanoseconds(std::min(500000LL, std::max(20000LL, waited / 32))));
+  }
+  give_event(dev, ev);
+  return e == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "round-trip wait (%d)", (int)e);
+}
+
+// Selects the index's device for one call and restores the caller's.
+struct DevSel {
+  int prev = -1, dev = -1;
+  bool ok = false;
+  explicit DevSel(const cbv2_index* ix) {
+    dev = cbv2_index_device(ix);
+    if (dev < 0 || hipGetDevice(&prev) != hipSuccess) return;
+    ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DevSel() {
+    if (ok && prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+  }
+};
 
 struct Kind {
   int32_t dtype = 0, faithful = 0;
@@ -165,6 +234,12 @@ size_t cbv2_retrieve_workspace_bytes(const cbv2_index* ix, const cbv2_comm* c, i
   return layout(ix, c, kd, B, lq, k, kb, C, nullptr).total;
 }
 
+int64_t cbv2_retrieve_wait_events(void) {
+  EventPool& P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  return P.created;
+}
+
 size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C) {
   if (B < 1 || k < 1 || kb < 0 || C < 1) return 0;
   return host_words(B, k, kb, C) * 4;
@@ -178,6 +253,8 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   const Layout L = layout(ix, c, kd, B, lq, k, kb, C, workspace);
   if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
     return err(CBV2_EINVAL, "workspace too small or not 256-B aligned (%zu bytes needed)", L.total);
+  DevSel ds(ix);
+  if (!ds.ok) return err(CBV2_EHIP, "cannot select the index's device %d", ds.dev);
   if (c)
     return cbv2_search_sharded_local(ix, c, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, kb, L.base, L.stage2, stream);
   if (kd.faithful)
@@ -200,6 +277,8 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     return err(CBV2_EINVAL, "workspace too small or not 256-B aligned (%zu bytes needed)", L.total);
   if (!host_stage || host_bytes < host_words(B, k, kb, C) * 4)
     return err(CBV2_EINVAL, "host stage too small (%zu bytes needed)", host_words(B, k, kb, C) * 4);
+  DevSel ds(ix);
+  if (!ds.ok) return err(CBV2_EHIP, "cannot select the index's device %d", ds.dev);
   hipStream_t st = (hipStream_t)stream;
   const HostLayout H = host_layout(host_stage, B, k, kb, C);
   const int32_t* bm = lex_ids;   // the stage-1 lists the RRF reads (host)
@@ -219,14 +298,15 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     bm = H.lex_merged;
   }
   RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
-  if ((rc = wait_copy(st))) return rc;   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  if ((rc = wait_copy(st, ds.dev, B))) return rc;   // the one host round trip: the ColBERT (and merged BM25) top-k are here
   if ((rc = cbv2_rrf_fuse(bm, kb, H.ids, k, B, rrf_k, C, H.cand, nullptr, nullptr))) return rc;
   RT_HIP(hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st));
   if (c)
     return cbv2_rerank_sharded(ix, c, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
-  if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank too
+  if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank when it is still there
     return cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
-                                        B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+                                        B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos,
+                                        (const float*)Q, st);
   return cbv2_rerank_ws(ix, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
 }
 

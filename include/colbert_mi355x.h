@@ -558,6 +558,19 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    comm, B, lq, k, kb, C) bytes, the same one for begin and finish;
  *    host_stage: host (pinned for asynchronous copies),
  *    cbv2_retrieve_host_bytes(B, k, kb, C) bytes, one per stream.
+ *  Q at finish: the same buffer and contents as at begin.  For a single
+ *    fp32-faithful shard finish reuses the query split begin left in the
+ *    workspace while it is still the last split enqueued there (same index,
+ *    Q pointer, B, lq); if anything split other queries into that workspace
+ *    in between, finish splits Q again (same results either way).
+ *  Both calls select the index's device themselves (the caller's current
+ *    device may differ) and restore the caller's.  finish's wait polls for
+ *    B <= 8 (a small scan: the wake-up of a blocking wait would be tens of
+ *    microseconds of the latency) and sleeps in a blocking-sync event wait
+ *    for larger batches, so it never holds a core for a whole batch scan.
+ * cbv2_retrieve_wait_events: the events finish's waits have created in this
+ *    process (a pool per device, reused across calls and threads: at most
+ *    the number of threads that ever waited at once, per device and kind).
  * cbv2_index_kind: the index's dtype (CBV2_DTYPE_*) and whether a residual is
  *    attached (fp32-faithful, 1) or not (0).                                */
 #define CBV2_RETRIEVE_BAND_CAP 16384
@@ -565,6 +578,7 @@ int cbv2_index_kind(const cbv2_index* index, int32_t* dtype, int32_t* faithful);
 size_t cbv2_retrieve_workspace_bytes(const cbv2_index* index, const cbv2_comm* comm, int32_t B, int32_t lq,
                                      int32_t k, int32_t kb, int32_t C);
 size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C);
+int64_t cbv2_retrieve_wait_events(void);
 int cbv2_retrieve_begin(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
                         int32_t k, int32_t kb, int32_t C, void* workspace, size_t workspace_bytes, void* stream);
 int cbv2_retrieve_finish(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,

@@ -79,3 +79,26 @@ def test_run_leg_symmetric_failure(world, fail_rank):
             assert a == {"sum": expect_sum} and first_ran
         assert b == {"sum": expect_sum}
         assert "ValueError: symmetric" in c["error"]
+
+
+def test_main_line_takes_native_numbers_once_validated():
+    """bench.main_line: the N > 1 line's value / ms_per_step / p50 come from
+    the in-ABI exchange when it validated
+    on every rank, with the torch.distributed numbers beside; otherwise the
+    torch.distributed numbers stay the line's.  No collective involved."""
+    import bench
+    own = (1000.0, 256.0, 0.9, 1.1)
+    good = {"value": 1200.0, "ms_per_step": 213.3, "p50_ms_b1": 0.7, "p99_ms_b1": 0.8,
+            "validated_on_every_rank": True}
+    line, torch_leg = bench.main_line(*own, good, False)
+    assert (line["value"], line["ms_per_step"], line["p50_ms_b1"]) == (1200.0, 213.3, 0.7)
+    assert line["exchange"].startswith("native")
+    assert torch_leg == {"value": 1000.0, "ms_per_step": 256.0, "p50_ms_b1": 0.9, "p99_ms_b1": 1.1,
+                         "exchange": "torch.distributed"}
+    for native in (dict(good, validated_on_every_rank=False), {"error": "failed on another rank"}, None,
+                   dict(good, p50_ms_b1=None)):
+        line, torch_leg = bench.main_line(*own, native, False)
+        assert (line["value"], line["ms_per_step"], line["p50_ms_b1"]) == (1000.0, 256.0, 0.9)
+        assert torch_leg is None
+    line, torch_leg = bench.main_line(*own, good, True)     # --native-exchange: the main legs ran native
+    assert line["value"] == 1000.0 and torch_leg is None and line["exchange"].startswith("native")

@@ -1,0 +1,132 @@
+"""GPU: the host side of the one-round-trip retrieve (csrc/retrieve.cpp) --
+how cbv2_retrieve_finish waits for its D2H copy, which device it records
+its event on, and when the fp32-faithful rerank may reuse begin's query
+split (HybridRetriever.retrieve, LRC:894-935).
+
+Done =
+* a B = 256 finish sleeps in its wait: the process CPU time of a whole
+  one-trip call (begin + finish, no stage 1) stays <= 5 ms while the GPU
+  scans for tens of ms (a polling wait would burn the whole scan);
+* the wait's events come from a pool: 1,000 calls on 8 threads, polled (B =
+  1) and blocking (B = 16) waits, create at most 8 events per kind;
+* the caller's current device is restored after begin / finish, from a
+  thread that never selected one (one GPU on the box: the index-on-another-
+  device case itself needs a second device);
+* a faithful finish whose workspace got another query split between begin
+  and finish (a search of other queries in the stage-1 callable) splits Q
+  again: its results equal the composed stages on Q bit for bit."""
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from hybrid_rag_colbertv2_amd import _lib, synth
+from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, rrf_fuse
+from hybrid_rag_colbertv2_amd.index import ColbertIndex, _stream_ptr
+
+pytestmark = pytest.mark.gpu
+
+K, C, KF = 100, 50, 10
+
+
+def _index(dev, N, B, seed, dtype=torch.bfloat16):
+    Qf = synth.make_queries(B, seed=seed)
+    planted = synth.planted_ids(B, N, 10, seed=seed + 1)
+    tokens, doclens = synth.make_shard(0, N, Qf, planted, dev, dtype=dtype)
+    return Qf, planted, tokens, doclens
+
+
+def _composed(index, Q):
+    _, ids = index.search(Q, K)
+    cand = rrf_fuse(np.zeros((ids.shape[0], 0), np.int32), ids.cpu().numpy(), rrf_k=60, C=C)
+    return index.rerank(Q, torch.from_numpy(cand).to(index.device), KF)
+
+
+def test_large_batch_wait_sleeps(dev):
+    N, B = 200_000, 256
+    Qf, _, tokens, doclens = _index(dev, N, B, seed=3)
+    ix = ColbertIndex(tokens, doclens)
+    Q = Qf.to(dev, torch.bfloat16)
+    one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+    one(Q)
+    torch.cuda.synchronize()
+    cpu, wall = [], []
+    for _ in range(3):
+        t0, c0 = time.perf_counter(), time.process_time()
+        out = one(Q)
+        c1, t1 = time.process_time(), time.perf_counter()
+        cpu.append(c1 - c0)
+        wall.append(t1 - t0)
+    torch.cuda.synchronize()
+    assert min(wall) > 0.010, f"the call should wait for a scan of {N} docs x {B} queries (took {min(wall)} s)"
+    assert sorted(cpu)[1] <= 0.005, f"a B=256 one-trip call used {cpu} s of CPU over {wall} s of wall time"
+    assert out[1].shape == (B, KF)
+
+
+def test_wait_events_pooled_and_device_restored(dev):
+    N = 3000
+    L = _lib.lib()
+    Qf, _, tokens, doclens = _index(dev, N, 16, seed=9)
+    ix = ColbertIndex(tokens, doclens)
+    Q1, Q16 = Qf[:1].to(dev, torch.bfloat16).contiguous(), Qf.to(dev, torch.bfloat16)
+    want1, want16 = [x.cpu() for x in _composed(ix, Q1)], [x.cpu() for x in _composed(ix, Q16)]
+    before = int(L.cbv2_retrieve_wait_events())
+    errs, devs = [], []
+
+    def body(t):
+        try:
+            one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+            s = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(s):
+                for i in range(125):
+                    Q, want = (Q1, want1) if (i + t) % 2 else (Q16, want16)
+                    got = [x.cpu() for x in one(Q)]
+                    if not all(torch.equal(g, w) for g, w in zip(got, want)):
+                        raise AssertionError(f"thread {t} call {i}: results differ from the composed stages")
+            devs.append(torch.cuda.current_device())
+        except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
+            errs.append(e)
+
+    ts = [threading.Thread(target=body, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a thread hung"
+    if errs:
+        raise errs[0]
+    created = int(L.cbv2_retrieve_wait_events()) - before
+    assert created <= 16, f"1,000 calls on 8 threads created {created} wait events"
+    assert devs == [dev.index or 0] * 8
+
+
+def test_faithful_finish_resplits_after_foreign_split(dev):
+    N, B = 6000, 4
+    L = _lib.lib()
+    Qf, planted, tokens, doclens = _index(dev, N, B, seed=21, dtype=torch.float32)
+    ix = ColbertIndex.faithful_f32(tokens, doclens)
+    Q = Qf.to(dev).contiguous()
+    Q2 = torch.flip(Q, dims=[0]).contiguous() * 0.5          # other queries, same shape
+    one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+    want = [x.cpu() for x in _composed(ix, Q)]
+    assert all(torch.equal(x.cpu(), w) for x, w in zip(one(Q), want))       # begin's split reused
+    ws = one._sized[1][0]
+    cap = 16384
+    sw = int(L.cbv2_f32_workspace_bytes(ix._h, _lib.F32_SEARCH, B, Q.shape[1], cap))
+    s2 = torch.empty((B, K), dtype=torch.float32, device=dev)
+    i2 = torch.empty((B, K), dtype=torch.int32, device=dev)
+    st2 = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def foreign():     # stage 1 of this call: another search into the same workspace
+        _lib.check(L.cbv2_search_f32(ix._h, Q2.data_ptr(), B, Q2.shape[1], K, cap, ws, sw, s2.data_ptr(),
+                                     i2.data_ptr(), st2.data_ptr(), _stream_ptr(dev)))
+        return np.full((B, 1), -1, np.int32), np.zeros((B, 1), np.float32)
+
+    got = [x.cpu() for x in one(Q, foreign)]
+    want_lex = [x.cpu() for x in _composed(ix, Q)]
+    for g, w, name in zip(got, want_lex, ("scores", "ids", "positions")):
+        assert torch.equal(g, w), f"{name}: the rerank did not re-split Q after a foreign split"
+    for b in range(B):
+        assert set(got[1][b].tolist()) == set(planted[b].tolist())
