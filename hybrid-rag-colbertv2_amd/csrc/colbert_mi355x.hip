@@ -2494,6 +2494,7 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
   const int shifts[3] = {21, 10, 0};
   const int bits[3] = {11, 11, 10};
   uint32_t prefix = 0, mask = 0, kleft = (uint32_t)kk, last_count = 0;
+#pragma unroll 1
   for (int p = 0; p < 3; ++p) {
     const int nb = 1 << bits[p];
     for (int b = tid; b < nb; b += nth) hist[b] = 0;
@@ -2516,6 +2517,7 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
   uint32_t id_thr = 0xffffffffu;  // ties at ustar with index <= id_thr are taken
   if (kleft < last_count) {
     uint32_t iprefix = 0, imask = 0, kl2 = kleft;
+#pragma unroll 1
     for (int p = 0; p < 3; ++p) {
       const int nb = 1 << bits[p];
       for (int b = tid; b < nb; b += nth) hist[b] = 0;
@@ -2869,38 +2871,102 @@ __global__ __launch_bounds__(256) void block_max_kernel(const float* __restrict_
   }
 }
 
-__global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
-                                                               int k, int64_t id_base, const uint32_t* __restrict__ bm,
-                                                               int64_t bm_ld, const uint32_t* __restrict__ sb,
-                                                               int64_t sb_ld, float* __restrict__ out_s,
-                                                               int32_t* __restrict__ out_i) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
-  uint64_t* const sel = reinterpret_cast<uint64_t*>(bm_dyn);   // [kBmCand]
+// In-launch hand-off to the row's LAST workgroup (the workgroups of a row
+// each store part of the row, the last one to finish reads all of it), by
+// the write-through protocol of MI355X_MICROARCH.md's hand-off table, row 1 --
+// no fences (an agent-scope __threadfence costs ~3.5 us per workgroup, more
+// than the kernel boundary it would save):
+//  * every handed-off store is an sc1 store (st_sc1) and every load of those
+//    bytes in the last workgroup an sc1 load (ld_sc1: global_*, never flat_);
+//  * each storing wave drains its stores (s_waitcnt vmcnt(0)) before the
+//    workgroup barrier, then ONE lane adds to an agent-scope counter; the
+//    workgroup whose add returned the last count is told so by the value;
+//  * shards = 8 (launches of up to ~1k workgroups per row): the counter is
+//    kept per XCD (blockIdx.x mod 8 -- a row's workgroups x and x + 8 share an
+//    XCD), each on a 128-B line of its own, and each shard's last adder adds
+//    to the row's top counter: ~1/8 of the serialised same-address atomics
+//    (~12 ns each, "fanin" row of the price table).  shards = 1: one counter.
+// The counters are zero before the launch; the last adders re-zero them, so
+// the next launch on the stream finds them zero again.  Every workgroup of
+// the row calls this exactly once (block-uniform); returns block-uniform.
+constexpr int kArriveInts = 9 * 32;   // one row's sharded counters: 8 XCD shards + the top, 128 B apart
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool row_last_arrival(int32_t* __restrict__ ctr, int nwg, int shards, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int last = 0;
+    if (shards == 1) {
+      last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1;
+      if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const int sh = (int)(blockIdx.x & 7u);
+      const int per = (nwg - sh + 7) / 8;   // this shard's workgroups: x = sh (mod 8), x < nwg
+      int32_t* c = ctr + 32 * sh;
+      if (__hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1) {
+        __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int used = nwg < 8 ? nwg : 8;
+        last = __hip_atomic_fetch_add(ctr + 256, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == used - 1;
+        if (last) __hip_atomic_store(ctr + 256, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// The select of one row (topk_bmax_kernel's work; run by a whole workgroup):
+// bm / sb = the row's block and superblock keys, lds = kBmFixedLds + ns * 4
+// bytes of LDS.
+// SC1: bm / sb were stored in this launch (bmax_topk_kernel): read them with
+// sc1 loads (the write-through hand-off, row_last_arrival).
+template <bool SC1 = false>
+__device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int64_t id_base,
+                              const uint32_t* __restrict__ brow, const uint32_t* __restrict__ srow, float* os,
+                              int32_t* oi, uint8_t* lds) {
+  uint64_t* const sel = reinterpret_cast<uint64_t*>(lds);   // [kBmCand]
   uint32_t* const hist = reinterpret_cast<uint32_t*>(sel + kBmCand);   // [2048]
   uint32_t* const qual = hist + 2048;                              // [kBmQual]
   uint32_t* const misc = qual + kBmQual;                           // [16]
   uint32_t* const keys = misc + 16;                                // [ns] superblock keys
   const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6;
-  const int row = blockIdx.x;
   const int nb = (int)((n + 63) >> 6);
   const int ns = (int)((n + 255) >> 8);
-  const float* x = scores + (size_t)row * ld;
-  const uint32_t* brow = bm + (size_t)row * bm_ld;
-  const uint32_t* srow = sb + (size_t)row * sb_ld;
   const int kk = (int)((int64_t)k < n ? k : n);
-  for (int i = tid; i < ns; i += nth) keys[i] = srow[i];
+  // kk large against the superblock count (kk * 8 > ns: rows of 65k-262k docs
+  // with k up to 1,024): the kk-th superblock key would sit near the row's
+  // bottom and qualify nearly every doc (then the full-row fallback), so the
+  // threshold comes from the 64-doc block keys instead (read in place: up to
+  // 4 ns of them)
+  const bool by_block = (int64_t)kk * 8 > ns;
+  for (int i = tid; i < ns; i += nth) keys[i] = SC1 ? ld_sc1(srow + i) : srow[i];
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
-  // 1. t = the kk-th largest SUPERBLOCK key, to its top 22 bits (two 11-bit
-  //    digits): kk superblocks have a max >= t, so the kk-th largest score is
-  //    >= t, and every doc >= t lies in a 64-doc block whose key is >= t
-  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < ns ? kk : ns);
+  // 1. t = the kk-th largest SUPERBLOCK key (or block key), to its top 22
+  //    bits (two 11-bit digits): kk superblocks (blocks) have a max >= t, so
+  //    the kk-th largest score is >= t, and every doc >= t lies in a 64-doc
+  //    block whose key is >= t
+  const int nk = by_block ? nb : ns;
+  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < nk ? kk : nk);
   for (int p = 0; p < 2; ++p) {
     const int shift = 21 - 11 * p;
     for (int b = tid; b < 2048; b += nth) hist[b] = 0;
     __syncthreads();
-    for (int i = tid; i < ns; i += nth) {
-      const uint32_t u = keys[i];
+    for (int i = tid; i < nk; i += nth) {
+      const uint32_t u = by_block ? (SC1 ? ld_sc1(brow + i) : brow[i]) : keys[i];
       hist_add(hist, (u >> shift) & 2047u, (u & mask) == prefix);
     }
     __syncthreads();
@@ -2915,7 +2981,7 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
   // 2. the 64-doc blocks (of the superblocks >= t) whose max reaches t, then their docs >= t
   for (int i = tid; i < 4 * ns; i += nth) {
     const int sbk = i >> 2, j = i;
-    if (j < nb && keys[sbk] >= t && brow[j] >= t) {
+    if (j < nb && keys[sbk] >= t && (SC1 ? ld_sc1(brow + j) : brow[j]) >= t) {
       const uint32_t pos = atomicAdd(&misc[0], 1u);
       if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)j;
     }
@@ -2950,8 +3016,6 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
     topk_exact_row(x, n, kk, sel, hist, &misc[4], &misc[5], &misc[6], &misc[7]);
     m = kk;
   }
-  float* os = out_s + (size_t)row * k;
-  int32_t* oi = out_i + (size_t)row * k;
   if (m <= kBmRankMax) {   // rank by counting: keys are unique, rank = #greater
     for (int i = tid; i < m; i += nth) {
       const uint64_t key = sel[i];
@@ -2969,6 +3033,74 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
   } else {
     sort_and_write(sel, m, k, id_base, os, oi);
   }
+}
+
+__global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
+                                                               int k, int64_t id_base, const uint32_t* __restrict__ bm,
+                                                               int64_t bm_ld, const uint32_t* __restrict__ sb,
+                                                               int64_t sb_ld, float* __restrict__ out_s,
+                                                               int32_t* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
+  const int row = blockIdx.x;
+  topk_bmax_row(scores + (size_t)row * ld, n, k, id_base, bm + (size_t)row * bm_ld, sb + (size_t)row * sb_ld,
+                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn);
+}
+
+// Block-max top-k in ONE launch (small batches, the latency path): grid (P, B)
+// of 1024-thread workgroups, each writing the block and superblock keys of 256
+// blocks (16,384 docs) of row b as block_max_kernel does, then the row's last
+// workgroup to finish (row_last_arrival on done[b]) runs the row's select
+// (topk_bmax_row).  Same keys, same select: the same results as block_max +
+// topk_bmax_kernel, one launch and its gap fewer.
+constexpr int kBmFusedBlocksPerWg = 16 * (kTkThreads / 64);   // 16 blocks per wave
+__global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __restrict__ scores, int64_t n, int64_t ld,
+                                                               int k, int64_t id_base, uint32_t* __restrict__ bm,
+                                                               int64_t bm_ld, uint32_t* __restrict__ sb, int64_t sb_ld,
+                                                               int32_t* __restrict__ done, int64_t done_ld,
+                                                               float* __restrict__ out_s, int32_t* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
+  __shared__ int s_last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.y;
+  const int64_t nb = (n + 63) >> 6;
+  const int c = lane & 15, r = lane >> 4;
+  const int64_t b0 = (int64_t)blockIdx.x * kBmFusedBlocksPerWg + wave * 16;
+  const float* x = scores + (size_t)row * ld;
+  uint32_t* brow = bm + (size_t)row * bm_ld;
+  uint32_t* srow = sb + (size_t)row * sb_ld;
+  const bool vec = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(scores) & 15) == 0);
+  uint32_t key[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {   // block b0 + 4u + r, docs 64 * blk + 4c .. + 3
+    const int64_t blk = b0 + 4 * u + r;
+    const int64_t i = blk * 64 + 4 * c;
+    uint32_t m = 0u;
+    if (blk < nb) {
+      if (vec && i + 3 < n) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+        m = max(max(f2u(v[0]), f2u(v[1])), max(f2u(v[2]), f2u(v[3])));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = (i + e < n) ? max(m, f2u(x[i + e])) : m;
+      }
+    }
+    key[u] = m;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {   // max over each 16-lane row = one block
+    uint32_t v = key[u];
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+    const int64_t blk = b0 + 4 * u + r;
+    if (c == 0 && blk < nb) st_sc1(brow + blk, v);
+    const uint32_t s4 = umax_over_rows(v);   // blocks b0 + 4u .. + 3 (b0 is a multiple of 16)
+    if (lane == 0 && b0 + 4 * u < nb) st_sc1(srow + (b0 >> 2) + u, s4);
+  }
+  // <= 96 workgroups per row (n <= 64 * kBmMaxBlocks): one counter
+  if (!row_last_arrival(done + (size_t)row * done_ld, (int)gridDim.x, 1, &s_last)) return;
+  topk_bmax_row<true>(x, n, k, id_base, brow, srow, out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn);
 }
 
 // ---------------------------------------------------------------------------
@@ -3383,14 +3515,21 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 // resets the row's band state (each nullable): count[b] = count0 (the band
 // collect's counter; k when the band's first k slots are the bf16 top-k
 // already rescored by phase 1), lbu[b] = ~0 (the atomic-min of the bf16 top-k's
-// faithful scores, order-preserving bits) and done[b] = 0 (the fallback's
-// finished-workgroup counter) -- one launch fewer than separate memsets.
+// faithful scores, order-preserving bits), done[b] = 0 (the fallback's
+// finished-workgroup counter), the row's arrival counters (arrive: narrive
+// ints per row over kArriveSlotsK slots -- the launches that select in their
+// last workgroup: the block-max select, the band select, the rerank select)
+// and -- ctr, the search's scan -- the scan's task-counter block: launches
+// fewer than separate memsets.
+constexpr int kArriveSlotsK = 3;   // slots of the faithful workspace's arrival counters (kArriveSlots)
 __global__ __launch_bounds__(512) void split_query_kernel(const float* __restrict__ Q, int lq,
                                                           uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
                                                           float E, float M, float* __restrict__ beta,
                                                           int32_t* __restrict__ count = nullptr,
                                                           uint32_t* __restrict__ lbu = nullptr,
-                                                          int32_t* __restrict__ done = nullptr, int count0 = 0) {
+                                                          int32_t* __restrict__ done = nullptr, int count0 = 0,
+                                                          int32_t* __restrict__ arrive = nullptr, int narrive = 0,
+                                                          int* __restrict__ ctr = nullptr, int nctr = 0) {
   // one 16-lane group per query token (lq <= 32: one pass, no loop -- the B=1
   // latency path waits on this launch); the per-token bound terms are summed
   // in the order of the round-3 one-wave kernel (4 strided partial sums, then
@@ -3418,6 +3557,15 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
     if (lbu != nullptr) lbu[b] = 0xffffffffu;
     if (done != nullptr) done[b] = 0;
   }
+  if (arrive != nullptr) {   // slot j of row b at (j * B + b) * per
+    const int per = narrive / kArriveSlotsK;
+    for (int i = tid; i < narrive; i += blockDim.x) {
+      const int j = i / per, e = i - j * per;
+      arrive[((size_t)j * gridDim.x + b) * per + e] = 0;
+    }
+  }
+  if (ctr != nullptr && b == 0)   // the scan's task counters (the scan that follows skips its memset)
+    for (int i = tid; i < nctr; i += blockDim.x) ctr[i] = 0;
 }
 
 // One row tile, faithful product: acc = init + lo.qhi + hi.qlo + hi.qhi.
@@ -3600,6 +3748,106 @@ __device__ __forceinline__ float faithful_doc_split(const uint8_t* __restrict__ 
   return v;
 }
 
+// Selections run by a row's LAST workgroup (row_last_arrival, 8 shards) in
+// the launch that scored the row, instead of a select launch after it.
+struct RowSelect {
+  int mode = 0;                  // kSelNone / kSelCand / kSelBand
+  int32_t* arrive = nullptr;     // row b's counters at arrive + b * kArriveInts (zero before the launch)
+  int k = 0;
+  float* out_s = nullptr;
+  int32_t* out_i = nullptr;
+  int32_t* out_p = nullptr;      // kSelCand: positions in the candidate list (nullable)
+  const float* lb = nullptr;     // kSelBand: a lower bound of the row's k-th score (nullable), or
+  const uint32_t* lbu = nullptr; //   its order-preserving bits (the two-pass band's)
+  int32_t* status = nullptr;     // kSelBand: the band size (the fallback writes -1 for overflowed rows)
+};
+constexpr int kSelNone = 0, kSelCand = 1, kSelBand = 2;
+
+// kSelCand (= select_small_kernel's work): the row's C <= kSmallMax raw
+// scores (stored in this launch: sc1 loads), ranked with the position rule.
+__device__ void select_cand_row(const float* raw, const int32_t* crow, int C, int k, float* os, int32_t* oi,
+                                int32_t* op, float* sc, uint64_t* keys) {
+  for (int t = threadIdx.x; t < C; t += blockDim.x) {
+    sc[t] = ld_sc1(raw + t);
+    keys[t] = rank_key(sc[t], (uint32_t)t);
+  }
+  __syncthreads();
+  select_from_lds(sc, keys, C, k, crow, os, oi, op);
+}
+
+// kSelBand (= band_select_kernel's result): the exact top-k of the row's cnt
+// band keys (score desc, id asc; F stored in this launch or before it: sc1
+// loads).  The keys reaching the lower bound lb hold the top-k (k docs score
+// at least lb); when 1024 or fewer do, they alone are ranked by counting,
+// otherwise (ties at the top, or a shard's band with fewer than k keys above
+// a global bound) the kk-th largest key is found by six radix passes over all
+// the keys and the kk keys at or above it are ranked.
+__device__ void select_band_row(const float* F, const int32_t* cand, int cnt, int k, int64_t id_base, bool has_lb,
+                                float lbv, float* os, int32_t* oi, uint64_t* sel, uint32_t* hist, uint32_t* misc) {
+  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6;
+  const int kk = k < cnt ? k : cnt;
+  auto key_at = [&](int i) { return rank_key(ld_sc1(F + i), (uint32_t)((int64_t)cand[i] - id_base)); };
+  if (tid < 8) misc[tid] = 0;
+  __syncthreads();
+  const uint32_t ulb = has_lb ? f2u(lbv) : 0u;
+  for (int i = tid; i < cnt; i += nth) {
+    const uint64_t key = key_at(i);
+    if ((uint32_t)(key >> 32) >= ulb) {
+      const uint32_t pos = atomicAdd(&misc[0], 1u);
+      if (pos < (uint32_t)kTopkMax) sel[pos] = key;
+    }
+  }
+  __syncthreads();
+  int m = (int)misc[0];
+  __syncthreads();
+  if (m < kk || m > kTopkMax) {
+    const int shifts[6] = {53, 42, 32, 21, 10, 0};
+    const int bits[6] = {11, 11, 10, 11, 11, 10};
+    uint64_t prefix = 0, mask = 0;
+    uint32_t kleft = (uint32_t)kk;
+    for (int p = 0; p < 6; ++p) {
+      const int nb = 1 << bits[p];
+      for (int i = tid; i < nb; i += nth) hist[i] = 0;
+      __syncthreads();
+      for (int i = tid; i < cnt; i += nth) {
+        const uint64_t key = key_at(i);
+        hist_add(hist, (uint32_t)(key >> shifts[p]) & (uint32_t)(nb - 1), (key & mask) == prefix);
+      }
+      __syncthreads();
+      if (wave == 0) find_bin(hist, nb, kleft, &misc[4], &misc[5], &misc[6]);
+      __syncthreads();
+      kleft -= misc[5];
+      prefix |= (uint64_t)misc[4] << shifts[p];
+      mask |= (uint64_t)(nb - 1) << shifts[p];
+      __syncthreads();
+    }
+    if (tid == 0) misc[0] = 0;
+    __syncthreads();
+    for (int i = tid; i < cnt; i += nth) {   // exactly kk keys reach the kk-th largest (keys are unique)
+      const uint64_t key = key_at(i);
+      if (key >= prefix) {
+        const uint32_t pos = atomicAdd(&misc[0], 1u);
+        if (pos < (uint32_t)kTopkMax) sel[pos] = key;
+      }
+    }
+    __syncthreads();
+    m = kk;
+  }
+  for (int i = tid; i < m; i += nth) {   // rank = #greater (unique keys)
+    const uint64_t key = sel[i];
+    int r = 0;
+    for (int j = 0; j < m; ++j) r += sel[j] > key ? 1 : 0;
+    if (r < k) {
+      os[r] = u2f((uint32_t)(key >> 32));
+      oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+    }
+  }
+  for (int j = m + tid; j < k; j += nth) {
+    os[j] = neg_inf();
+    oi[j] = -1;
+  }
+}
+
 template <bool LONG = false, int NW = 4>
 __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
@@ -3607,8 +3855,13 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
     float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld,
     uint32_t* __restrict__ lb_min, int64_t c0, float* __restrict__ fb_T = nullptr, int32_t* __restrict__ fb_done = nullptr,
-    int fb_k = 0, float* __restrict__ fb_s = nullptr, int32_t* __restrict__ fb_i = nullptr) {
+    int fb_k = 0, float* __restrict__ fb_s = nullptr, int32_t* __restrict__ fb_i = nullptr, RowSelect rs = RowSelect()) {
   __shared__ float s_m[4][32];
+  __shared__ uint64_t sel[kTopkMax];   // the fallback's / the row select's
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
+  __shared__ uint32_t misc[8];
+  __shared__ int s_last;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
@@ -3620,11 +3873,8 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     if (fb_T != nullptr && cb > limit) {   // block-uniform: the row's band overflowed its capacity
       // the full-scan fallback in this launch (fallback_split_kernel's work:
       // every doc's faithful score into fb_T, then the row's last workgroup
-      // runs the exact top-k into fb_s / fb_i; band_select leaves such rows)
-      __shared__ uint64_t sel[kTopkMax];
-      __shared__ uint32_t hist[2048];
-      __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
-      __shared__ int s_last;
+      // runs the exact top-k into fb_s / fb_i; band_select leaves such rows,
+      // a row select in this launch (rs) marks them -1 here)
       bf16x8 qh[2][4], ql[2][4];
       load_qfrag16(qhi, b, b + 1, lq, lane, qh);
       load_qfrag16(qlo, b, b + 1, lq, lane, ql);
@@ -3642,23 +3892,43 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
       const int kk = (int)((int64_t)fb_k < n ? fb_k : n);
       topk_exact_row(row, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
       sort_and_write(sel, kk, fb_k, id_base, fb_s + (size_t)b * fb_k, fb_i + (size_t)b * fb_k);
+      if (rs.mode == kSelBand && threadIdx.x == 0) rs.status[b] = -1;
       return;
     }
   }
-  if (c0 + (int64_t)blockIdx.x >= lim) return;  // block-uniform
-  bf16x8 qh[2][4], ql[2][4];
-  load_qfrag16(qhi, b, b + 1, lq, lane, qh);
-  load_qfrag16(qlo, b, b + 1, lq, lane, ql);
-  for (int64_t c = c0 + blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
-    const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
-    const int64_t loc = id - id_base;
-    float v = neg_inf();
-    if (id >= 0 && loc >= 0 && loc < n)                      // block-uniform
-      v = faithful_doc_split<LONG, NW>(hi, lo, loc, ld, doclens[loc], qh, ql, lane, wave, lq, s_m);
-    if (threadIdx.x == 0) {
-      out[(size_t)b * ld_out + c] = v;
-      if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
+  const bool idle = c0 + (int64_t)blockIdx.x >= lim;   // block-uniform
+  if (idle && rs.mode == kSelNone) return;
+  if (!idle) {
+    bf16x8 qh[2][4], ql[2][4];
+    load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+    load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+    for (int64_t c = c0 + blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
+      const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
+      const int64_t loc = id - id_base;
+      float v = neg_inf();
+      if (id >= 0 && loc >= 0 && loc < n)                      // block-uniform
+        v = faithful_doc_split<LONG, NW>(hi, lo, loc, ld, doclens[loc], qh, ql, lane, wave, lq, s_m);
+      if (threadIdx.x == 0) {
+        if (rs.mode != kSelNone)
+          st_sc1(out + (size_t)b * ld_out + c, v);   // handed to the row's last workgroup
+        else
+          out[(size_t)b * ld_out + c] = v;
+        if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
+      }
     }
+  }
+  if (rs.mode == kSelNone) return;
+  if (!row_last_arrival(rs.arrive + (size_t)b * kArriveInts, (int)gridDim.x, 8, &s_last)) return;
+  if (rs.mode == kSelCand) {   // C = limit candidates, ids = the row's cand
+    select_cand_row(out + (size_t)b * ld_out, cand + (size_t)b * ld_c, (int)limit, rs.k, rs.out_s + (size_t)b * rs.k,
+                    rs.out_i + (size_t)b * rs.k, rs.out_p ? rs.out_p + (size_t)b * rs.k : nullptr,
+                    reinterpret_cast<float*>(hist), sel);
+  } else {                     // the band: lim keys (count[b] <= limit here)
+    const bool has_lb = rs.lb != nullptr || rs.lbu != nullptr;
+    const float lbv = rs.lbu != nullptr ? u2f(rs.lbu[b]) : (rs.lb != nullptr ? rs.lb[b] : 0.0f);
+    select_band_row(out + (size_t)b * ld_out, cand + (size_t)b * ld_c, (int)lim, rs.k, id_base, has_lb, lbv,
+                    rs.out_s + (size_t)b * rs.k, rs.out_i + (size_t)b * rs.k, sel, hist, misc);
+    if (threadIdx.x == 0) rs.status[b] = (int32_t)lim;
   }
 }
 
@@ -4085,30 +4355,44 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
     // bm (nullable): the row's 64-doc block maxima of the block-max top-k
     // (keys f2u(max), [B][ceil(n / 64)]) -- a block whose key is below the
     // threshold holds no band doc and its scores are never read: ~1 block in
-    // 18 at 1M docs (883 band docs / query), instead of the whole 4 MB row
+    // 18 at 1M docs (883 band docs / query), instead of the whole 4 MB row.
+    // A workgroup takes 64 consecutive block keys (one per lane, read by every
+    // wave); the qualifying blocks are dealt to its waves in turn, and a wave
+    // reads 4 of them per step (16 lanes per block, a float4 each): at a small
+    // shard most blocks qualify (125k docs: the band spans most of the
+    // 1,954 blocks) and ~31 workgroups share them.
     const int64_t nb = (n + 63) >> 6;
     const uint32_t* krow = bm + (size_t)b * nb;
     const uint32_t uthr = f2u(thr);
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int64_t g0 = ((int64_t)blockIdx.x * nw + wave) * 64; g0 < nb; g0 += (int64_t)gridDim.x * nw * 64) {
+    const int c16 = lane & 15, r4 = lane >> 4;
+    const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(T) & 15) == 0;
+    for (int64_t g0 = (int64_t)blockIdx.x * 64; g0 < nb; g0 += (int64_t)gridDim.x * 64) {
       const int64_t kb = g0 + lane;   // one block key per lane
-      uint64_t qual = __ballot(kb < nb && krow[kb] >= uthr);
-      while (qual != 0) {             // wave-uniform; up to 4 qualifying blocks' scores in flight
-        int64_t blk[4];
-        float v[4];
+      const uint64_t qual = __ballot(kb < nb && krow[kb] >= uthr);
+      uint64_t mine = 0;              // this wave's share: qualifying blocks q = wave (mod nw)
+      int q = 0;
+      for (uint64_t m = qual; m != 0; m &= m - 1, ++q)
+        if (q % nw == wave) mine |= m & (~m + 1);
+      while (mine != 0) {             // wave-uniform; 4 blocks per step
+        int64_t blk = -1;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          blk[u] = -1;
-          if (qual != 0) {
-            blk[u] = g0 + (__ffsll((long long)qual) - 1);
-            qual &= qual - 1;
-          }
-          const int64_t i = blk[u] >= 0 ? (blk[u] << 6) + lane : n;
-          v[u] = i < n ? row[i] : 0.0f;
+          const int64_t bu = mine != 0 ? g0 + (__ffsll((long long)mine) - 1) : -1;
+          if (mine != 0) mine &= mine - 1;
+          if (u == r4) blk = bu;
+        }
+        const int64_t i0 = blk >= 0 ? (blk << 6) + 4 * c16 : n;
+        float v[4];
+        if (vec && i0 + 3 < n) {
+          const f32x4 x4 = *reinterpret_cast<const f32x4*>(row + i0);
+          v[0] = x4[0], v[1] = x4[1], v[2] = x4[2], v[3] = x4[3];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = i0 + e < n ? row[i0 + e] : 0.0f;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (blk[u] >= 0) offer((blk[u] << 6) + lane, v[u]);
+        for (int e = 0; e < 4; ++e) offer(i0 + e < n ? i0 + e : n, v[e]);
       }
     }
   } else {
@@ -4758,6 +5042,24 @@ struct ScanSplit {
   int ring_slot = -1;   // >= 0: the handle's ring slot, released by finish_split
 };
 
+// The task-counter block of the scans this host thread issues next (a caller's
+// workspace counters, ctr_ws): kCtrDefault zeroes what the launch's tail uses;
+// kCtrPrezeroed -- an earlier launch on the stream zeroed the whole block (the
+// faithful query split): no memset; kCtrZeroAll -- zero the whole block, tail
+// or not (arrival counters of later launches live past the tail's; plan_split
+// records in g_ctr_zeroed that it did).  Set with CtrPolicy around the call.
+constexpr int kCtrDefault = 0, kCtrPrezeroed = 1, kCtrZeroAll = 2;
+thread_local int g_ctr_policy = kCtrDefault;
+thread_local bool g_ctr_zeroed = false;
+struct CtrPolicy {
+  int prev;
+  explicit CtrPolicy(int p) : prev(g_ctr_policy) {
+    g_ctr_policy = p;
+    g_ctr_zeroed = false;
+  }
+  ~CtrPolicy() { g_ctr_policy = prev; }
+};
+
 int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, int task_docs, hipStream_t st,
                ScanSplit* sp, int* ctr_ws) {
   int64_t n_chunks = target / nq_groups;   // never more workgroups than resident slots
@@ -4787,8 +5089,17 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
       sp->ctr = ix->task_ring + (size_t)slot * kRingInts;
       sp->ring_slot = (int)slot;
     }
-    CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sp->slices * sizeof(int), st));
+    if (ctr_ws == nullptr || g_ctr_policy == kCtrDefault) {
+      CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sp->slices * sizeof(int), st));
+    } else if (g_ctr_policy == kCtrZeroAll) {
+      CBV2_HIP(hipMemsetAsync(sp->ctr, 0, kCtrBytes, st));
+      g_ctr_zeroed = true;
+    }
   } else {
+    if (ctr_ws != nullptr && g_ctr_policy == kCtrZeroAll) {
+      CBV2_HIP(hipMemsetAsync(ctr_ws, 0, kCtrBytes, st));
+      g_ctr_zeroed = true;
+    }
     sp->chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
     n_chunks = (ix->n + sp->chunk_docs - 1) / sp->chunk_docs;
     sp->static_docs = ix->n;
@@ -5309,17 +5620,31 @@ size_t bm_ws_bytes(int32_t B, int64_t n) {
   return ((size_t)B * (size_t)(bm_blocks(n) + bm_supers(n)) * 4 + 255) & ~(size_t)255;
 }
 
-// blocks_ready: bm already holds the block maxima (folded into the scan)
+// blocks_ready: bm already holds the block maxima (folded into the scan).
+// done (nullable; B <= kBmFusedMaxB): zeroed per-row arrival counters -- the
+// block maxima and the select then run in ONE launch (bmax_topk_kernel).
+constexpr int kBmFusedMaxB = 8;
+constexpr int kBmDoneOff = kRingInts - kBmFusedMaxB;   // cbv2_search's arrival counters in its counter block
 int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, uint32_t* bm,
-              float* out_s, int32_t* out_i, hipStream_t st, int dev, bool blocks_ready = false) {
+              float* out_s, int32_t* out_i, hipStream_t st, int dev, bool blocks_ready = false,
+              int32_t* done = nullptr, int64_t done_ld = 1) {
   static std::atomic<bool> attr_set[64] = {};
   if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
-    CBV2_HIP(hipFuncSetAttribute((const void*)topk_bmax_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)(kBmFixedLds + (size_t)(kBmMaxBlocks / 4) * 4)));
+    const int lds_max = (int)(kBmFixedLds + (size_t)(kBmMaxBlocks / 4) * 4);
+    CBV2_HIP(hipFuncSetAttribute((const void*)topk_bmax_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
+    CBV2_HIP(hipFuncSetAttribute((const void*)bmax_topk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
     if (dev >= 0 && dev < 64) attr_set[dev].store(true, std::memory_order_relaxed);
   }
   const int64_t nb = bm_blocks(n), ns = bm_supers(n);
   uint32_t* sb = bm_super_keys(bm, B, n);
+  if (!blocks_ready && done != nullptr && B <= kBmFusedMaxB) {
+    const size_t lds = kBmFixedLds + (size_t)ns * 4;
+    hipLaunchKernelGGL(bmax_topk_kernel, dim3((unsigned)((nb + kBmFusedBlocksPerWg - 1) / kBmFusedBlocksPerWg),
+                                               (unsigned)B),
+                       dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm, nb, sb, ns, done, done_ld, out_s,
+                       out_i);
+    return launch_check("bmax_topk_kernel");
+  }
   if (!blocks_ready) {
     hipLaunchKernelGGL(block_max_kernel, dim3((unsigned)((nb + kBmBlocksPerWg - 1) / kBmBlocksPerWg), (unsigned)B),
                        dim3(256), 0, st, scores, n, ld, bm, nb, sb, ns);
@@ -5489,7 +5814,8 @@ struct F32Ws {
   float* beta = nullptr;
   float* lb = nullptr;        // SEARCH: the two-pass band's bound, order-preserving bits (atomic min)
   int32_t* count = nullptr;
-  int32_t* done = nullptr;    // SEARCH: finished-workgroup counter per row (reset by the split)
+  int32_t* done = nullptr;    // SEARCH: the fallback's finished-workgroup counter per row (zeroed by the split)
+  int32_t* arrive = nullptr;  // [kArriveSlots][B][kArriveInts] row_last_arrival counters (zeroed by the split)
   int32_t* cand = nullptr;
   float* F = nullptr;
   void* tk = nullptr;
@@ -5506,6 +5832,13 @@ struct F32Ws {
   int32_t* pair_c = nullptr;
 };
 
+// Per-row arrival counters of a faithful workspace (F32Ws::arrive, row b of
+// slot j at (j * B + b) * kArriveInts): the launches whose last workgroup per
+// row runs the row's selection (row_last_arrival).
+constexpr int kArriveSlots = kArriveSlotsK;
+constexpr int kArrBmax = 0, kArrBand = 1, kArrRerank = 2;
+inline int32_t* arrive_row0(const F32Ws& w, int slot, int B) { return w.arrive + (size_t)slot * B * kArriveInts; }
+
 // op SCORE: split queries; RERANK: + F [B][C]; SEARCH: + band [B][cap] + scan.
 size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8_t* base, F32Ws* w) {
   size_t off = 0;
@@ -5521,6 +5854,7 @@ size_t f32_ws_layout(const cbv2_index* ix, int op, int B, int lq, int cap, uint8
   w->beta = (float*)take((size_t)B * sizeof(float));
   if (op == CBV2_F32_SEARCH) w->lb = (float*)take((size_t)B * sizeof(float));
   if (op == CBV2_F32_RERANK) w->F = (float*)take((size_t)B * cap * sizeof(float));
+  if (op != CBV2_F32_SCORE) w->arrive = (int32_t*)take((size_t)kArriveSlots * B * kArriveInts * sizeof(int32_t));
   if (op == CBV2_F32_SEARCH) {
     w->count = (int32_t*)take((size_t)B * sizeof(int32_t));
     w->done = (int32_t*)take((size_t)B * sizeof(int32_t));
@@ -5592,10 +5926,14 @@ bool split_holds(const cbv2_index* ix, const float* Q, int B, int lq, const void
   return false;
 }
 
-int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st, int count0 = 0) {
+// zero_ctr: the split also zeroes the scan's task-counter block (w->ctr; the
+// search's scan then runs under CtrPrezeroed and skips its memset launch).
+int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st, int count0 = 0,
+                  bool zero_ctr = false) {
   note_split(ix, Q, B, lq, w->qhi);
   hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(512), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
-                     ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0);
+                     ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0,
+                     w->arrive, kArriveSlots * kArriveInts, zero_ctr ? w->ctr : nullptr, zero_ctr ? kRingInts : 0);
   return launch_check("split_query_kernel");
 }
 
@@ -5607,12 +5945,13 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
                    int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
                    const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr, int64_t c0 = 0,
                    float* fb_T = nullptr, int32_t* fb_done = nullptr, int fb_k = 0, float* fb_s = nullptr,
-                   int32_t* fb_i = nullptr) {
-  if (limit <= c0 && fb_T == nullptr) return CBV2_OK;
+                   int32_t* fb_i = nullptr, const RowSelect& rs = RowSelect()) {
+  if (limit <= c0 && fb_T == nullptr && rs.mode == kSelNone) return CBV2_OK;
   if (ix->rescore_split) {   // one pair per workgroup (its doc split over 4 waves, or 2 for launches past
                              // the chip's resident 4-wave workgroups: one round of 2-wave ones instead of two)
     int64_t span = limit - c0;   // (pairs [c0, min(count, limit)) of a row)
     if (fb_T != nullptr) span = std::max<int64_t>(span, std::min<int64_t>(ix->n, 256));   // the fallback's grid
+    if (span < 1) span = 1;      // a row select runs in the row's (last) workgroup even with no pair to score
     // workgroups per row: ~4k per launch, 256..1024 per row -- a row's pairs
     // beyond that grid-stride (band at 1M docs, grid 1024 / 512 / 256: B=256
     // 2.76 / 2.64 / 2.57 ms, B=16 0.247 / 0.238 / 0.225, B=1 39 / 40 / 41 us;
@@ -5625,10 +5964,11 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
                               : (two ? rescore_split_kernel<false, 2> : rescore_split_kernel<false, 4>);
     hipLaunchKernelGGL(kern, dim3(gx, (unsigned)B), dim3(two ? 128 : 256), 0, st, ix->tokens, ix->resid, ix->doclens,
                        ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out, only_neg,
-                       (int)ix->ld, lb_min, c0, fb_T, fb_done, fb_k, fb_s, fb_i);
+                       (int)ix->ld, lb_min, c0, fb_T, fb_done, fb_k, fb_s, fb_i, rs);
     return launch_check("rescore_split_kernel");
   }
-  if (c0 != 0 || fb_T != nullptr) return fail(CBV2_EUNSUPPORTED, "pair offset / fallback need the split rescoring");
+  if (c0 != 0 || fb_T != nullptr || rs.mode != kSelNone)
+    return fail(CBV2_EUNSUPPORTED, "pair offset / fallback / row select need the split rescoring");
   if (pw <= 0) pw = (int64_t)B * limit <= kRsSmallPairs ? 1 : kRsPerWave;
   const int64_t per_wg = 4LL * pw;
   int64_t gx = (limit + per_wg - 1) / per_wg;
@@ -5881,8 +6221,17 @@ int cbv2_search(cbv2_index* ix, int32_t scorer, const void* Q, int32_t q_dtype, 
     uint32_t* bm = (uint32_t*)rest;
     float* sc = (float*)(rest + bm_ws_bytes(B, ix->n));
     const bool fold = scan_folds_bmax(ix, B);   // the B <= 2 streaming scans write the block maxima themselves
-    if ((rc = scan_maxsim_timed(ix, Q, B, lq, sc, ix->n, st, ctr, nullptr, fold ? bm : nullptr))) return rc;
-    return topk_bmax(sc, B, ix->n, ix->n, k, ix->id_base, bm, out_scores, out_ids, st, ix->device, fold);
+    // small batches select in the block-max launch's last workgroup: its
+    // per-row arrival counters sit at the end of the counter block, zeroed
+    // with the scan's task counters (no separate launch when the scan zeroes)
+    const bool fused = !fold && B <= kBmFusedMaxB;
+    int32_t* done = fused ? ctr + kBmDoneOff : nullptr;
+    {
+      CtrPolicy cp(fused ? kCtrZeroAll : kCtrDefault);
+      if ((rc = scan_maxsim_timed(ix, Q, B, lq, sc, ix->n, st, ctr, nullptr, fold ? bm : nullptr))) return rc;
+      if (fused && !g_ctr_zeroed) CBV2_HIP(hipMemsetAsync(done, 0, (size_t)B * sizeof(int32_t), st));
+    }
+    return topk_bmax(sc, B, ix->n, ix->n, k, ix->id_base, bm, out_scores, out_ids, st, ix->device, fold, done);
   }
   const size_t tk = topk_ws_bytes(B, ix->n);
   float* sc = (float*)(rest + tk);
@@ -6126,7 +6475,7 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     if ((rc = topk_impl_empty(B, k, out_scores, out_ids, st))) return rc;
     return 1;
   }
-  if ((rc = split_queries(ix, Q, B, lq, &w, st, want_lb && band_reuses_topk(ix, B, k) ? k : 0))) return rc;
+  if ((rc = split_queries(ix, Q, B, lq, &w, st, want_lb && band_reuses_topk(ix, B, k) ? k : 0, true))) return rc;
   if (k > kBandCapMax) {   // no band can hold k: every row takes the full faithful scan (status -1)
     CBV2_HIP(hipMemsetAsync(out_status, 0xff, (size_t)B * sizeof(int32_t), st));
     if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st))) return rc;
@@ -6137,10 +6486,13 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
   const bool bmax = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k);
   const bool fold = bmax && scan_folds_bmax(ix, B);
-  if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr, nullptr, fold ? (uint32_t*)w.tk : nullptr)))
-    return rc;
+  {
+    CtrPolicy cp(kCtrPrezeroed);   // the split zeroed the scan's counters
+    if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr, nullptr, fold ? (uint32_t*)w.tk : nullptr)))
+      return rc;
+  }
   if ((rc = bmax ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st,
-                             ix->device, fold)
+                             ix->device, fold, arrive_row0(w, kArrBmax, B), kArriveInts)
                  : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st,
                              ix->device)))
     return rc;
@@ -6182,6 +6534,11 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
   } else {
     // phase 1's block-max select left the rows' 64-doc block keys in w.tk
     const bool bkeys = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k) && ix->band_block_skip;
+    if (bkeys) {   // 64 block keys per workgroup, as many workgroups as that takes up to ~8 per CU
+      const int64_t per_row = (8LL * cu_count(ix->device) + B - 1) / B;
+      const int64_t groups = (bm_blocks(ix->n) + 63) / 64;
+      splits = std::max<int64_t>(1, std::min(per_row, groups));
+    }
     hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
                        out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb, lbu,
                        reuse ? out_ids : nullptr, bkeys ? reinterpret_cast<const uint32_t*>(w.tk) : nullptr);
@@ -6223,10 +6580,25 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
                          w.act, w.act_off, w.act_cnt, w.dctr, w.pair_b, w.pair_c, w.F, cap, (int)ix->ld);
       if ((rc = launch_check("rescore_docs_kernel"))) return rc;
     }
-  } else if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
-                                   B <= kBandPairMaxB ? 1 : 0, nullptr, c0, fb_fused ? w.T : nullptr,
-                                   fb_fused ? w.done : nullptr, k, out_scores, out_ids))) {
-    return rc;
+  } else {
+    // small batches (the latency path): the band select runs in the rescoring
+    // launch's last workgroup per row (select_band_row), no select launch
+    RowSelect rs;
+    if (fb_fused && B <= kBandPairMaxB) {
+      rs.mode = kSelBand;
+      rs.arrive = arrive_row0(w, kArrBand, B);
+      rs.k = k;
+      rs.out_s = out_scores;
+      rs.out_i = out_ids;
+      rs.lb = lb;
+      rs.lbu = lbu;
+      rs.status = out_status;
+    }
+    if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
+                             B <= kBandPairMaxB ? 1 : 0, nullptr, c0, fb_fused ? w.T : nullptr,
+                             fb_fused ? w.done : nullptr, k, out_scores, out_ids, rs)))
+      return rc;
+    if (rs.mode != kSelNone) return CBV2_OK;   // selected (and the fallback run) in that launch
   }
   hipLaunchKernelGGL(band_select_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, w.F, w.cand, w.count, cap, k,
                      ix->id_base, out_scores, out_ids, out_status, lb, lbu);
@@ -6263,10 +6635,24 @@ int search_f32_phase2(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int32_t 
 
 // The faithful rerank after its query split: rescoring of the C candidates
 // (raw scores), then the top-k select (k == 0: the raw scores themselves).
+// arrive (nullable): the rerank slot's zeroed arrival counters -- the select
+// then runs in the rescoring launch's last workgroup per row (C <= kSmallMax).
 int rerank_f32_split(cbv2_index* ix, F32Ws& w, int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k,
-                     float* out_scores, int32_t* out_ids, int32_t* out_pos, hipStream_t st) {
+                     float* out_scores, int32_t* out_ids, int32_t* out_pos, hipStream_t st,
+                     int32_t* arrive = nullptr) {
   int rc;
   float* raw = k == 0 ? out_scores : w.F;
+  if (k > 0 && C <= kSmallMax && arrive != nullptr && ix->rescore_split) {
+    RowSelect rs;
+    rs.mode = kSelCand;
+    rs.arrive = arrive;
+    rs.k = k;
+    rs.out_s = out_scores;
+    rs.out_i = out_ids;
+    rs.out_p = out_pos;
+    return launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
+                          nullptr, nullptr, rs);
+  }
   if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
   if (k == 0) return CBV2_OK;
   if (C > kSmallMax) return topk_multi(raw, B, C, C, k, 0, cand, C, out_scores, out_ids, out_pos, st);
@@ -6356,7 +6742,7 @@ int cbv2_rerank_f32(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, const
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
   hipStream_t st = (hipStream_t)stream;
   if ((rc = split_queries(ix, Q, B, lq, &w, st))) return rc;
-  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st);
+  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st, arrive_row0(w, kArrRerank, B));
 }
 
 // Internal (retrieve.cpp): cbv2_rerank_f32 for the queries a cbv2_search_f32
@@ -6384,15 +6770,18 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
   DeviceGuard dg(ix->device);
   if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
   const hipStream_t st = (hipStream_t)stream;
+  int32_t* arrive;   // zeroed by the split the rerank reads
   if (split_holds(ix, Q, B, lq, sw.qhi)) {
     w.qhi = sw.qhi;
     w.qlo = sw.qlo;
+    arrive = arrive_row0(sw, kArrRerank, B);
   } else {
     CBV2_REQUIRE(Q != nullptr, "null queries");
     int rc = split_queries(ix, Q, B, lq, &w, st);
     if (rc) return rc;
+    arrive = arrive_row0(w, kArrRerank, B);
   }
-  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st);
+  return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st, arrive);
 }
 
 // Internal (retrieve.cpp): the device an index lives on (-1: null index).

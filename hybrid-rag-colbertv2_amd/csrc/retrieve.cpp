@@ -128,6 +128,69 @@ int wait_copy(hipStream_t st, int dev, int32_t B) {
   return e == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "round-trip wait (%d)", (int)e);
 }
 
+// The fused candidates the one-shard rerank reads straight from host memory:
+// coherent, device-mapped pinned buffers (hipHostMallocMapped | Coherent; the
+// caller's host stage may be pageable or non-coherent pinned memory, so it is
+// never handed to a kernel).  The host RRF writes the [B][C] candidate ids
+// into one, and the rerank's workgroups read their candidate id through the
+// mapped pointer (one 4-byte PCIe read each): no H2D copy launch between the
+// host fusion and the rerank -- the latency path's host -> GPU hop is one
+// kernel launch.  A buffer goes back to the per-device pool with an event
+// recorded after the rerank that reads it; it is handed out again only once
+// that event completed, so a later call (any thread, any stream) never
+// overwrites candidates a queued rerank has still to read.
+struct MappedBuf {
+  void* h = nullptr;
+  void* d = nullptr;
+  size_t bytes = 0;
+  hipEvent_t ev = nullptr;
+  bool recorded = false;
+};
+struct MappedPool {
+  std::mutex mu;
+  std::vector<MappedBuf> free_buf[kMaxDev];
+};
+MappedPool& mapped_pool() {
+  static MappedPool* p = new MappedPool;   // never destroyed (buffers live for the process)
+  return *p;
+}
+
+// A buffer of >= bytes whose last reader finished; false: none could be made
+// (the caller falls back to the copy through its own host stage).
+bool take_mapped(int dev, size_t bytes, MappedBuf* out) {
+  MappedPool& P = mapped_pool();
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto& v = P.free_buf[dev];
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (v[i].bytes < bytes) continue;
+      if (v[i].recorded && hipEventQuery(v[i].ev) != hipSuccess) continue;   // still read by a queued rerank
+      *out = v[i];
+      v.erase(v.begin() + (long)i);
+      return true;
+    }
+  }
+  MappedBuf b;
+  b.bytes = std::max<size_t>(bytes, 64 * 1024);
+  if (hipHostMalloc(&b.h, b.bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+    return false;
+  if (hipHostGetDevicePointer(&b.d, b.h, 0) != hipSuccess ||
+      hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipHostFree(b.h);
+    return false;
+  }
+  *out = b;
+  return true;
+}
+
+void give_mapped(int dev, MappedBuf b, hipStream_t st) {
+  b.recorded = hipEventRecord(b.ev, st) == hipSuccess;
+  if (!b.recorded) (void)hipStreamSynchronize(st);   // cannot mark the reader: wait for it instead
+  MappedPool& P = mapped_pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.free_buf[dev].push_back(b);
+}
+
 // Selects the index's device for one call and restores the caller's.
 struct DevSel {
   int prev = -1, dev = -1;
@@ -298,16 +361,29 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     bm = H.lex_merged;
   }
   RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
-  if ((rc = wait_copy(st, ds.dev, B))) return rc;   // the one host round trip: the ColBERT (and merged BM25) top-k are here
-  if ((rc = cbv2_rrf_fuse(bm, kb, H.ids, k, B, rrf_k, C, H.cand, nullptr, nullptr))) return rc;
-  RT_HIP(hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st));
-  if (c)
-    return cbv2_rerank_sharded(ix, c, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
-  if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank when it is still there
-    return cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
-                                        B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos,
+  // one shard: the fused candidates go to a mapped buffer the rerank reads
+  // in place (no H2D launch); sharded: through the device workspace (the
+  // exchange's collectives read device memory)
+  MappedBuf mb;
+  const bool mapped = !c && ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, (size_t)B * C * 4, &mb);
+  int32_t* cand_h = mapped ? (int32_t*)mb.h : H.cand;
+  const int32_t* cand_d = mapped ? (const int32_t*)mb.d : L.cand;
+  rc = wait_copy(st, ds.dev, B);   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  if (!rc) rc = cbv2_rrf_fuse(bm, kb, H.ids, k, B, rrf_k, C, cand_h, nullptr, nullptr);
+  if (!rc && !mapped && hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+    rc = err(CBV2_EHIP, "candidate upload failed");
+  if (!rc) {
+    if (c)
+      rc = cbv2_rerank_sharded(ix, c, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+    else if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank when it is still there
+      rc = cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
+                                        B, lq, cand_d, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos,
                                         (const float*)Q, st);
-  return cbv2_rerank_ws(ix, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+    else
+      rc = cbv2_rerank_ws(ix, Q, B, lq, cand_d, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+  }
+  if (mapped) give_mapped(ds.dev, mb, st);   // free again once the rerank that reads it ran
+  return rc;
 }
 
 }  // extern "C"

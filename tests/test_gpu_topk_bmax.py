@@ -43,7 +43,11 @@ def _both(ix, Q, k):
 
 
 @pytest.mark.parametrize("n,B,k", [(65536, 1, 100), (100_003, 2, 100), (125_000, 5, 10), (100_000, 16, 100),
-                                   (70_001, 40, 1), (131_072, 64, 1024), (100_000, 256, 100)])
+                                   (70_001, 40, 1), (131_072, 64, 1024), (100_000, 256, 100),
+                                   # k large against the superblock count (k * 8 > n / 256): the
+                                   # threshold from block keys (advisor, round 4), streaming scan and
+                                   # the one-launch block-max select (B = 3-8)
+                                   (70_001, 1, 1024), (70_001, 4, 1024), (262_143, 2, 1024)])
 def test_bmax_equals_sampled_and_oracle_selection(dev, n, B, k):
     Q, tokens, doclens = _corpus(dev, n, B, seed=n % 97 + B)
     ix = ColbertIndex(tokens, doclens, id_base=17)
@@ -105,3 +109,21 @@ def test_bmax_faithful_search(dev, B):
     (s1, i1), (s0, i0) = _both(ix, Q, k)
     assert torch.equal(i1, i0) and torch.equal(s1, s0)
     assert all(set(i1[b, :10].tolist()) == set(planted[b].tolist()) for b in range(B))
+
+
+@pytest.mark.parametrize("B", [1, 2, 3, 8])
+def test_bmax_one_launch_dense_docs(dev, B):
+    """Dense-doc index (every doc 128 tokens: the 4 x 1 scan, whose keys the
+    one-launch bmax_topk_kernel writes and selects from, B <= 8) and a
+    repeated call (its arrival counters are re-zeroed by the last workgroup):
+    equal to the sampled path and to the oracle's selection."""
+    n, k = 125_000, 100
+    Qf = synth.make_queries(B, 32, seed=B)
+    planted = synth.planted_ids(B, n, 10, seed=B + 1)
+    tokens, doclens = synth.make_shard(0, n, Qf, planted, dev, seed=B)
+    ix = ColbertIndex(tokens, doclens)
+    Q = Qf.to(dev, torch.bfloat16)
+    (s1, i1), (s0, i0) = _both(ix, Q, k)
+    s2, i2 = ix.search(Q, k)
+    assert torch.equal(i1, i0) and torch.equal(s1, s0) and torch.equal(i2, i1) and torch.equal(s2, s1)
+    assert_selection_exact(i1.cpu().numpy(), s1.cpu().numpy(), ix.score(Q).cpu().numpy(), k)
