@@ -104,7 +104,8 @@ _SIGS = {
     "cbv2_index_kind": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "cbv2_retrieve_workspace_bytes": (_sz, [_p, _p, _i32, _i32, _i32, _i32, _i32]),
     "cbv2_retrieve_host_bytes": (_sz, [_i32, _i32, _i32, _i32]),
-    "cbv2_retrieve_wait_events": (_i64, []),
+    "cbv2_retrieve_host_marks": (ctypes.c_int, [_p, _i32]),
+    "cbv2_retrieve_pool_stats": (ctypes.c_int, [_p, _i32]),
     "cbv2_retrieve_begin": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _sz, _p]),
     "cbv2_retrieve_finish": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _i32, _i32, _i32,
                                             _p, _sz, _p, _sz, _p, _p, _p, _p]),

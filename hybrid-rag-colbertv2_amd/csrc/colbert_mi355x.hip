@@ -2551,7 +2551,17 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
 }
 
 // Sort sel[0..cnt) descending (padding to a power of two) and write the best k.
-__device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, float* out_s, int32_t* out_i) {
+// The ids of a selection also written straight to host memory (the latency
+// path's device-mapped buffer, read by the host after the stream's event):
+// system-scope write-through stores, so the host sees them once the kernel
+// has completed.
+__device__ __forceinline__ void st_host(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// mirror (nullable): out_i's values also to mirror[0..k) (st_host)
+__device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, float* out_s, int32_t* out_i,
+                               int32_t* mirror = nullptr) {
   int P = 1;
   while (P < cnt) P <<= 1;
   for (int i = cnt + threadIdx.x; i < P; i += blockDim.x) sel[i] = 0;
@@ -2566,6 +2576,7 @@ __device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, f
     }
     out_s[j] = s;
     out_i[j] = id;
+    if (mirror != nullptr) st_host(mirror + j, id);
   }
 }
 
@@ -2936,7 +2947,7 @@ __device__ __forceinline__ bool row_last_arrival(int32_t* __restrict__ ctr, int 
 template <bool SC1 = false>
 __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int64_t id_base,
                               const uint32_t* __restrict__ brow, const uint32_t* __restrict__ srow, float* os,
-                              int32_t* oi, uint8_t* lds) {
+                              int32_t* oi, uint8_t* lds, int32_t* mirror = nullptr) {
   uint64_t* const sel = reinterpret_cast<uint64_t*>(lds);   // [kBmCand]
   uint32_t* const hist = reinterpret_cast<uint32_t*>(sel + kBmCand);   // [2048]
   uint32_t* const qual = hist + 2048;                              // [kBmQual]
@@ -2961,7 +2972,31 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
   //    block whose key is >= t
   const int nk = by_block ? nb : ns;
   uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < nk ? kk : nk);
-  for (int p = 0; p < 2; ++p) {
+  // rows of at most one superblock key per thread (n <= 262,144 at 1,024
+  // threads: the shards of a multi-GPU node): the kk-th largest key EXACTLY,
+  // by counting -- key u is it when fewer than kk keys exceed it and at least
+  // kk reach it -- one pass over the keys in LDS (broadcast reads) instead of
+  // two radix passes and their six barriers; an exact t is never looser than
+  // the rounded one, and the select below does not depend on which is used
+  const bool by_count = !by_block && ns <= nth;
+  if (by_count) {
+    if (tid < ns) {
+      const uint32_t u = keys[tid];
+      uint32_t gt = 0, ge = 0;
+      for (int j = 0; j < ns; ++j) {
+        const uint32_t v = keys[j];
+        gt += v > u ? 1u : 0u;
+        ge += v >= u ? 1u : 0u;
+      }
+      if (gt < kleft && kleft <= ge) misc[4] = u;   // every such thread writes the same key
+    }
+    __syncthreads();
+    prefix = misc[4];
+    __syncthreads();
+    if (tid == 4) misc[4] = 0;
+    __syncthreads();
+  }
+  for (int p = 0; p < (by_count ? 0 : 2); ++p) {
     const int shift = 21 - 11 * p;
     for (int b = tid; b < 2048; b += nth) hist[b] = 0;
     __syncthreads();
@@ -3024,14 +3059,16 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
       if (r < k) {
         os[r] = u2f((uint32_t)(key >> 32));
         oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+        if (mirror != nullptr) st_host(mirror + r, oi[r]);
       }
     }
     for (int j = m + tid; j < k; j += nth) {
       os[j] = neg_inf();
       oi[j] = -1;
+      if (mirror != nullptr) st_host(mirror + j, -1);
     }
   } else {
-    sort_and_write(sel, m, k, id_base, os, oi);
+    sort_and_write(sel, m, k, id_base, os, oi, mirror);
   }
 }
 
@@ -3039,11 +3076,12 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
                                                                int k, int64_t id_base, const uint32_t* __restrict__ bm,
                                                                int64_t bm_ld, const uint32_t* __restrict__ sb,
                                                                int64_t sb_ld, float* __restrict__ out_s,
-                                                               int32_t* __restrict__ out_i) {
+                                                               int32_t* __restrict__ out_i,
+                                                               int32_t* __restrict__ mirror = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   const int row = blockIdx.x;
   topk_bmax_row(scores + (size_t)row * ld, n, k, id_base, bm + (size_t)row * bm_ld, sb + (size_t)row * sb_ld,
-                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn);
+                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn, mirror ? mirror + (size_t)row * k : nullptr);
 }
 
 // Block-max top-k in ONE launch (small batches, the latency path): grid (P, B)
@@ -3057,7 +3095,8 @@ __global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __re
                                                                int k, int64_t id_base, uint32_t* __restrict__ bm,
                                                                int64_t bm_ld, uint32_t* __restrict__ sb, int64_t sb_ld,
                                                                int32_t* __restrict__ done, int64_t done_ld,
-                                                               float* __restrict__ out_s, int32_t* __restrict__ out_i) {
+                                                               float* __restrict__ out_s, int32_t* __restrict__ out_i,
+                                                               int32_t* __restrict__ mirror) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   __shared__ int s_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -3100,7 +3139,8 @@ __global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __re
   }
   // <= 96 workgroups per row (n <= 64 * kBmMaxBlocks): one counter
   if (!row_last_arrival(done + (size_t)row * done_ld, (int)gridDim.x, 1, &s_last)) return;
-  topk_bmax_row<true>(x, n, k, id_base, brow, srow, out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn);
+  topk_bmax_row<true>(x, n, k, id_base, brow, srow, out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn,
+                      mirror ? mirror + (size_t)row * k : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -3760,6 +3800,7 @@ struct RowSelect {
   const float* lb = nullptr;     // kSelBand: a lower bound of the row's k-th score (nullable), or
   const uint32_t* lbu = nullptr; //   its order-preserving bits (the two-pass band's)
   int32_t* status = nullptr;     // kSelBand: the band size (the fallback writes -1 for overflowed rows)
+  int32_t* ids_mirror = nullptr; // kSelBand: [B][k] host mirror of the final ids (nullable; st_host)
 };
 constexpr int kSelNone = 0, kSelCand = 1, kSelBand = 2;
 
@@ -3783,7 +3824,8 @@ __device__ void select_cand_row(const float* raw, const int32_t* crow, int C, in
 // a global bound) the kk-th largest key is found by six radix passes over all
 // the keys and the kk keys at or above it are ranked.
 __device__ void select_band_row(const float* F, const int32_t* cand, int cnt, int k, int64_t id_base, bool has_lb,
-                                float lbv, float* os, int32_t* oi, uint64_t* sel, uint32_t* hist, uint32_t* misc) {
+                                float lbv, float* os, int32_t* oi, uint64_t* sel, uint32_t* hist, uint32_t* misc,
+                                int32_t* mirror) {
   const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6;
   const int kk = k < cnt ? k : cnt;
   auto key_at = [&](int i) { return rank_key(ld_sc1(F + i), (uint32_t)((int64_t)cand[i] - id_base)); };
@@ -3840,11 +3882,13 @@ __device__ void select_band_row(const float* F, const int32_t* cand, int cnt, in
     if (r < k) {
       os[r] = u2f((uint32_t)(key >> 32));
       oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+      if (mirror != nullptr) st_host(mirror + r, oi[r]);
     }
   }
   for (int j = m + tid; j < k; j += nth) {
     os[j] = neg_inf();
     oi[j] = -1;
+    if (mirror != nullptr) st_host(mirror + j, -1);
   }
 }
 
@@ -3891,7 +3935,8 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
       __threadfence();   // every workgroup's scores of the row are in
       const int kk = (int)((int64_t)fb_k < n ? fb_k : n);
       topk_exact_row(row, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
-      sort_and_write(sel, kk, fb_k, id_base, fb_s + (size_t)b * fb_k, fb_i + (size_t)b * fb_k);
+      sort_and_write(sel, kk, fb_k, id_base, fb_s + (size_t)b * fb_k, fb_i + (size_t)b * fb_k,
+                     rs.ids_mirror ? rs.ids_mirror + (size_t)b * fb_k : nullptr);
       if (rs.mode == kSelBand && threadIdx.x == 0) rs.status[b] = -1;
       return;
     }
@@ -3927,7 +3972,8 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     const bool has_lb = rs.lb != nullptr || rs.lbu != nullptr;
     const float lbv = rs.lbu != nullptr ? u2f(rs.lbu[b]) : (rs.lb != nullptr ? rs.lb[b] : 0.0f);
     select_band_row(out + (size_t)b * ld_out, cand + (size_t)b * ld_c, (int)lim, rs.k, id_base, has_lb, lbv,
-                    rs.out_s + (size_t)b * rs.k, rs.out_i + (size_t)b * rs.k, sel, hist, misc);
+                    rs.out_s + (size_t)b * rs.k, rs.out_i + (size_t)b * rs.k, sel, hist, misc,
+                    rs.ids_mirror ? rs.ids_mirror + (size_t)b * rs.k : nullptr);
     if (threadIdx.x == 0) rs.status[b] = (int32_t)lim;
   }
 }
@@ -5049,6 +5095,12 @@ struct ScanSplit {
 // or not (arrival counters of later launches live past the tail's; plan_split
 // records in g_ctr_zeroed that it did).  Set with CtrPolicy around the call.
 constexpr int kCtrDefault = 0, kCtrPrezeroed = 1, kCtrZeroAll = 2;
+// The latency path's host mirror of a search's final ids (cbv2_retrieve_begin
+// sets it around its search, retrieve.cpp): the launches that write every
+// row's final ids also write them to this device-mapped host buffer and set
+// g_ids_mirror_used, so finish needs no D2H copy.
+thread_local int32_t* g_ids_mirror = nullptr;
+thread_local bool g_ids_mirror_used = false;
 thread_local int g_ctr_policy = kCtrDefault;
 thread_local bool g_ctr_zeroed = false;
 struct CtrPolicy {
@@ -5628,6 +5680,8 @@ constexpr int kBmDoneOff = kRingInts - kBmFusedMaxB;   // cbv2_search's arrival 
 int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, uint32_t* bm,
               float* out_s, int32_t* out_i, hipStream_t st, int dev, bool blocks_ready = false,
               int32_t* done = nullptr, int64_t done_ld = 1) {
+  int32_t* mirror = g_ids_mirror;
+  if (mirror != nullptr) g_ids_mirror_used = true;   // every row's ids written to it below
   static std::atomic<bool> attr_set[64] = {};
   if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
     const int lds_max = (int)(kBmFixedLds + (size_t)(kBmMaxBlocks / 4) * 4);
@@ -5642,7 +5696,7 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
     hipLaunchKernelGGL(bmax_topk_kernel, dim3((unsigned)((nb + kBmFusedBlocksPerWg - 1) / kBmFusedBlocksPerWg),
                                                (unsigned)B),
                        dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm, nb, sb, ns, done, done_ld, out_s,
-                       out_i);
+                       out_i, mirror);
     return launch_check("bmax_topk_kernel");
   }
   if (!blocks_ready) {
@@ -5652,7 +5706,7 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   }
   const size_t lds = kBmFixedLds + (size_t)ns * 4;
   hipLaunchKernelGGL(topk_bmax_kernel, dim3((unsigned)B), dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm,
-                     nb, sb, ns, out_s, out_i);
+                     nb, sb, ns, out_s, out_i, mirror);
   return launch_check("topk_bmax_kernel");
 }
 
@@ -6491,11 +6545,13 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr, nullptr, fold ? (uint32_t*)w.tk : nullptr)))
       return rc;
   }
-  if ((rc = bmax ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st,
-                             ix->device, fold, arrive_row0(w, kArrBmax, B), kArriveInts)
-                 : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st,
-                             ix->device)))
-    return rc;
+  int32_t* const mirror = g_ids_mirror;   // the bf16 top-k is not the search's answer: no host mirror here
+  g_ids_mirror = nullptr;
+  rc = bmax ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st, ix->device,
+                        fold, arrive_row0(w, kArrBmax, B), kArriveInts)
+            : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device);
+  g_ids_mirror = mirror;
+  if (rc) return rc;
   if ((rc = band_mark(ix, false, st))) return rc;
   if (fk_out != nullptr)     // the bf16 top-k's own faithful scores, for the caller's cross-shard bound
     return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, fk_out, k, st);
@@ -6593,6 +6649,8 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
       rs.lb = lb;
       rs.lbu = lbu;
       rs.status = out_status;
+      rs.ids_mirror = g_ids_mirror;
+      if (g_ids_mirror != nullptr) g_ids_mirror_used = true;   // selected or fallen back, every row writes it
     }
     if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
                              B <= kBandPairMaxB ? 1 : 0, nullptr, c0, fb_fused ? w.T : nullptr,
@@ -6783,6 +6841,15 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
   }
   return rerank_f32_split(ix, w, B, lq, cand, C, k, out_scores, out_ids, out_pos, st, arrive);
 }
+
+// Internal (retrieve.cpp): the host mirror of the next search's final ids on
+// this thread (nullptr: none); cbv2_ids_mirror_used: whether the search just
+// issued writes it (then it holds every row's ids once the stream gets there).
+void cbv2_set_ids_mirror(int32_t* p) {
+  g_ids_mirror = p;
+  g_ids_mirror_used = false;
+}
+int cbv2_ids_mirror_used(void) { return g_ids_mirror_used ? 1 : 0; }
 
 // Internal (retrieve.cpp): the device an index lives on (-1: null index).
 int cbv2_index_device(const cbv2_index* ix) { return ix ? ix->device : -1; }

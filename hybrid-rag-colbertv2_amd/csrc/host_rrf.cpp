@@ -22,9 +22,14 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
                   int32_t rrf_k, int32_t C, int32_t* out_ids, double* out_scores, int32_t* out_count) {
   if (!(B >= 1 && C >= 1 && kb >= 0 && kc >= 0)) return cbv2_set_error(CBV2_EINVAL, "bad sizes");
   if (!((kb == 0 || bm25_ids) && (kc == 0 || colbert_ids) && out_ids)) return cbv2_set_error(CBV2_EINVAL, "null pointer");
-  std::vector<int32_t> ids;
-  std::vector<double> sc;
-  std::vector<int> order;
+  // per-thread scratch, reused across calls (the B = 1 latency path fuses
+  // 200 ids per call: allocation would be most of its cost)
+  thread_local std::vector<int32_t> ids, slot;
+  thread_local std::vector<double> sc;
+  thread_local std::vector<int> order;
+  thread_local std::vector<uint32_t> used;
+  ids.clear();
+  sc.clear();
   ids.reserve(kb + kc);
   sc.reserve(kb + kc);
   // id -> position in `ids` by open addressing (a power of two >= 2 (kb + kc)
@@ -35,8 +40,8 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
   int bits = 4;
   while ((1 << bits) < 2 * (kb + kc)) ++bits;
   const uint32_t mask = (1u << bits) - 1;
-  std::vector<int32_t> slot(mask + 1, -1);
-  std::vector<uint32_t> used;
+  slot.assign(mask + 1, -1);
+  used.clear();
   used.reserve(kb + kc);
   for (int32_t b = 0; b < B; ++b) {
     ids.clear();

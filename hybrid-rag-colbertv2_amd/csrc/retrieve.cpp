@@ -32,6 +32,8 @@ extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_w
                                             size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
                                             const float* Q, void* stream);
 extern "C" int cbv2_index_device(const cbv2_index* ix);
+extern "C" void cbv2_set_ids_mirror(int32_t* p);
+extern "C" int cbv2_ids_mirror_used(void);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -51,81 +53,55 @@ int err(int code, const char* fmt, ...) {
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// The round trip's wait: an event recorded after the D2H copy.  A blocking
-// wait wakes the host tens of microseconds after the copy lands (measured:
-// 26-39 us from the D2H copy's end to the next H2D copy's start), a poll
-// (hipEventQuery) within about a microsecond -- but a poll holds a core for
-// as long as the stream work ahead of the copy runs.  So only small batches
-// poll flat out: B <= kSpinMaxB (one scan of <= 8 queries: ~5-7 ms at 1M
-// docs, where a wake-up would be ~0.5 % of the latency), for at most kSpinNs,
-// then as below.
-// Larger batches (one B=256 scan: ~140 ms, whose host side runs the BM25
-// threads meanwhile) poll between sleeps of 1/32 of the time waited so far
+// The round trip's wait: poll the stream until the work enqueued on it -- the
+// search and the D2H copy (or the ids' host mirror) -- has completed
+// (hipStreamQuery), small batches flat out, larger ones sleeping between
+// polls.  A blocking hipStreamSynchronize wakes the host tens of microseconds
+// after the work lands (measured: 26-39 us from the D2H copy's end to the
+// next H2D copy's start); a poll sees it within about a microsecond.  But a
+// poll holds a core for as long as the stream runs, so only B <= kSpinMaxB
+// (one scan of <= 8 queries: ~5-7 ms at 1M docs, where a wake-up would be
+// ~0.5 % of the latency) polls flat out, for at most kSpinNs, then as below;
+// larger batches (one B=256 scan: ~140 ms, whose host side runs the BM25
+// threads meanwhile) sleep between polls for 1/32 of the time waited so far
 // (20 us .. 500 us): the thread wakes at most ~3 % (and 0.5 ms) after the
-// copy and is asleep otherwise.  (hipEventSynchronize is no substitute:
-// measured on the GPU box, a B=256 call over 200k docs burned its whole
-// 28 ms wait on a core even with a hipEventBlockingSync event.)
-//
-// Events come from a process-wide pool per device: taken for one wait and
-// returned after it, so the pool holds at most as many events as threads
-// ever waited at once (cbv2_retrieve_wait_events counts them), none leaks per
-// thread, and an event is always created on the device of the index whose
-// stream it is recorded on (the caller's current device may differ).
+// work and is asleep otherwise (hipEventSynchronize is no substitute:
+// measured on the GPU box, a B=256 call over 200k docs burned its whole 28 ms
+// wait on a core even with a hipEventBlockingSync event).
+// Stream query rather than an event recorded after the copy (round 5 lab,
+// profiles/r05/latency_wait_ab.jsonl, same process, interleaved): B=1 p50 at a
+// 125k-doc faithful shard 726.1 -> 719.5 us, 1M 4713.9 -> 4709.5 -- the event
+// record is a marker packet of its own.  The stream must not be shared with
+// other threads' work while finish waits (it would wait for theirs too).
 constexpr long long kSpinNs = 50LL * 1000 * 1000;
 constexpr int32_t kSpinMaxB = 8;
 constexpr int kMaxDev = 64;
 
-struct EventPool {
-  std::mutex mu;
-  std::vector<hipEvent_t> free_ev[kMaxDev];
-  int64_t created = 0;
-};
-EventPool& pool() {
-  static EventPool* p = new EventPool;   // never destroyed: no teardown-order issue at exit
-  return *p;
-}
+// Lab knob (cbv2_set_wait_mode, internal): 1 = poll hipStreamQuery (default),
+// 0 = record an event after the copy and poll hipEventQuery (round 4's wait).
+int g_wait_mode = 1;
 
-int take_event(int dev, hipEvent_t* ev) {
-  EventPool& P = pool();
-  {
-    std::lock_guard<std::mutex> lk(P.mu);
-    auto& v = P.free_ev[dev];
-    if (!v.empty()) {
-      *ev = v.back();
-      v.pop_back();
-      return CBV2_OK;
+int wait_copy(hipStream_t st, int32_t B) {
+  hipEvent_t ev = nullptr;
+  if (g_wait_mode == 0) {
+    RT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (hipEventRecord(ev, st) != hipSuccess) {
+      (void)hipEventDestroy(ev);
+      return err(CBV2_EHIP, "hipEventRecord failed");
     }
   }
-  RT_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-  std::lock_guard<std::mutex> lk(P.mu);
-  ++P.created;
-  return CBV2_OK;
-}
-
-void give_event(int dev, hipEvent_t ev) {
-  EventPool& P = pool();
-  std::lock_guard<std::mutex> lk(P.mu);
-  P.free_ev[dev].push_back(ev);
-}
-
-// The caller has selected the index's device (DevSel below).
-int wait_copy(hipStream_t st, int dev, int32_t B) {
-  if (dev < 0 || dev >= kMaxDev) return hipStreamSynchronize(st) == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "sync failed");
-  hipEvent_t ev = nullptr;
-  if (int rc = take_event(dev, &ev)) return rc;
-  hipError_t e = hipEventRecord(ev, st);
   const auto t0 = std::chrono::steady_clock::now();
-  while (e == hipSuccess) {
-    e = hipEventQuery(ev);
-    if (e != hipErrorNotReady) break;
-    e = hipSuccess;
+  hipError_t q;
+  for (;;) {
+    q = ev ? hipEventQuery(ev) : hipStreamQuery(st);
+    if (q != hipErrorNotReady) break;
     const long long waited =
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     if (B > kSpinMaxB || waited > kSpinNs)   // a long wait: sleep between polls
       std::this_thread::sleep_for(std::chrono::nanoseconds(std::min(500000LL, std::max(20000LL, waited / 32))));
   }
-  give_event(dev, ev);
-  return e == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "round-trip wait (%d)", (int)e);
+  if (ev) (void)hipEventDestroy(ev);
+  return q == hipSuccess ? CBV2_OK : err(CBV2_EHIP, "round-trip wait (%d)", (int)q);
 }
 
 // The fused candidates the one-shard rerank reads straight from host memory:
@@ -149,6 +125,7 @@ struct MappedBuf {
 struct MappedPool {
   std::mutex mu;
   std::vector<MappedBuf> free_buf[kMaxDev];
+  int64_t created = 0;
 };
 MappedPool& mapped_pool() {
   static MappedPool* p = new MappedPool;   // never destroyed (buffers live for the process)
@@ -179,6 +156,10 @@ bool take_mapped(int dev, size_t bytes, MappedBuf* out) {
     (void)hipHostFree(b.h);
     return false;
   }
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    ++P.created;
+  }
   *out = b;
   return true;
 }
@@ -189,6 +170,54 @@ void give_mapped(int dev, MappedBuf b, hipStream_t st) {
   MappedPool& P = mapped_pool();
   std::lock_guard<std::mutex> lk(P.mu);
   P.free_buf[dev].push_back(b);
+}
+
+// begin -> finish: the mapped buffer a one-shard begin took for its call
+// ([B][k] ids mirrored by the search's final select | [B][C] fused
+// candidates), keyed by the workspace (begin and finish share it).
+struct Pending {
+  MappedBuf mb;
+  bool ids_mirrored = false;
+};
+std::mutex g_pending_mu;
+std::vector<std::pair<const void*, Pending>> g_pending;
+
+void put_pending(const void* ws, const Pending& p, int dev, hipStream_t st) {
+  Pending old;
+  bool had = false;
+  {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    for (auto& e : g_pending)
+      if (e.first == ws) {
+        old = e.second;
+        e.second = p;
+        had = true;
+        break;
+      }
+    if (!had) g_pending.emplace_back(ws, p);
+  }
+  if (had) give_mapped(dev, old.mb, st);   // a begin without its finish: the buffer goes back
+}
+
+bool take_pending(const void* ws, Pending* out) {
+  std::lock_guard<std::mutex> lk(g_pending_mu);
+  for (size_t i = 0; i < g_pending.size(); ++i)
+    if (g_pending[i].first == ws) {
+      *out = g_pending[i].second;
+      g_pending.erase(g_pending.begin() + (long)i);
+      return true;
+    }
+  return false;
+}
+
+// Host marks of this thread's last cbv2_retrieve_finish (steady_clock ns,
+// CLOCK_MONOTONIC on Linux): [0] enter, [1] D2H issued, [2] wait done, [3]
+// fusion done, [4] rerank enqueued, [5] exit (cbv2_retrieve_host_marks; the
+// latency lab lines them up with a kernel trace).
+thread_local int64_t t_marks[6] = {};
+inline void mark(int i) {
+  t_marks[i] = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // Selects the index's device for one call and restores the caller's.
@@ -297,10 +326,25 @@ size_t cbv2_retrieve_workspace_bytes(const cbv2_index* ix, const cbv2_comm* c, i
   return layout(ix, c, kd, B, lq, k, kb, C, nullptr).total;
 }
 
-int64_t cbv2_retrieve_wait_events(void) {
-  EventPool& P = pool();
+int cbv2_retrieve_host_marks(int64_t* out, int32_t max) {
+  if (!out || max < 0) return err(CBV2_EINVAL, "null output");
+  for (int i = 0; i < 6 && i < max; ++i) out[i] = t_marks[i];
+  return CBV2_OK;
+}
+
+void cbv2_set_wait_mode(int32_t mode) { g_wait_mode = mode; }
+
+int cbv2_retrieve_pool_stats(int64_t* out, int32_t max) {
+  if (!out || max < 0) return err(CBV2_EINVAL, "null output");
+  MappedPool& P = mapped_pool();
   std::lock_guard<std::mutex> lk(P.mu);
-  return P.created;
+  if (max > 0) out[0] = P.created;
+  if (max > 1) {
+    int64_t idle = 0;
+    for (int d = 0; d < kMaxDev; ++d) idle += (int64_t)P.free_buf[d].size();
+    out[1] = idle;
+  }
+  return CBV2_OK;
 }
 
 size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C) {
@@ -320,16 +364,34 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   if (!ds.ok) return err(CBV2_EHIP, "cannot select the index's device %d", ds.dev);
   if (c)
     return cbv2_search_sharded_local(ix, c, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, kb, L.base, L.stage2, stream);
+  // one shard: a mapped host buffer for this call -- the search's final select
+  // mirrors the ids into it (no D2H copy in finish) and the fusion writes the
+  // candidates the rerank reads from it
+  Pending pd;
+  const bool mapped = ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, (size_t)B * (k + C) * 4, &pd.mb);
+  cbv2_set_ids_mirror(mapped ? (int32_t*)pd.mb.d : nullptr);
+  int rc;
   if (kd.faithful)
-    return cbv2_search_f32(ix, (const float*)Q, B, lq, k, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
-                           L.base, L.stage2, L.s, L.ids, L.status, stream);
-  return cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
+    rc = cbv2_search_f32(ix, (const float*)Q, B, lq, k, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
+                         L.base, L.stage2, L.s, L.ids, L.status, stream);
+  else
+    rc = cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
+  pd.ids_mirrored = mapped && cbv2_ids_mirror_used() != 0;
+  cbv2_set_ids_mirror(nullptr);
+  if (mapped) {
+    if (rc == CBV2_OK)
+      put_pending(workspace, pd, ds.dev, (hipStream_t)stream);
+    else
+      give_mapped(ds.dev, pd.mb, (hipStream_t)stream);
+  }
+  return rc;
 }
 
 int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
                          int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
                          int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
                          size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+  mark(0);
   Kind kd;
   if (int rc = check_common(ix, &kd, c, Q, q_dtype, B, lq, k, kb)) return rc;
   if (C < 1 || final_k < 1) return err(CBV2_EINVAL, "C and final_k must be >= 1 (got %d, %d)", C, final_k);
@@ -360,16 +422,22 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     if (kb > 0) RT_HIP(hipMemcpyAsync(H.lex_merged, L.lex_ids, (size_t)B * kb * 4, hipMemcpyDeviceToHost, st));
     bm = H.lex_merged;
   }
-  RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
-  // one shard: the fused candidates go to a mapped buffer the rerank reads
-  // in place (no H2D launch); sharded: through the device workspace (the
-  // exchange's collectives read device memory)
-  MappedBuf mb;
-  const bool mapped = !c && ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, (size_t)B * C * 4, &mb);
-  int32_t* cand_h = mapped ? (int32_t*)mb.h : H.cand;
-  const int32_t* cand_d = mapped ? (const int32_t*)mb.d : L.cand;
-  rc = wait_copy(st, ds.dev, B);   // the one host round trip: the ColBERT (and merged BM25) top-k are here
-  if (!rc) rc = cbv2_rrf_fuse(bm, kb, H.ids, k, B, rrf_k, C, cand_h, nullptr, nullptr);
+  // one shard: the mapped buffer begin took -- the ids are already mirrored
+  // into it by the search's select (else copied down as for the sharded
+  // path), the fused candidates go into it and the rerank reads them in place
+  // (no H2D launch); sharded: through the device workspace (the exchange's
+  // collectives read device memory)
+  Pending pd;
+  const bool mapped = !c && take_pending(workspace, &pd);
+  const int32_t* ids_h = mapped && pd.ids_mirrored ? (const int32_t*)pd.mb.h : H.ids;
+  if (ids_h == H.ids) RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
+  mark(1);
+  int32_t* cand_h = mapped ? (int32_t*)pd.mb.h + (size_t)B * k : H.cand;
+  const int32_t* cand_d = mapped ? (const int32_t*)pd.mb.d + (size_t)B * k : L.cand;
+  rc = wait_copy(st, B);   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  mark(2);
+  if (!rc) rc = cbv2_rrf_fuse(bm, kb, ids_h, k, B, rrf_k, C, cand_h, nullptr, nullptr);
+  mark(3);
   if (!rc && !mapped && hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st) != hipSuccess)
     rc = err(CBV2_EHIP, "candidate upload failed");
   if (!rc) {
@@ -382,7 +450,9 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     else
       rc = cbv2_rerank_ws(ix, Q, B, lq, cand_d, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
   }
-  if (mapped) give_mapped(ds.dev, mb, st);   // free again once the rerank that reads it ran
+  mark(4);
+  if (mapped) give_mapped(ds.dev, pd.mb, st);   // free again once the rerank that reads it ran
+  mark(5);
   return rc;
 }
 

@@ -28,6 +28,8 @@ import torch
 from . import _lib
 from .bm25 import HostBM25, Stemmer, tokenize
 from .config import RAGConfig
+from .index import LQ_MAX as _LQ_MAX
+from .index import _stream_ptr as _stream_ptr_fn
 from .retriever import JinaColBERTRetriever
 
 
@@ -389,9 +391,12 @@ class OneTripRetriever:
         self.k, self.C, self.final_k, self.rrf_k = int(colbert_k), int(fused), int(final_k), int(rrf_k)
         self.lexical_k = int(lexical_k)
         self.device = index.device
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._ws = None
         self._host = None
         self._sized = None        # (B, lq, kb) -> (ws pointer, bytes): the sizes of the last call
+        self.record_marks = False   # latency lab: host timestamps of the last call in self.marks
+        self.marks = None
 
     def _buffers(self, B: int, lq: int, kb: int):
         if self._sized is not None and self._sized[0] == (B, lq, kb):
@@ -416,20 +421,24 @@ class OneTripRetriever:
         return out
 
     def __call__(self, Q: torch.Tensor, lexical=None):
-        from .index import LQ_MAX, _stream_ptr
+        t_enter = time.monotonic_ns() if self.record_marks else 0
         L = _lib.lib()
-        if Q.dim() == 3 and Q.shape[1] > LQ_MAX and self.comm is None:
+        shape = Q.shape
+        if len(shape) == 3 and shape[1] > _LQ_MAX and self.comm is None:
             return self._stages(Q, lexical)     # long queries: the index sums blocks of <= 32 tokens
-        if (Q.dim() == 3 and Q.is_contiguous() and Q.device == self.device and 1 <= Q.shape[1] <= LQ_MAX
-                and Q.shape[2] == 128 and Q.dtype == self._qdtype()):   # the index's query layout: no conversion
+        if (len(shape) == 3 and 1 <= shape[1] <= _LQ_MAX and shape[2] == 128 and Q.dtype == self._qdtype()
+                and Q.is_cuda and Q.get_device() == self._dev_index
+                and Q.is_contiguous()):   # the index's query layout: no conversion
             _keep, qptr, qdt, B, lq = Q, Q.data_ptr(), self._qabi, int(Q.shape[0]), int(Q.shape[1])
         else:
             _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
         kb_cap = self.lexical_k if callable(lexical) else (0 if lexical is None else int(np.shape(lexical)[1]))
         ws, wsb = self._buffers(B, lq, kb_cap)
-        st = _stream_ptr(self.device)
+        st = _stream_ptr_fn(self.device)
+        t_prep = time.monotonic_ns() if self.record_marks else 0
         _lib.check(L.cbv2_retrieve_begin(self.index._h, self.comm, qptr, qdt, B, lq, self.k, kb_cap, self.C,
                                          ws, wsb, st))
+        t_begun = time.monotonic_ns() if self.record_marks else 0
         lex_i = lex_s = None
         kb = 0
         if lexical is not None:       # stage 1 on the host while the GPU scans
@@ -452,6 +461,11 @@ class OneTripRetriever:
             lex_i.ctypes.data if kb else None, lex_s.ctypes.data if (kb and lex_s is not None) else None, kb,
             self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
             out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), st))
+        if self.record_marks:
+            c_marks = (ctypes.c_int64 * 6)()
+            L.cbv2_retrieve_host_marks(c_marks, 6)
+            self.marks = {"enter": t_enter, "prep": t_prep, "begun": t_begun, "finish": list(c_marks),
+                          "exit": time.monotonic_ns()}
         return out_s, out_i, out_p
 
     def _qdtype(self):

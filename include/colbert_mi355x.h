@@ -564,13 +564,20 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    Q pointer, B, lq); if anything split other queries into that workspace
  *    in between, finish splits Q again (same results either way).
  *  Both calls select the index's device themselves (the caller's current
- *    device may differ) and restore the caller's.  finish's wait polls for
- *    B <= 8 (a small scan: the wake-up of a blocking wait would be tens of
- *    microseconds of the latency) and sleeps in a blocking-sync event wait
- *    for larger batches, so it never holds a core for a whole batch scan.
- * cbv2_retrieve_wait_events: the events finish's waits have created in this
- *    process (a pool per device, reused across calls and threads: at most
- *    the number of threads that ever waited at once, per device and kind).
+ *    device may differ) and restore the caller's.  finish's wait polls the
+ *    stream (hipStreamQuery) -- flat out for B <= 8, sleeping between polls
+ *    for larger batches, so it never holds a core for a whole batch scan;
+ *    the stream must carry no other thread's work meanwhile.  A one-shard
+ *    call takes a device-mapped host buffer from a per-device pool at begin
+ *    (the search's final select writes the ids into it, the fused candidates
+ *    go into it and the rerank reads them in place) and returns it at finish,
+ *    reusable once that rerank has run.
+ * cbv2_retrieve_host_marks (diagnostic): host timestamps (steady_clock ns) of
+ *    this thread's last finish: enter, D2H issued, wait done, fusion done,
+ *    rerank enqueued, exit (max entries written, up to 6).
+ * cbv2_retrieve_pool_stats (diagnostic): [0] mapped buffers created in this
+ *    process, [1] buffers idle in the pools (at most the number of calls that
+ *    ever ran at once).
  * cbv2_index_kind: the index's dtype (CBV2_DTYPE_*) and whether a residual is
  *    attached (fp32-faithful, 1) or not (0).                                */
 #define CBV2_RETRIEVE_BAND_CAP 16384
@@ -578,7 +585,8 @@ int cbv2_index_kind(const cbv2_index* index, int32_t* dtype, int32_t* faithful);
 size_t cbv2_retrieve_workspace_bytes(const cbv2_index* index, const cbv2_comm* comm, int32_t B, int32_t lq,
                                      int32_t k, int32_t kb, int32_t C);
 size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C);
-int64_t cbv2_retrieve_wait_events(void);
+int cbv2_retrieve_host_marks(int64_t* out, int32_t max);
+int cbv2_retrieve_pool_stats(int64_t* out, int32_t max);
 int cbv2_retrieve_begin(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
                         int32_t k, int32_t kb, int32_t C, void* workspace, size_t workspace_bytes, void* stream);
 int cbv2_retrieve_finish(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,

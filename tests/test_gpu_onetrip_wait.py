@@ -1,20 +1,22 @@
 """GPU: the host side of the one-round-trip retrieve (csrc/retrieve.cpp) --
-how cbv2_retrieve_finish waits for its D2H copy, which device it records
-its event on, and when the fp32-faithful rerank may reuse begin's query
-split (HybridRetriever.retrieve, LRC:894-935).
+how cbv2_retrieve_finish waits for stage 2, which device it runs on, where
+its host buffers come from, and when the fp32-faithful rerank may reuse
+begin's query split (HybridRetriever.retrieve, LRC:894-935).
 
 Done =
 * a B = 256 finish sleeps in its wait: the process CPU time of a whole
   one-trip call (begin + finish, no stage 1) stays <= 5 ms while the GPU
   scans for tens of ms (a polling wait would burn the whole scan);
-* the wait's events come from a pool: 1,000 calls on 8 threads, polled (B =
-  1) and blocking (B = 16) waits, create at most 8 events per kind;
+* the one-shard call's device-mapped host buffers come from a pool: 1,000
+  calls on 8 threads (B = 1 and B = 16) create at most 16, every one back in
+  the pool at the end;
 * the caller's current device is restored after begin / finish, from a
   thread that never selected one (one GPU on the box: the index-on-another-
   device case itself needs a second device);
 * a faithful finish whose workspace got another query split between begin
   and finish (a search of other queries in the stage-1 callable) splits Q
   again: its results equal the composed stages on Q bit for bit."""
+import ctypes
 import threading
 import time
 
@@ -65,14 +67,15 @@ def test_large_batch_wait_sleeps(dev):
     assert out[1].shape == (B, KF)
 
 
-def test_wait_events_pooled_and_device_restored(dev):
+def test_mapped_buffers_pooled_and_device_restored(dev):
     N = 3000
     L = _lib.lib()
     Qf, _, tokens, doclens = _index(dev, N, 16, seed=9)
     ix = ColbertIndex(tokens, doclens)
     Q1, Q16 = Qf[:1].to(dev, torch.bfloat16).contiguous(), Qf.to(dev, torch.bfloat16)
     want1, want16 = [x.cpu() for x in _composed(ix, Q1)], [x.cpu() for x in _composed(ix, Q16)]
-    before = int(L.cbv2_retrieve_wait_events())
+    st0 = (ctypes.c_int64 * 2)()
+    L.cbv2_retrieve_pool_stats(st0, 2)
     errs, devs = [], []
 
     def body(t):
@@ -97,8 +100,12 @@ def test_wait_events_pooled_and_device_restored(dev):
     assert not any(t.is_alive() for t in ts), "a thread hung"
     if errs:
         raise errs[0]
-    created = int(L.cbv2_retrieve_wait_events()) - before
-    assert created <= 16, f"1,000 calls on 8 threads created {created} wait events"
+    torch.cuda.synchronize()
+    st1 = (ctypes.c_int64 * 2)()
+    L.cbv2_retrieve_pool_stats(st1, 2)
+    created = int(st1[0] - st0[0])
+    assert created <= 16, f"1,000 calls on 8 threads created {created} mapped buffers"
+    assert int(st1[1]) == int(st1[0]), "a mapped buffer was not returned to its pool"
     assert devs == [dev.index or 0] * 8
 
 

@@ -7,7 +7,13 @@ duration and the idle gap before it, and the scan-end -> last-event total.
 
   run:    rocprofv3 --kernel-trace --memory-copy-trace -f csv -d D -o t -- \
               python3 tools/b1_timeline.py --dtype fp32 --docs 1000000
-  parse:  python3 tools/b1_timeline.py --parse D"""
+  parse:  python3 tools/b1_timeline.py --parse D
+
+--marks F (run) records the host timestamps of every timed call (monotonic
+ns: Python entry, begin returned, cbv2_retrieve_host_marks of finish, exit,
+synchronize returned) into F; `--parse D --marks F` prints them on the
+kernel timeline (rocprofv3's timestamps are on the same clock when the first
+kernel of an iteration starts a few us after the Python entry)."""
 import argparse
 import csv
 import glob
@@ -50,6 +56,9 @@ def run(a):
         legs["bf16"] = (OneTripRetriever(ColbertIndex(ix.tokens, ix.doclens)),
                         Qf[:1].to(dev, torch.bfloat16).contiguous())
     lat = {k: [] for k in legs}
+    marks = []
+    for name, (one, _) in legs.items():
+        one.record_marks = bool(a.marks)
     for it in range(a.iters + 5):
         for name, (one, Q1) in legs.items():
             torch.cuda.synchronize()
@@ -59,6 +68,27 @@ def run(a):
             torch.cuda.synchronize()
             if it >= 5:
                 lat[name].append((time.perf_counter() - t) * 1e3)
+                if a.marks:
+                    marks.append(dict(one.marks, leg=name, it=it, synced=time.monotonic_ns()))
+    if a.marks:
+        with open(a.marks, "w") as f:
+            for m in marks:
+                f.write(json.dumps(m) + "\n")
+        for name in legs:   # host-only view (valid without a profiler attached)
+            ms = [m for m in marks if m["leg"] == name]
+            med = lambda f: round(statistics.median(f(m) for m in ms) / 1e3, 1)   # noqa: E731
+            print(json.dumps({"leg": name, "host_us": {
+                "prep": med(lambda m: m["prep"] - m["enter"]),
+                "begin_call": med(lambda m: m["begun"] - m["prep"]),
+                "begin_return_to_finish": med(lambda m: m["finish"][0] - m["begun"]),
+                "finish_to_D2H_issued": med(lambda m: m["finish"][1] - m["finish"][0]),
+                "D2H_issued_to_wait_done": med(lambda m: m["finish"][2] - m["finish"][1]),
+                "fusion": med(lambda m: m["finish"][3] - m["finish"][2]),
+                "rerank_enqueue": med(lambda m: m["finish"][4] - m["finish"][3]),
+                "finish_tail": med(lambda m: m["finish"][5] - m["finish"][4]),
+                "finish_exit_to_python_exit": med(lambda m: m["exit"] - m["finish"][5]),
+                "python_exit_to_synced": med(lambda m: m["synced"] - m["exit"]),
+                "total": med(lambda m: m["synced"] - m["enter"])}}), flush=True)
     from hybrid_rag_colbertv2_amd.index import hbm_placement
     for name, v in lat.items():
         print(json.dumps({"docs": n, "dtype": name, "iters": a.iters, "p50_ms": round(statistics.median(v), 4),
@@ -70,7 +100,7 @@ def short(name):
     return name.split("(")[0][:60]
 
 
-def parse(d, scan_key):
+def parse(d, scan_key, marks_path=None):
     kf = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     mf = glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=True)
     ev = []
@@ -90,9 +120,28 @@ def parse(d, scan_key):
     if cur:
         groups.append(cur)
     per_kind = {}
+    marks = [json.loads(x) for x in open(marks_path)] if marks_path else []
+    host = {}
     for g in groups:
         if not any(scan_key in e[2] for e in g):
             continue
+        if marks:   # the call whose entry precedes this iteration's first kernel by < 1 ms
+            t0 = g[0][0]
+            near = [m for m in marks if 0 <= t0 - m["enter"] < 1_000_000]
+            if near:
+                m = max(near, key=lambda m: m["enter"])
+                f = m["finish"]
+                last_end = max(e[1] for e in g)
+                copies = [e[1] for e in g if e[2].startswith("copy") and e[1] <= f[2]]
+                row = {"python entry -> first kernel start": t0 - m["enter"],
+                       "python prep (entry -> begin call)": m["prep"] - m["enter"],
+                       "begin returned (from first kernel start)": m["begun"] - t0,
+                       "finish entered": f[0] - t0, "D2H issued": f[1] - t0,
+                       "wait done - D2H copy end": f[2] - max(copies) if copies else None,
+                       "fusion": f[3] - f[2], "rerank enqueued - wait done": f[4] - f[2],
+                       "finish exit - wait done": f[5] - f[2], "python exit - last kernel end": m["exit"] - last_end,
+                       "synchronize returned - last kernel end": m["synced"] - last_end}
+                host.setdefault(m["leg"], []).append(row)
         rows, prev = [], g[0][0]
         for (a, b, nm) in g:
             rows.append((nm, (b - a) / 1e3, max(0, a - prev) / 1e3))
@@ -105,6 +154,12 @@ def parse(d, scan_key):
     for kind, per in per_kind.items():
         print(f"[{kind}]")
         _fold(per, scan_key)
+    for leg, rows in host.items():
+        print(f"[host marks, {leg}: {len(rows)} calls; medians in us]")
+        for key in rows[0]:
+            vals = [r[key] for r in rows if r[key] is not None]
+            if vals:
+                print(f"  {key:45s} {statistics.median(vals) / 1e3:9.1f}")
 
 
 def _fold(per, scan_key):
@@ -135,8 +190,9 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--parse", default=None, help="a rocprofv3 output directory to fold")
     ap.add_argument("--scan", default="maxsim_scan", help="substring naming the scan kernel")
+    ap.add_argument("--marks", default=None, help="host timestamps file (run: written; parse: read)")
     a = ap.parse_args()
     if a.parse:
-        parse(a.parse, a.scan)
+        parse(a.parse, a.scan, a.marks)
     else:
         run(a)
