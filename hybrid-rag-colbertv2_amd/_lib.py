@@ -105,6 +105,7 @@ _SIGS = {
     "cbv2_retrieve_workspace_bytes": (_sz, [_p, _p, _i32, _i32, _i32, _i32, _i32]),
     "cbv2_retrieve_host_bytes": (_sz, [_i32, _i32, _i32, _i32]),
     "cbv2_retrieve_host_marks": (ctypes.c_int, [_p, _i32]),
+    "cbv2_retrieve_cancel": (ctypes.c_int, [_p, _p, _p]),
     "cbv2_retrieve_pool_stats": (ctypes.c_int, [_p, _i32]),
     "cbv2_retrieve_begin": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _sz, _p]),
     "cbv2_retrieve_finish": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _i32, _i32, _i32,

@@ -485,9 +485,62 @@ struct NoTileHook {
 // PROBE (lab energy probe, INVALID scores): 1 = odd tiles reuse the even
 // tile's A fragments (half the LDS read bytes, same MFMAs); 2 (kernel) = no
 // doc streaming after the ring's first fill (no L2 -> LDS traffic).
+// PROBE 3 (lab power probe, INVALID scores): the same FLOPs on
+// v_mfma_f32_32x32x16_bf16 -- each pair of 16-row tiles as one 32-row tile of
+// 8 k-steps, one 16-register chain per query, its 16 values folded into the
+// running max (the same v_max3 count per FLOP as the 16x16 chains) -- with the
+// same LDS reads; half the register-operand bytes per FLOP of the 16x16x32
+// form.  Timing only: is the mid-batch scan's held clock (power) sensitive
+// to the operand path?
+template <int QW, int D, int NT>
+__device__ __forceinline__ void iter4_full_probe32(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
+                                                   float (&m)[QW][2]) {
+  static_assert(NT % 2 == 0, "tile pairs");
+  constexpr int NT2 = NT / 2, NK = NT2 * QW;
+  const int c = lane & 15, g = lane >> 4;
+  const uint8_t* rowp = buf + (4 * NT * (c >> 2) + (c & 3)) * kRowBytes;
+  auto frag = [&](int t, bf16x8 (&af)[8]) {   // tiles 2t, 2t + 1
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        af[4 * h + s] = *reinterpret_cast<const bf16x8*>(rowp + 4 * (2 * t + h) * kRowBytes + 16 * ((4 * g + s) ^ c));
+  };
+  // one A buffer (a second does not fit beside 4 queries' fragments): the next
+  // tile's fragments load right after the tile's last chain has issued, under
+  // that chain's MFMAs
+  bf16x8 a[8];
+  f32x16 acc[D + 1];
+  frag(0, a);
+#pragma unroll
+  for (int k = 0; k < NK + D; ++k) {
+    if (k < NK) {
+      const int t = k / QW, q = k % QW;
+      f32x16 x = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], qf[q][s >> 2][s & 3], x, 0, 0, 0);
+      acc[k % (D + 1)] = x;
+      if (q == QW - 1 && t + 1 < NT2) frag(t + 1, a);
+    }
+    if (k >= D) {
+      const int q = (k - D) % QW;
+      const f32x16& y = acc[(k - D) % (D + 1)];
+      float& mm = m[q][0];
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mm = fmaxf(fmaxf(mm, y[r]), y[r + 1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int QW, int D, int NT = 8, typename Hook = NoTileHook, int PROBE = 0>
 __device__ __forceinline__ void iter4_full(const uint8_t* buf, int lane, const bf16x8 (&qf)[QW][2][4],
                                            float (&m)[QW][2], Hook hook = Hook{}) {
+  if constexpr (PROBE == 3) {
+    iter4_full_probe32<QW, D, NT>(buf, lane, qf, m);
+    return;
+  }
   constexpr int NC = 2 * QW;
   constexpr int NK = NT * NC;
   const int c = lane & 15, g = lane >> 4;

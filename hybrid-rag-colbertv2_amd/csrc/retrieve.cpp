@@ -68,11 +68,12 @@ size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 // work and is asleep otherwise (hipEventSynchronize is no substitute:
 // measured on the GPU box, a B=256 call over 200k docs burned its whole 28 ms
 // wait on a core even with a hipEventBlockingSync event).
-// Stream query rather than an event recorded after the copy (round 5 lab,
-// profiles/r05/latency_wait_ab.jsonl, same process, interleaved): B=1 p50 at a
-// 125k-doc faithful shard 726.1 -> 719.5 us, 1M 4713.9 -> 4709.5 -- the event
-// record is a marker packet of its own.  The stream must not be shared with
-// other threads' work while finish waits (it would wait for theirs too).
+// Small batches poll the stream rather than an event recorded after the copy
+// (round 5 lab, profiles/r05/latency_wait_ab.jsonl, same process,
+// interleaved): B=1 p50 at a 125k-doc faithful shard 726.1 -> 719.5 us, 1M
+// 4713.9 -> 4709.5 -- the event record is a marker packet of its own.  The
+// stream must not be shared with other threads' work while finish waits (it
+// would wait for theirs too).  Large batches keep the event (below).
 constexpr long long kSpinNs = 50LL * 1000 * 1000;
 constexpr int32_t kSpinMaxB = 8;
 constexpr int kMaxDev = 64;
@@ -83,7 +84,10 @@ int g_wait_mode = 1;
 
 int wait_copy(hipStream_t st, int32_t B) {
   hipEvent_t ev = nullptr;
-  if (g_wait_mode == 0) {
+  // large batches poll an event between sleeps: a hipStreamQuery call held
+  // the core for the whole wait (measured: a B=256 call over 200k docs used
+  // 29 ms of CPU for its 29 ms wait even sleeping between queries)
+  if (g_wait_mode == 0 || B > kSpinMaxB) {
     RT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     if (hipEventRecord(ev, st) != hipSuccess) {
       (void)hipEventDestroy(ev);
@@ -334,6 +338,16 @@ int cbv2_retrieve_host_marks(int64_t* out, int32_t max) {
 
 void cbv2_set_wait_mode(int32_t mode) { g_wait_mode = mode; }
 
+int cbv2_retrieve_cancel(cbv2_index* ix, void* workspace, void* stream) {
+  if (!ix) return err(CBV2_EINVAL, "null index");
+  Pending pd;
+  if (!take_pending(workspace, &pd)) return CBV2_OK;   // nothing outstanding (sharded, or finished)
+  DevSel ds(ix);
+  if (!ds.ok) return err(CBV2_EHIP, "cannot select the index's device %d", ds.dev);
+  give_mapped(ds.dev, pd.mb, (hipStream_t)stream);      // reusable once begin's search has run
+  return CBV2_OK;
+}
+
 int cbv2_retrieve_pool_stats(int64_t* out, int32_t max) {
   if (!out || max < 0) return err(CBV2_EINVAL, "null output");
   MappedPool& P = mapped_pool();
@@ -430,11 +444,13 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
   Pending pd;
   const bool mapped = !c && take_pending(workspace, &pd);
   const int32_t* ids_h = mapped && pd.ids_mirrored ? (const int32_t*)pd.mb.h : H.ids;
-  if (ids_h == H.ids) RT_HIP(hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
+  rc = CBV2_OK;
+  if (ids_h == H.ids && hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    rc = err(CBV2_EHIP, "stage-2 ids copy failed");
   mark(1);
   int32_t* cand_h = mapped ? (int32_t*)pd.mb.h + (size_t)B * k : H.cand;
   const int32_t* cand_d = mapped ? (const int32_t*)pd.mb.d + (size_t)B * k : L.cand;
-  rc = wait_copy(st, B);   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  if (!rc) rc = wait_copy(st, B);   // the one host round trip: the ColBERT (and merged BM25) top-k are here
   mark(2);
   if (!rc) rc = cbv2_rrf_fuse(bm, kb, ids_h, k, B, rrf_k, C, cand_h, nullptr, nullptr);
   mark(3);

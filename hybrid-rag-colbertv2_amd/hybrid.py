@@ -439,6 +439,13 @@ class OneTripRetriever:
         _lib.check(L.cbv2_retrieve_begin(self.index._h, self.comm, qptr, qdt, B, lq, self.k, kb_cap, self.C,
                                          ws, wsb, st))
         t_begun = time.monotonic_ns() if self.record_marks else 0
+        try:
+            return self._finish(L, Q, lexical, qptr, qdt, B, lq, kb_cap, ws, wsb, st, t_enter, t_prep, t_begun)
+        except BaseException:
+            L.cbv2_retrieve_cancel(self.index._h, ws, st)   # begin's host buffer back to its pool
+            raise
+
+    def _finish(self, L, Q, lexical, qptr, qdt, B, lq, kb_cap, ws, wsb, st, t_enter, t_prep, t_begun):
         lex_i = lex_s = None
         kb = 0
         if lexical is not None:       # stage 1 on the host while the GPU scans

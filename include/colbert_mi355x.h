@@ -572,6 +572,8 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    (the search's final select writes the ids into it, the fused candidates
  *    go into it and the rerank reads them in place) and returns it at finish,
  *    reusable once that rerank has run.
+ * cbv2_retrieve_cancel: a begin that will not be finished (the caller's
+ *    stage 1 failed): returns its host buffer to the pool (no-op otherwise).
  * cbv2_retrieve_host_marks (diagnostic): host timestamps (steady_clock ns) of
  *    this thread's last finish: enter, D2H issued, wait done, fusion done,
  *    rerank enqueued, exit (max entries written, up to 6).
@@ -585,6 +587,7 @@ int cbv2_index_kind(const cbv2_index* index, int32_t* dtype, int32_t* faithful);
 size_t cbv2_retrieve_workspace_bytes(const cbv2_index* index, const cbv2_comm* comm, int32_t B, int32_t lq,
                                      int32_t k, int32_t kb, int32_t C);
 size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C);
+int cbv2_retrieve_cancel(cbv2_index* index, void* workspace, void* stream);
 int cbv2_retrieve_host_marks(int64_t* out, int32_t max);
 int cbv2_retrieve_pool_stats(int64_t* out, int32_t max);
 int cbv2_retrieve_begin(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,

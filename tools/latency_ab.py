@@ -5,7 +5,9 @@ the one-round-trip C++ path (hybrid.OneTripRetriever: cbv2_retrieve_begin /
 _finish), interleaved in one process on the same index.  Prints one JSON line
 per (docs, dtype) with p50 / p99 of each and the scan's own event time.
 
-usage: latency_ab.py [--docs 125000,1000000] [--dtype bf16] [--iters 200]"""
+usage: latency_ab.py [--docs 125000,1000000] [--dtype bf16] [--iters 200] [--root TREE --tag T]
+(--root: another tree's package, for a before/after of two builds on one box;
+`one_trip_minus_scan_us` = one-trip p50 - the scan's own event p50.)"""
 import argparse
 import json
 import os
@@ -17,6 +19,8 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if "--root" in sys.argv:
+    ROOT = os.path.abspath(sys.argv[sys.argv.index("--root") + 1])
 sys.path.insert(0, ROOT)
 from hybrid_rag_colbertv2_amd import bm25 as bm25_mod  # noqa: E402
 from hybrid_rag_colbertv2_amd import synth  # noqa: E402
@@ -29,6 +33,8 @@ def main():
     ap.add_argument("--docs", default="125000,1000000")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--root", default=ROOT)
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for n in (int(x) for x in a.docs.split(",")):
@@ -76,12 +82,15 @@ def main():
         torch.cuda.synchronize()
         scan = statistics.median(ix.scan_times()[-20:])
         ix.time_scans(False)
-        rec = {"docs": n, "dtype": a.dtype, "B": B, "iters": a.iters, "scan_event_ms_p50": round(scan, 4),
+        from hybrid_rag_colbertv2_amd import _lib
+        rec = {"tag": a.tag, "lib": _lib.lib().cbv2_build_stamp().decode(), "docs": n, "dtype": a.dtype, "B": B,
+               "iters": a.iters, "scan_event_ms_p50": round(scan, 4),
                "identical": same, "top10": out[1][0].tolist()[:3]}
         for name, v in lat.items():
             rec[name] = {"p50_ms": round(statistics.median(v), 4), "p99_ms": round(float(np.percentile(v, 99)), 4),
                          "min_ms": round(min(v), 4)}
         rec["p50_gain_us"] = round((rec["composed"]["p50_ms"] - rec["one_trip"]["p50_ms"]) * 1e3, 1)
+        rec["one_trip_minus_scan_us"] = round((rec["one_trip"]["p50_ms"] - scan) * 1e3, 1)
         print(json.dumps(rec), flush=True)
         del ix, one, lex
 

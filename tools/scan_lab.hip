@@ -402,6 +402,21 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
     return launch_scan16x4<4, 2, 2, 2, 2, false, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs);
   if (kind == 28 && stamps != nullptr)
     return launch_scan16x4<4, 2, 2, 2, 2, true, 32>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps);
+  // kinds 29-32 (round 5, power probe): the one-group non-temporal mid-batch
+  // shapes -- 29: 4 x 4 (B = 9-16, production kScan16x4W4Nt), 30: the same
+  // with PROBE 3 (INVALID: the FLOPs on v_mfma_f32_32x32x16_bf16); 31 / 32:
+  // 4 x 2 (B = 5-8) and its PROBE 3 build
+  // stamps != null: the STAMPS build of the same shape (per-workgroup clock)
+#define LAB_MID(W, QW_, D_, PR)                                                                                  \
+  return stamps ? launch_scan16x4<W, QW_, 2, D_, 2, true, 32, 2, false, 0, false, false, PR, kLd, 0, 2>(            \
+                      ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)                   \
+                : launch_scan16x4<W, QW_, 2, D_, 2, false, 32, 2, false, 0, false, false, PR, kLd, 0, 2>(           \
+                      ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr)
+  if (kind == 29) LAB_MID(4, 4, 2, 0);
+  if (kind == 30) LAB_MID(4, 4, 0, 3);
+  if (kind == 31) LAB_MID(4, 2, 2, 0);
+  if (kind == 32) LAB_MID(4, 2, 1, 3);
+#undef LAB_MID
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
