@@ -2608,13 +2608,51 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
 // path's device-mapped buffer, read by the host after the stream's event):
 // system-scope write-through stores, so the host sees them once the kernel
 // has completed.
-__device__ __forceinline__ void st_host(int32_t* p, int32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// The words are 8 bytes, {id, seq} (seq in the high half), LL-style: a word
+// is whole or absent, so the host polling them needs no ordering between the
+// stores -- every word of the call carries the call's seq once written.
+struct Mirror {
+  uint64_t* w = nullptr;
+  uint32_t seq = 0;
+  __device__ __forceinline__ void put(size_t i, int32_t id) const {
+    __hip_atomic_store(w + i, ((uint64_t)seq << 32) | (uint32_t)id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __device__ __host__ __forceinline__ Mirror row(size_t b, int k) const {
+    return Mirror{w ? w + b * (size_t)k : nullptr, seq};
+  }
+};
+
+// The pre-armed rerank of the latency path (retrieve.cpp): the rerank is
+// launched before the host has fused stage 1 and 2, and its candidates arrive
+// in a device-mapped host buffer as 8-byte words {id, seq} (whole or absent),
+// written by the host after the launch.  Thread 0 of a workgroup polls its
+// candidate's word (system-scope loads, s_sleep between polls) until the tag
+// is the call's seq -- so the host's fusion -> rerank hop costs a PCIe read,
+// not a kernel launch.  It never waits forever: after kCandWaitTicks of
+// s_memrealtime (100 MHz) the candidate reads as -1 (scores -inf), and the
+// host, which writes the words whatever happens (-1 words on its own
+// failure), reports an error then.
+struct TaggedCand {
+  const uint64_t* w = nullptr;
+  uint32_t seq = 0;
+};
+constexpr uint64_t kCandWaitTicks = 100000000ull;   // 1 s
+__device__ __forceinline__ int32_t wait_tagged(const uint64_t* w, uint32_t seq) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((uint32_t)(v >> 32) == seq) return (int32_t)(uint32_t)v;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kCandWaitTicks) return -1;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+__device__ __forceinline__ int32_t read_tagged(const uint64_t* w) {
+  return (int32_t)(uint32_t)__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// mirror (nullable): out_i's values also to mirror[0..k) (st_host)
+// mirror (w nullable): out_i's values also to mirror's words [0, k)
 __device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, float* out_s, int32_t* out_i,
-                               int32_t* mirror = nullptr) {
+                               Mirror mirror = Mirror()) {
   int P = 1;
   while (P < cnt) P <<= 1;
   for (int i = cnt + threadIdx.x; i < P; i += blockDim.x) sel[i] = 0;
@@ -2629,7 +2667,7 @@ __device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, f
     }
     out_s[j] = s;
     out_i[j] = id;
-    if (mirror != nullptr) st_host(mirror + j, id);
+    if (mirror.w != nullptr) mirror.put(j, id);
   }
 }
 
@@ -3000,7 +3038,7 @@ __device__ __forceinline__ bool row_last_arrival(int32_t* __restrict__ ctr, int 
 template <bool SC1 = false>
 __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int64_t id_base,
                               const uint32_t* __restrict__ brow, const uint32_t* __restrict__ srow, float* os,
-                              int32_t* oi, uint8_t* lds, int32_t* mirror = nullptr) {
+                              int32_t* oi, uint8_t* lds, Mirror mirror = Mirror()) {
   uint64_t* const sel = reinterpret_cast<uint64_t*>(lds);   // [kBmCand]
   uint32_t* const hist = reinterpret_cast<uint32_t*>(sel + kBmCand);   // [2048]
   uint32_t* const qual = hist + 2048;                              // [kBmQual]
@@ -3112,13 +3150,13 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
       if (r < k) {
         os[r] = u2f((uint32_t)(key >> 32));
         oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
-        if (mirror != nullptr) st_host(mirror + r, oi[r]);
+        if (mirror.w != nullptr) mirror.put(r, oi[r]);
       }
     }
     for (int j = m + tid; j < k; j += nth) {
       os[j] = neg_inf();
       oi[j] = -1;
-      if (mirror != nullptr) st_host(mirror + j, -1);
+      if (mirror.w != nullptr) mirror.put(j, -1);
     }
   } else {
     sort_and_write(sel, m, k, id_base, os, oi, mirror);
@@ -3130,11 +3168,11 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
                                                                int64_t bm_ld, const uint32_t* __restrict__ sb,
                                                                int64_t sb_ld, float* __restrict__ out_s,
                                                                int32_t* __restrict__ out_i,
-                                                               int32_t* __restrict__ mirror = nullptr) {
+                                                               Mirror mirror = Mirror()) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   const int row = blockIdx.x;
   topk_bmax_row(scores + (size_t)row * ld, n, k, id_base, bm + (size_t)row * bm_ld, sb + (size_t)row * sb_ld,
-                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn, mirror ? mirror + (size_t)row * k : nullptr);
+                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn, mirror.row(row, k));
 }
 
 // Block-max top-k in ONE launch (small batches, the latency path): grid (P, B)
@@ -3149,7 +3187,7 @@ __global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __re
                                                                int64_t bm_ld, uint32_t* __restrict__ sb, int64_t sb_ld,
                                                                int32_t* __restrict__ done, int64_t done_ld,
                                                                float* __restrict__ out_s, int32_t* __restrict__ out_i,
-                                                               int32_t* __restrict__ mirror) {
+                                                               Mirror mirror) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   __shared__ int s_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -3193,7 +3231,7 @@ __global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __re
   // <= 96 workgroups per row (n <= 64 * kBmMaxBlocks): one counter
   if (!row_last_arrival(done + (size_t)row * done_ld, (int)gridDim.x, 1, &s_last)) return;
   topk_bmax_row<true>(x, n, k, id_base, brow, srow, out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn,
-                      mirror ? mirror + (size_t)row * k : nullptr);
+                      mirror.row(row, k));
 }
 
 // ---------------------------------------------------------------------------
@@ -3279,20 +3317,26 @@ __device__ void select_from_lds(const float* sc, const uint64_t* keys, int C, in
   }
 }
 
+// ids_tagged (nullable): the ids as the pre-armed rerank's tagged words (all
+// present: the rerank that ran before on the stream waited for them)
 __global__ __launch_bounds__(256) void select_small_kernel(const float* __restrict__ scores,
                                                            const int32_t* __restrict__ ids, int C, int k,
                                                            float* __restrict__ out_s,
                                                            int32_t* __restrict__ out_i,
-                                                           int32_t* __restrict__ out_p) {
+                                                           int32_t* __restrict__ out_p,
+                                                           const uint64_t* __restrict__ ids_tagged = nullptr) {
   __shared__ float sc[kSmallMax];
   __shared__ uint64_t keys[kSmallMax];
+  __shared__ int32_t tid_ids[kSmallMax];
   const size_t b = blockIdx.x;
   for (int t = threadIdx.x; t < C; t += blockDim.x) {
     sc[t] = scores[b * C + t];
     keys[t] = rank_key(sc[t], (uint32_t)t);
+    if (ids_tagged != nullptr) tid_ids[t] = read_tagged(ids_tagged + b * C + t);
   }
   __syncthreads();
-  select_from_lds(sc, keys, C, k, ids ? ids + b * C : nullptr, out_s + b * k, out_i ? out_i + b * k : nullptr,
+  const int32_t* idr = ids_tagged != nullptr ? tid_ids : (ids ? ids + b * C : nullptr);
+  select_from_lds(sc, keys, C, k, idr, out_s + b * k, out_i ? out_i + b * k : nullptr,
                   out_p ? out_p + b * k : nullptr);
 }
 
@@ -3475,12 +3519,21 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_raw_kernel(
 // all 8 tiles), at one 8 KiB HBM round trip per wave instead of 32 KiB.
 __global__ __launch_bounds__(256, 2) void rerank_split_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
-    const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, float* __restrict__ raw, int ld) {
+    const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, float* __restrict__ raw, int ld,
+    TaggedCand tc = TaggedCand()) {
   __shared__ float s_m[4][32];
+  __shared__ int32_t s_cid;
   const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y, c = blockIdx.x;
-  const int32_t id = cand[(size_t)b * C + c];
+  int32_t id;
+  if (tc.w != nullptr) {   // pre-armed: the host writes the candidate after this launch
+    if (threadIdx.x == 0) s_cid = wait_tagged(tc.w + (size_t)b * C + c, tc.seq);
+    __syncthreads();
+    id = s_cid;
+  } else {
+    id = cand[(size_t)b * C + c];
+  }
   const int64_t loc = (int64_t)id - id_base;
   if (id < 0 || loc < 0 || loc >= n) {   // block-uniform
     if (threadIdx.x == 0) raw[(size_t)b * C + c] = neg_inf();
@@ -3853,7 +3906,7 @@ struct RowSelect {
   const float* lb = nullptr;     // kSelBand: a lower bound of the row's k-th score (nullable), or
   const uint32_t* lbu = nullptr; //   its order-preserving bits (the two-pass band's)
   int32_t* status = nullptr;     // kSelBand: the band size (the fallback writes -1 for overflowed rows)
-  int32_t* ids_mirror = nullptr; // kSelBand: [B][k] host mirror of the final ids (nullable; st_host)
+  Mirror ids_mirror;             // kSelBand: [B][k] host mirror of the final ids (w nullable)
 };
 constexpr int kSelNone = 0, kSelCand = 1, kSelBand = 2;
 
@@ -3878,7 +3931,7 @@ __device__ void select_cand_row(const float* raw, const int32_t* crow, int C, in
 // the keys and the kk keys at or above it are ranked.
 __device__ void select_band_row(const float* F, const int32_t* cand, int cnt, int k, int64_t id_base, bool has_lb,
                                 float lbv, float* os, int32_t* oi, uint64_t* sel, uint32_t* hist, uint32_t* misc,
-                                int32_t* mirror) {
+                                Mirror mirror) {
   const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6;
   const int kk = k < cnt ? k : cnt;
   auto key_at = [&](int i) { return rank_key(ld_sc1(F + i), (uint32_t)((int64_t)cand[i] - id_base)); };
@@ -3935,13 +3988,13 @@ __device__ void select_band_row(const float* F, const int32_t* cand, int cnt, in
     if (r < k) {
       os[r] = u2f((uint32_t)(key >> 32));
       oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
-      if (mirror != nullptr) st_host(mirror + r, oi[r]);
+      if (mirror.w != nullptr) mirror.put(r, oi[r]);
     }
   }
   for (int j = m + tid; j < k; j += nth) {
     os[j] = neg_inf();
     oi[j] = -1;
-    if (mirror != nullptr) st_host(mirror + j, -1);
+    if (mirror.w != nullptr) mirror.put(j, -1);
   }
 }
 
@@ -3952,13 +4005,15 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     const int32_t* __restrict__ cand, const int32_t* __restrict__ count, int64_t limit, int64_t ld_c,
     float* __restrict__ out, int64_t ld_out, const int32_t* __restrict__ only_neg, int ld,
     uint32_t* __restrict__ lb_min, int64_t c0, float* __restrict__ fb_T = nullptr, int32_t* __restrict__ fb_done = nullptr,
-    int fb_k = 0, float* __restrict__ fb_s = nullptr, int32_t* __restrict__ fb_i = nullptr, RowSelect rs = RowSelect()) {
+    int fb_k = 0, float* __restrict__ fb_s = nullptr, int32_t* __restrict__ fb_i = nullptr, RowSelect rs = RowSelect(),
+    TaggedCand tc = TaggedCand()) {
   __shared__ float s_m[4][32];
   __shared__ uint64_t sel[kTopkMax];   // the fallback's / the row select's
   __shared__ uint32_t hist[2048];
   __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
   __shared__ uint32_t misc[8];
   __shared__ int s_last;
+  __shared__ int32_t s_cid;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
@@ -3989,7 +4044,7 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
       const int kk = (int)((int64_t)fb_k < n ? fb_k : n);
       topk_exact_row(row, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
       sort_and_write(sel, kk, fb_k, id_base, fb_s + (size_t)b * fb_k, fb_i + (size_t)b * fb_k,
-                     rs.ids_mirror ? rs.ids_mirror + (size_t)b * fb_k : nullptr);
+                     rs.ids_mirror.row(b, fb_k));
       if (rs.mode == kSelBand && threadIdx.x == 0) rs.status[b] = -1;
       return;
     }
@@ -4001,7 +4056,15 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     load_qfrag16(qhi, b, b + 1, lq, lane, qh);
     load_qfrag16(qlo, b, b + 1, lq, lane, ql);
     for (int64_t c = c0 + blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
-      const int64_t id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
+      int64_t id;
+      if (tc.w != nullptr) {   // pre-armed (the latency path's rerank): the host writes the candidate after the launch
+        if (threadIdx.x == 0) s_cid = wait_tagged(tc.w + (size_t)b * ld_c + c, tc.seq);
+        __syncthreads();
+        id = s_cid;
+        __syncthreads();   // s_cid is rewritten by the next pair
+      } else {
+        id = cand ? (int64_t)cand[b * ld_c + c] : id_base + c;
+      }
       const int64_t loc = id - id_base;
       float v = neg_inf();
       if (id >= 0 && loc >= 0 && loc < n)                      // block-uniform
@@ -4018,7 +4081,13 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
   if (rs.mode == kSelNone) return;
   if (!row_last_arrival(rs.arrive + (size_t)b * kArriveInts, (int)gridDim.x, 8, &s_last)) return;
   if (rs.mode == kSelCand) {   // C = limit candidates, ids = the row's cand
-    select_cand_row(out + (size_t)b * ld_out, cand + (size_t)b * ld_c, (int)limit, rs.k, rs.out_s + (size_t)b * rs.k,
+    const int32_t* crow = cand + (size_t)b * ld_c;
+    if (tc.w != nullptr) {       // the tagged words, all present (every workgroup of the row waited for its own)
+      int32_t* ids_lds = reinterpret_cast<int32_t*>(hist) + kSmallMax;
+      for (int t = threadIdx.x; t < (int)limit; t += blockDim.x) ids_lds[t] = read_tagged(tc.w + (size_t)b * ld_c + t);
+      crow = ids_lds;            // (published by select_cand_row's barrier)
+    }
+    select_cand_row(out + (size_t)b * ld_out, crow, (int)limit, rs.k, rs.out_s + (size_t)b * rs.k,
                     rs.out_i + (size_t)b * rs.k, rs.out_p ? rs.out_p + (size_t)b * rs.k : nullptr,
                     reinterpret_cast<float*>(hist), sel);
   } else {                     // the band: lim keys (count[b] <= limit here)
@@ -4026,7 +4095,7 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     const float lbv = rs.lbu != nullptr ? u2f(rs.lbu[b]) : (rs.lb != nullptr ? rs.lb[b] : 0.0f);
     select_band_row(out + (size_t)b * ld_out, cand + (size_t)b * ld_c, (int)lim, rs.k, id_base, has_lb, lbv,
                     rs.out_s + (size_t)b * rs.k, rs.out_i + (size_t)b * rs.k, sel, hist, misc,
-                    rs.ids_mirror ? rs.ids_mirror + (size_t)b * rs.k : nullptr);
+                    rs.ids_mirror.row(b, rs.k));
     if (threadIdx.x == 0) rs.status[b] = (int32_t)lim;
   }
 }
@@ -5152,8 +5221,12 @@ constexpr int kCtrDefault = 0, kCtrPrezeroed = 1, kCtrZeroAll = 2;
 // sets it around its search, retrieve.cpp): the launches that write every
 // row's final ids also write them to this device-mapped host buffer and set
 // g_ids_mirror_used, so finish needs no D2H copy.
-thread_local int32_t* g_ids_mirror = nullptr;
+thread_local Mirror g_ids_mirror;
 thread_local bool g_ids_mirror_used = false;
+// ... and its pre-armed rerank's candidates (cbv2_retrieve_finish sets them
+// around its rerank call): a rerank that can take them sets g_cand_tagged_used.
+thread_local TaggedCand g_cand_tagged;
+thread_local bool g_cand_tagged_used = false;
 thread_local int g_ctr_policy = kCtrDefault;
 thread_local bool g_ctr_zeroed = false;
 struct CtrPolicy {
@@ -5733,8 +5806,8 @@ constexpr int kBmDoneOff = kRingInts - kBmFusedMaxB;   // cbv2_search's arrival 
 int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, int64_t id_base, uint32_t* bm,
               float* out_s, int32_t* out_i, hipStream_t st, int dev, bool blocks_ready = false,
               int32_t* done = nullptr, int64_t done_ld = 1) {
-  int32_t* mirror = g_ids_mirror;
-  if (mirror != nullptr) g_ids_mirror_used = true;   // every row's ids written to it below
+  const Mirror mirror = g_ids_mirror;
+  if (mirror.w != nullptr) g_ids_mirror_used = true;   // every row's ids written to it below
   static std::atomic<bool> attr_set[64] = {};
   if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
     const int lds_max = (int)(kBmFixedLds + (size_t)(kBmMaxBlocks / 4) * 4);
@@ -6052,7 +6125,7 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
                    int64_t limit, int64_t ld_c, float* out, int64_t ld_out, hipStream_t st,
                    const int32_t* only_neg = nullptr, int pw = 0, uint32_t* lb_min = nullptr, int64_t c0 = 0,
                    float* fb_T = nullptr, int32_t* fb_done = nullptr, int fb_k = 0, float* fb_s = nullptr,
-                   int32_t* fb_i = nullptr, const RowSelect& rs = RowSelect()) {
+                   int32_t* fb_i = nullptr, const RowSelect& rs = RowSelect(), TaggedCand tc = TaggedCand()) {
   if (limit <= c0 && fb_T == nullptr && rs.mode == kSelNone) return CBV2_OK;
   if (ix->rescore_split) {   // one pair per workgroup (its doc split over 4 waves, or 2 for launches past
                              // the chip's resident 4-wave workgroups: one round of 2-wave ones instead of two)
@@ -6071,10 +6144,10 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
                               : (two ? rescore_split_kernel<false, 2> : rescore_split_kernel<false, 4>);
     hipLaunchKernelGGL(kern, dim3(gx, (unsigned)B), dim3(two ? 128 : 256), 0, st, ix->tokens, ix->resid, ix->doclens,
                        ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out, only_neg,
-                       (int)ix->ld, lb_min, c0, fb_T, fb_done, fb_k, fb_s, fb_i, rs);
+                       (int)ix->ld, lb_min, c0, fb_T, fb_done, fb_k, fb_s, fb_i, rs, tc);
     return launch_check("rescore_split_kernel");
   }
-  if (c0 != 0 || fb_T != nullptr || rs.mode != kSelNone)
+  if (c0 != 0 || fb_T != nullptr || rs.mode != kSelNone || tc.w != nullptr)
     return fail(CBV2_EUNSUPPORTED, "pair offset / fallback / row select need the split rescoring");
   if (pw <= 0) pw = (int64_t)B * limit <= kRsSmallPairs ? 1 : kRsPerWave;
   const int64_t per_wg = 4LL * pw;
@@ -6441,9 +6514,12 @@ static int rerank_impl(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, con
   if (B <= kRrSplitMaxB && (k == 0 || (!big && ws != nullptr && ws_bytes >= raw_bytes))) {
     float* raw = k == 0 ? out_scores : (float*)ws;
     const dim3 grid((unsigned)((C + kRrWaves - 1) / kRrWaves), (unsigned)B);
+    TaggedCand tc;
     if (!f8 && ix->rescore_split) {   // one candidate per workgroup, its rows over the 4 waves
+      tc = g_cand_tagged;             // the latency path's pre-armed rerank (cand unused then)
+      if (tc.w != nullptr) g_cand_tagged_used = true;
       hipLaunchKernelGGL(rerank_split_kernel, dim3((unsigned)C, (unsigned)B), dim3(256), 0, st, ix->tokens,
-                         ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, raw, (int)ix->ld);
+                         ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, raw, (int)ix->ld, tc);
       if ((rc = launch_check("rerank_split_kernel"))) return rc;
     } else if (f8)
       hipLaunchKernelGGL(rerank_raw_kernel<true>, grid, dim3(kRrWaves * 64), 0, st, ix->tokens, ix->scales,
@@ -6454,7 +6530,7 @@ static int rerank_impl(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, con
     if ((rc = launch_check("rerank_raw_kernel"))) return rc;
     if (k == 0) return CBV2_OK;
     hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
-                       out_pos);
+                       out_pos, tc.w);
     return launch_check("select_small_kernel");
   }
   if (f8) {
@@ -6598,8 +6674,8 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr, nullptr, fold ? (uint32_t*)w.tk : nullptr)))
       return rc;
   }
-  int32_t* const mirror = g_ids_mirror;   // the bf16 top-k is not the search's answer: no host mirror here
-  g_ids_mirror = nullptr;
+  const Mirror mirror = g_ids_mirror;   // the bf16 top-k is not the search's answer: no host mirror here
+  g_ids_mirror = Mirror();
   rc = bmax ? topk_bmax(w.T, B, ix->n, ix->n, k, ix->id_base, (uint32_t*)w.tk, out_scores, out_ids, st, ix->device,
                         fold, arrive_row0(w, kArrBmax, B), kArriveInts)
             : topk_impl(w.T, B, ix->n, ix->n, k, ix->id_base, w.tk, w.tk_bytes, out_scores, out_ids, st, ix->device);
@@ -6703,7 +6779,7 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
       rs.lbu = lbu;
       rs.status = out_status;
       rs.ids_mirror = g_ids_mirror;
-      if (g_ids_mirror != nullptr) g_ids_mirror_used = true;   // selected or fallen back, every row writes it
+      if (g_ids_mirror.w != nullptr) g_ids_mirror_used = true;   // selected or fallen back, every row writes it
     }
     if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
                              B <= kBandPairMaxB ? 1 : 0, nullptr, c0, fb_fused ? w.T : nullptr,
@@ -6761,8 +6837,10 @@ int rerank_f32_split(cbv2_index* ix, F32Ws& w, int32_t B, int32_t lq, const int3
     rs.out_s = out_scores;
     rs.out_i = out_ids;
     rs.out_p = out_pos;
+    const TaggedCand tc = g_cand_tagged;   // the latency path's pre-armed rerank (cand unused then)
+    if (tc.w != nullptr) g_cand_tagged_used = true;
     return launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
-                          nullptr, nullptr, rs);
+                          nullptr, nullptr, rs, tc);
   }
   if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
   if (k == 0) return CBV2_OK;
@@ -6898,11 +6976,16 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
 // Internal (retrieve.cpp): the host mirror of the next search's final ids on
 // this thread (nullptr: none); cbv2_ids_mirror_used: whether the search just
 // issued writes it (then it holds every row's ids once the stream gets there).
-void cbv2_set_ids_mirror(int32_t* p) {
-  g_ids_mirror = p;
+void cbv2_set_ids_mirror(void* p, uint32_t seq) {
+  g_ids_mirror = Mirror{(uint64_t*)p, seq};
   g_ids_mirror_used = false;
 }
 int cbv2_ids_mirror_used(void) { return g_ids_mirror_used ? 1 : 0; }
+void cbv2_set_cand_tagged(const void* p, uint32_t seq) {
+  g_cand_tagged = TaggedCand{(const uint64_t*)p, seq};
+  g_cand_tagged_used = false;
+}
+int cbv2_cand_tagged_used(void) { return g_cand_tagged_used ? 1 : 0; }
 
 // Internal (retrieve.cpp): the device an index lives on (-1: null index).
 int cbv2_index_device(const cbv2_index* ix) { return ix ? ix->device : -1; }

@@ -32,8 +32,10 @@ extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_w
                                             size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
                                             const float* Q, void* stream);
 extern "C" int cbv2_index_device(const cbv2_index* ix);
-extern "C" void cbv2_set_ids_mirror(int32_t* p);
+extern "C" void cbv2_set_ids_mirror(void* p, uint32_t seq);
 extern "C" int cbv2_ids_mirror_used(void);
+extern "C" void cbv2_set_cand_tagged(const void* p, uint32_t seq);
+extern "C" int cbv2_cand_tagged_used(void);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -125,6 +127,7 @@ struct MappedBuf {
   size_t bytes = 0;
   hipEvent_t ev = nullptr;
   bool recorded = false;
+  uint32_t seq = 0;   // the tag of this buffer's last call (words of older calls carry older tags)
 };
 struct MappedPool {
   std::mutex mu;
@@ -155,6 +158,7 @@ bool take_mapped(int dev, size_t bytes, MappedBuf* out) {
   b.bytes = std::max<size_t>(bytes, 64 * 1024);
   if (hipHostMalloc(&b.h, b.bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
     return false;
+  std::memset(b.h, 0, b.bytes);   // tag 0 is never a call's
   if (hipHostGetDevicePointer(&b.d, b.h, 0) != hipSuccess ||
       hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess) {
     (void)hipHostFree(b.h);
@@ -182,6 +186,7 @@ void give_mapped(int dev, MappedBuf b, hipStream_t st) {
 struct Pending {
   MappedBuf mb;
   bool ids_mirrored = false;
+  uint32_t seq = 0;
 };
 std::mutex g_pending_mu;
 std::vector<std::pair<const void*, Pending>> g_pending;
@@ -308,6 +313,42 @@ HostLayout host_layout(void* h, int32_t B, int32_t k, int32_t kb, int32_t C) {
   return H;
 }
 
+// Stage 3 of one call: the sharded rerank (all-reduce MAX), the faithful
+// rerank on begin's query split, or the bf16 / MXFP8 one.
+int rerank_call(cbv2_index* ix, cbv2_comm* c, Kind kd, const void* Q, int32_t B, int32_t lq, int32_t k,
+                const Layout& L, const int32_t* cand, int32_t C, int32_t final_k, float* out_scores,
+                int32_t* out_ids, int32_t* out_pos, hipStream_t st) {
+  if (c)
+    return cbv2_rerank_sharded(ix, c, Q, B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+  if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank when it is still there
+    return cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
+                                        B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos,
+                                        (const float*)Q, st);
+  return cbv2_rerank_ws(ix, Q, B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+}
+
+// Lab knob (cbv2_set_prearm, internal): 0 = the rerank is launched after the
+// fusion (no tagged candidates), 1 = pre-armed (default).
+int g_prearm = 1;
+
+// Polls the call's tagged stage-2 id words until every one carries seq (the
+// search's last kernel writes them; written whole, in any order).  Never
+// waits forever: a GPU that never writes them (a fault) fails the call after
+// 2 s.
+int wait_words(const uint64_t* w, size_t n, uint32_t seq) {
+  const volatile uint64_t* vw = w;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t i = 0; i < n;) {
+    if ((uint32_t)(vw[i] >> 32) == seq) {
+      ++i;
+      continue;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+      return err(CBV2_EHIP, "stage-2 results did not arrive (2 s)");
+  }
+  return CBV2_OK;
+}
+
 int check_common(const cbv2_index* ix, Kind* kd, const cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B,
                  int32_t lq, int32_t k, int32_t kb) {
   if (!ix) return err(CBV2_EINVAL, "null index");
@@ -337,6 +378,7 @@ int cbv2_retrieve_host_marks(int64_t* out, int32_t max) {
 }
 
 void cbv2_set_wait_mode(int32_t mode) { g_wait_mode = mode; }
+void cbv2_set_prearm(int32_t on) { g_prearm = on; }
 
 int cbv2_retrieve_cancel(cbv2_index* ix, void* workspace, void* stream) {
   if (!ix) return err(CBV2_EINVAL, "null index");
@@ -382,8 +424,12 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   // mirrors the ids into it (no D2H copy in finish) and the fusion writes the
   // candidates the rerank reads from it
   Pending pd;
-  const bool mapped = ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, (size_t)B * (k + C) * 4, &pd.mb);
-  cbv2_set_ids_mirror(mapped ? (int32_t*)pd.mb.d : nullptr);
+  const bool mapped = ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, (size_t)B * (k + C) * 8, &pd.mb);
+  if (mapped) {
+    pd.seq = ++pd.mb.seq;
+    if (pd.seq == 0) pd.seq = ++pd.mb.seq;
+  }
+  cbv2_set_ids_mirror(mapped ? pd.mb.d : nullptr, pd.seq);
   int rc;
   if (kd.faithful)
     rc = cbv2_search_f32(ix, (const float*)Q, B, lq, k, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
@@ -391,7 +437,7 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   else
     rc = cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
   pd.ids_mirrored = mapped && cbv2_ids_mirror_used() != 0;
-  cbv2_set_ids_mirror(nullptr);
+  cbv2_set_ids_mirror(nullptr, 0);
   if (mapped) {
     if (rc == CBV2_OK)
       put_pending(workspace, pd, ds.dev, (hipStream_t)stream);
@@ -443,28 +489,58 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
   // collectives read device memory)
   Pending pd;
   const bool mapped = !c && take_pending(workspace, &pd);
-  const int32_t* ids_h = mapped && pd.ids_mirrored ? (const int32_t*)pd.mb.h : H.ids;
+  // the call's tagged words in the mapped buffer: [B][k] stage-2 ids (the
+  // search's select wrote them, ids_mirrored) | [B][C] fused candidates
+  uint64_t* const idw = mapped ? (uint64_t*)pd.mb.h : nullptr;
+  uint64_t* const cw = mapped ? idw + (size_t)B * k : nullptr;
+  const uint64_t* const cwd = mapped ? (const uint64_t*)pd.mb.d + (size_t)B * k : nullptr;
+  const bool mirrored = mapped && pd.ids_mirrored;
+  // small batches pre-arm the rerank: it is launched now, before the wait,
+  // and polls its candidates' words (the host writes them after the fusion),
+  // so the host -> GPU hop after the fusion is a PCIe read, not a launch
+  const bool prearm = mirrored && g_prearm && B <= kSpinMaxB && (kd.faithful || kd.dtype == CBV2_DTYPE_BF16);
   rc = CBV2_OK;
-  if (ids_h == H.ids && hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+  if (!mirrored && hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
     rc = err(CBV2_EHIP, "stage-2 ids copy failed");
   mark(1);
-  int32_t* cand_h = mapped ? (int32_t*)pd.mb.h + (size_t)B * k : H.cand;
-  const int32_t* cand_d = mapped ? (const int32_t*)pd.mb.d + (size_t)B * k : L.cand;
-  if (!rc) rc = wait_copy(st, B);   // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  bool armed = false;
+  if (!rc && prearm) {
+    cbv2_set_cand_tagged(cwd, pd.seq);
+    rc = rerank_call(ix, c, kd, Q, B, lq, k, L, L.cand, C, final_k, out_scores, out_ids, out_pos, st);
+    armed = cbv2_cand_tagged_used() != 0;   // else it read L.cand (any ids are range-checked): rerun below
+    cbv2_set_cand_tagged(nullptr, 0);
+  }
+  // the one host round trip: the ColBERT (and merged BM25) top-k are here
+  if (!rc) rc = mirrored && B <= kSpinMaxB ? wait_words(idw, (size_t)B * k, pd.seq) : wait_copy(st, B);
   mark(2);
+  thread_local std::vector<int32_t> ids_s, cand_s;
+  const int32_t* ids_h = H.ids;
+  if (mirrored && !rc) {   // the ids out of their words (complete: polled, or the stream has run)
+    ids_s.resize((size_t)B * k);
+    for (size_t i = 0; i < ids_s.size(); ++i) ids_s[i] = (int32_t)(uint32_t)idw[i];
+    ids_h = ids_s.data();
+  }
+  int32_t* cand_h = H.cand;
+  if (mapped) {
+    cand_s.resize((size_t)B * C);
+    cand_h = cand_s.data();
+  }
   if (!rc) rc = cbv2_rrf_fuse(bm, kb, ids_h, k, B, rrf_k, C, cand_h, nullptr, nullptr);
   mark(3);
-  if (!rc && !mapped && hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st) != hipSuccess)
-    rc = err(CBV2_EHIP, "candidate upload failed");
-  if (!rc) {
-    if (c)
-      rc = cbv2_rerank_sharded(ix, c, Q, B, lq, L.cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
-    else if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank when it is still there
-      rc = cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
-                                        B, lq, cand_d, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos,
-                                        (const float*)Q, st);
-    else
-      rc = cbv2_rerank_ws(ix, Q, B, lq, cand_d, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+  if (armed) {   // always publish, failed or not: the armed rerank must not wait for its timeout
+    const uint64_t tag = (uint64_t)pd.seq << 32;
+    volatile uint64_t* vw = cw;
+    for (size_t i = 0; i < (size_t)B * C; ++i) vw[i] = tag | (uint32_t)(rc ? -1 : cand_h[i]);
+  } else if (!rc) {
+    const int32_t* cand_d = L.cand;
+    if (mapped) {   // plain ids in the buffer's candidate words, read in place by the rerank
+      int32_t* ci = (int32_t*)cw;
+      std::memcpy(ci, cand_h, (size_t)B * C * 4);
+      cand_d = (const int32_t*)cwd;
+    } else if (hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+      rc = err(CBV2_EHIP, "candidate upload failed");
+    }
+    if (!rc) rc = rerank_call(ix, c, kd, Q, B, lq, k, L, cand_d, C, final_k, out_scores, out_ids, out_pos, st);
   }
   mark(4);
   if (mapped) give_mapped(ds.dev, pd.mb, st);   // free again once the rerank that reads it ran
