@@ -29,6 +29,7 @@ from . import _lib
 from .bm25 import HostBM25, Stemmer, tokenize
 from .config import RAGConfig
 from .index import LQ_MAX as _LQ_MAX
+from .index import _raw_stream
 from .index import _stream_ptr as _stream_ptr_fn
 from .retriever import JinaColBERTRetriever
 
@@ -434,7 +435,7 @@ class OneTripRetriever:
             _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
         kb_cap = self.lexical_k if callable(lexical) else (0 if lexical is None else int(np.shape(lexical)[1]))
         ws, wsb = self._buffers(B, lq, kb_cap)
-        st = _stream_ptr_fn(self.device)
+        st = _raw_stream(self._dev_index) if _raw_stream is not None else _stream_ptr_fn(self.device)
         t_prep = time.monotonic_ns() if self.record_marks else 0
         _lib.check(L.cbv2_retrieve_begin(self.index._h, self.comm, qptr, qdt, B, lq, self.k, kb_cap, self.C,
                                          ws, wsb, st))

@@ -34,7 +34,14 @@ LQ_MAX = 32
 BAND_CAP = 16384   # fp32-faithful search: largest band rescored per query
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream_ptr(device: torch.device) -> int:
+    """The device's current stream as a raw hipStream_t (torch's C accessor:
+    no Stream object per call -- the latency path pays for every microsecond)."""
+    if _raw_stream is not None:
+        return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
 
 
