@@ -688,6 +688,8 @@ def main():
         latency_path = ("one host round trip over the native exchange (cbv2_retrieve_begin/_finish, "
                         "RCCL collectives inside the C ABI)")
     p50, p99 = mine["p50_ms_b1"], mine["p99_ms_b1"]
+    if world > 1 and mine["exchange"] is None:   # no native leg (gloo): the torch.distributed exchange
+        mine["exchange"] = "torch.distributed"
 
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     if rank == 0:
