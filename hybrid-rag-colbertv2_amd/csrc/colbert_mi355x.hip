@@ -2457,6 +2457,25 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_f8_stream_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kTkThreads = 1024;
 
+// Max / min over the 64 lanes, wave-uniform: 16-lane rows by DPP, then the
+// four rows' lane 0.  Full EXEC.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+  return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+  return min(min((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             min((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+
 // Wave 0 finds bin b with count(bins > b) < kleft <= count(bins >= b).
 __device__ void find_bin(const uint32_t* hist, int nb, uint32_t kleft, uint32_t* s_bin,
                          uint32_t* s_above, uint32_t* s_bincount) {
@@ -2484,6 +2503,49 @@ __device__ void find_bin(const uint32_t* hist, int nb, uint32_t kleft, uint32_t*
       }
       cum += c;
     }
+  }
+}
+
+// find_bin for 1024 bins (16 per lane): each lane's bins in registers (four
+// 16-B LDS reads, hist 16-B aligned), the suffix sums across lanes, then the
+// owning lane's own registers -- no dependent LDS reads.
+__device__ void find_bin1024(const uint32_t* hist, uint32_t kleft, uint32_t* s_bin, uint32_t* s_above,
+                             uint32_t* s_bincount) {
+  const int lane = threadIdx.x & 63;
+  uint32_t h[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 v = reinterpret_cast<const uint4*>(hist + lane * 16)[q];
+    h[4 * q] = v.x, h[4 * q + 1] = v.y, h[4 * q + 2] = v.z, h[4 * q + 3] = v.w;
+  }
+  uint32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) tot += h[j];
+  uint32_t incl = tot;  // inclusive suffix sum over lanes >= lane
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_down(incl, off);
+    if (lane + off < 64) incl += t;
+  }
+  const uint32_t above = incl - tot;
+  if (above < kleft && kleft <= incl) {
+    uint32_t cum = above;
+    int bin = 0;
+    uint32_t cnt = 0, abv = 0;
+    bool found = false;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+      if (!found && cum + h[j] >= kleft) {
+        found = true;
+        bin = lane * 16 + j;
+        abv = cum;
+        cnt = h[j];
+      }
+      cum += h[j];
+    }
+    *s_bin = (uint32_t)bin;
+    *s_above = abv;
+    *s_bincount = cnt;
   }
 }
 
@@ -2635,6 +2697,24 @@ struct Mirror {
 struct TaggedCand {
   const uint64_t* w = nullptr;
   uint32_t seq = 0;
+};
+
+// The FINAL top-k of a retrieve call, also written to host memory by the
+// select that produces it (the latency path's device-mapped buffer, tagged
+// words as Mirror's): per row [k] score words, [k] id words, [k] position
+// words, {value bits, seq}.  The host polls them and has its results as soon
+// as the select stored them -- no D2H copy, no stream wait.
+struct FinalMirror {
+  uint64_t* w = nullptr;
+  uint32_t seq = 0;
+  int k = 0;
+  __device__ __forceinline__ void put(size_t b, int r, float s, int32_t id, int32_t pos) const {
+    uint64_t* row = w + b * 3 * (size_t)k;
+    const uint64_t t = (uint64_t)seq << 32;
+    __hip_atomic_store(row + r, t | __float_as_uint(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(row + k + r, t | (uint32_t)id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(row + 2 * k + r, t | (uint32_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 };
 constexpr uint64_t kCandWaitTicks = 100000000ull;   // 1 s
 __device__ __forceinline__ int32_t wait_tagged(const uint64_t* w, uint32_t seq) {
@@ -2914,9 +2994,23 @@ constexpr int kBmCand = 4096;          // gathered ranking keys (32 KiB)
 constexpr int kBmQual = 2048;          // qualifying blocks
 constexpr int kBmMaxBlocks = 24576;    // rows of n <= 1,572,864 (superblock keys in LDS: 24 KiB)
 constexpr int kBmRankMax = 512;        // gathered keys ranked by counting (else bitonic)
+constexpr int kBmBins = 1024;          // threshold bins (find_bin1024); qualifying superblocks listed in hist
+static_assert(kBmRankMax <= 1024, "the counting rank takes one key per thread at most (1024-thread selects)");
 constexpr size_t kBmFixedLds = kBmCand * 8 + 2048 * 4 + kBmQual * 4 + 64;
-inline int64_t bm_blocks(int64_t n) { return (n + 63) >> 6; }   // 64-doc blocks of a row
-inline int64_t bm_supers(int64_t n) { return (n + 255) >> 8; }  // 256-doc superblocks (4 blocks) of a row
+__host__ __device__ inline int64_t bm_blocks(int64_t n) { return (n + 63) >> 6; }   // 64-doc blocks of a row
+__host__ __device__ inline int64_t bm_supers(int64_t n) { return (n + 255) >> 8; }  // 256-doc superblocks of a row
+// kk large against the superblock count (kk * 8 > ns: rows of 65k-262k docs
+// with k up to 1,024): the kk-th superblock key would sit near the row's
+// bottom and qualify nearly every doc (then the full-row fallback), so the
+// select's threshold comes from the 64-doc block keys instead
+__host__ __device__ inline bool bm_by_block(int64_t n, int k) {
+  const int64_t kk = (int64_t)k < n ? k : n;
+  return kk * 8 > bm_supers(n);
+}
+// dynamic LDS of a row select: the fixed part + its threshold keys
+inline size_t bm_select_lds(int64_t n, int k) {
+  return kBmFixedLds + (size_t)(bm_by_block(n, k) ? bm_blocks(n) : bm_supers(n)) * 4;
+}
 // Workspace of the block-max top-k: block keys [B][nb], then superblock keys [B][ns].
 inline uint32_t* bm_super_keys(uint32_t* bm, int32_t B, int64_t n) { return bm + (size_t)B * bm_blocks(n); }
 
@@ -3031,14 +3125,22 @@ __device__ __forceinline__ bool row_last_arrival(int32_t* __restrict__ ctr, int 
 }
 
 // The select of one row (topk_bmax_kernel's work; run by a whole workgroup):
-// bm / sb = the row's block and superblock keys, lds = kBmFixedLds + ns * 4
+// bm / sb = the row's block and superblock keys, lds = bm_select_lds(n, k)
 // bytes of LDS.
 // SC1: bm / sb were stored in this launch (bmax_topk_kernel): read them with
 // sc1 loads (the write-through hand-off, row_last_arrival).
+// stamps (lab only, nullable): s_memrealtime at the phase ends -- [0] keys in
+// LDS, [1] threshold, [2] qualifying blocks, [3] gather, [4] ranked + written;
+// inside the threshold: [7] key range, [8] histogram, [9] bin found
+constexpr int kLabWgs = 4096;                          // workgroups with start / end stamps
+[[maybe_unused]] constexpr size_t kLabStride = 16 + 2 * (size_t)kLabWgs;   // u64 per stamped launch kind
+__device__ __forceinline__ void lab_stamp(uint64_t* stamps, int i) {
+  if (stamps != nullptr && threadIdx.x == 0) stamps[i] = __builtin_amdgcn_s_memrealtime();
+}
 template <bool SC1 = false>
 __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int64_t id_base,
                               const uint32_t* __restrict__ brow, const uint32_t* __restrict__ srow, float* os,
-                              int32_t* oi, uint8_t* lds, Mirror mirror = Mirror()) {
+                              int32_t* oi, uint8_t* lds, Mirror mirror = Mirror(), uint64_t* stamps = nullptr) {
   uint64_t* const sel = reinterpret_cast<uint64_t*>(lds);   // [kBmCand]
   uint32_t* const hist = reinterpret_cast<uint32_t*>(sel + kBmCand);   // [2048]
   uint32_t* const qual = hist + 2048;                              // [kBmQual]
@@ -3048,93 +3150,127 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
   const int nb = (int)((n + 63) >> 6);
   const int ns = (int)((n + 255) >> 8);
   const int kk = (int)((int64_t)k < n ? k : n);
-  // kk large against the superblock count (kk * 8 > ns: rows of 65k-262k docs
-  // with k up to 1,024): the kk-th superblock key would sit near the row's
-  // bottom and qualify nearly every doc (then the full-row fallback), so the
-  // threshold comes from the 64-doc block keys instead (read in place: up to
-  // 4 ns of them)
-  const bool by_block = (int64_t)kk * 8 > ns;
-  for (int i = tid; i < ns; i += nth) keys[i] = SC1 ? ld_sc1(srow + i) : srow[i];
-  if (tid < 16) misc[tid] = 0;
-  __syncthreads();
-  // 1. t = the kk-th largest SUPERBLOCK key (or block key), to its top 22
-  //    bits (two 11-bit digits): kk superblocks (blocks) have a max >= t, so
-  //    the kk-th largest score is >= t, and every doc >= t lies in a 64-doc
-  //    block whose key is >= t
+  // (bm_by_block: the threshold over the 64-doc block keys)
+  const bool by_block = bm_by_block(n, k);
   const int nk = by_block ? nb : ns;
-  uint32_t prefix = 0, mask = 0, kleft = (uint32_t)(kk < nk ? kk : nk);
-  // rows of at most one superblock key per thread (n <= 262,144 at 1,024
-  // threads: the shards of a multi-GPU node): the kk-th largest key EXACTLY,
-  // by counting -- key u is it when fewer than kk keys exceed it and at least
-  // kk reach it -- one pass over the keys in LDS (broadcast reads) instead of
-  // two radix passes and their six barriers; an exact t is never looser than
-  // the rounded one, and the select below does not depend on which is used
-  const bool by_count = !by_block && ns <= nth;
-  if (by_count) {
-    if (tid < ns) {
-      const uint32_t u = keys[tid];
-      uint32_t gt = 0, ge = 0;
-      for (int j = 0; j < ns; ++j) {
-        const uint32_t v = keys[j];
-        gt += v > u ? 1u : 0u;
-        ge += v >= u ? 1u : 0u;
-      }
-      if (gt < kleft && kleft <= ge) misc[4] = u;   // every such thread writes the same key
-    }
-    __syncthreads();
-    prefix = misc[4];
-    __syncthreads();
-    if (tid == 4) misc[4] = 0;
-    __syncthreads();
+  const uint32_t kleft = (uint32_t)(kk < nk ? kk : nk);
+  // the threshold's keys into LDS (superblock keys, or the block keys when
+  // by_block: lds = bm_select_lds), with this thread's range of them
+  uint32_t mx = 0u, mn = ~0u;
+  for (int i = tid; i < nk; i += nth) {
+    const uint32_t u = by_block ? (SC1 ? ld_sc1(brow + i) : brow[i]) : (SC1 ? ld_sc1(srow + i) : srow[i]);
+    keys[i] = u;
+    mx = max(mx, u);
+    mn = min(mn, u);
   }
-  for (int p = 0; p < (by_count ? 0 : 2); ++p) {
-    const int shift = 21 - 11 * p;
-    for (int b = tid; b < 2048; b += nth) hist[b] = 0;
-    __syncthreads();
+  for (int b = tid; b < kBmBins; b += nth) hist[b] = 0;
+  if (tid < 16) misc[tid] = (tid == 9 || tid == 10) ? ~0u : 0u;   // [8] max, [9] min, [10] t
+  mx = wave_max_u32(mx);
+  mn = wave_min_u32(mn);
+  __syncthreads();   // misc zeroed before the atomics below
+  if ((tid & 63) == 0) {
+    atomicMax(&misc[8], mx);
+    atomicMin(&misc[9], mn);
+  }
+  __syncthreads();
+  lab_stamp(stamps, 0);
+  // 1. t = a key that at least kleft = min(kk, keys) of the keys reach:
+  //    kleft superblocks (blocks) have a max >= t, so the kk-th largest score
+  //    is >= t, and every doc >= t lies in a 64-doc block whose key is >= t.
+  //    Any such t is correct -- the kleft-th largest key itself or one below
+  //    it (a lower t only gathers more candidates) -- so no exact selection:
+  //    the keys' range [lo, hi] in kBmBins linear bins, the bin at which the
+  //    count from the top reaches kleft (find_bin), t = the smallest key of
+  //    that bin and the bins above it.  Keys in LDS, one histogram pass, one
+  //    minimum pass.  (Lab, B=1 at 125k docs: 7.2 us for two exact radix
+  //    passes over the block keys in L2; 24 us for one wave bisecting them.)
+  const uint32_t khi = misc[8];
+  const uint64_t span = (uint64_t)(khi - misc[9]) + 1;
+  // larger key -> higher bin (find_bin counts from the top bin down)
+  auto bin_of = [&](uint32_t u) { return (uint32_t)(kBmBins - 1) - (uint32_t)(((uint64_t)(khi - u) * kBmBins) / span); };
+  for (int i = tid; i < nk; i += nth) atomicAdd(&hist[bin_of(keys[i])], 1u);   // linear bins: few collisions
+  __syncthreads();
+  if (wave == 0) find_bin1024(hist, kleft, &misc[4], &misc[5], &misc[6]);
+  __syncthreads();
+  {
+    const uint32_t bstar = misc[4];
+    uint32_t tm = ~0u;
     for (int i = tid; i < nk; i += nth) {
-      const uint32_t u = by_block ? (SC1 ? ld_sc1(brow + i) : brow[i]) : keys[i];
-      hist_add(hist, (u >> shift) & 2047u, (u & mask) == prefix);
+      const uint32_t u = keys[i];
+      if (bin_of(u) >= bstar) tm = min(tm, u);
     }
-    __syncthreads();
-    if (wave == 0) find_bin(hist, 2048, kleft, &misc[4], &misc[5], &misc[6]);
-    __syncthreads();
-    kleft -= misc[5];
-    prefix |= misc[4] << shift;
-    mask |= 2047u << shift;
-    __syncthreads();
+    tm = wave_min_u32(tm);
+    if ((tid & 63) == 0) atomicMin(&misc[10], tm);
   }
-  const uint32_t t = prefix;
-  // 2. the 64-doc blocks (of the superblocks >= t) whose max reaches t, then their docs >= t
-  for (int i = tid; i < 4 * ns; i += nth) {
-    const int sbk = i >> 2, j = i;
-    if (j < nb && keys[sbk] >= t && (SC1 ? ld_sc1(brow + j) : brow[j]) >= t) {
-      const uint32_t pos = atomicAdd(&misc[0], 1u);
-      if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)j;
+  __syncthreads();
+  const uint32_t t = misc[10];
+  lab_stamp(stamps, 1);
+  // 2. the 64-doc blocks whose max reaches t: by superblock, the superblocks
+  //    >= t first (their keys in LDS; listed in hist, free again), then the
+  //    <= 4 block keys of each, all loads in flight at once (not a pass over
+  //    every block key: ~4 dependent load rounds per thread at 1M docs)
+  if (by_block) {
+    for (int j = tid; j < nb; j += nth)
+      if (keys[j] >= t) {
+        const uint32_t pos = atomicAdd(&misc[0], 1u);
+        if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)j;
+      }
+  } else {
+    for (int i = tid; i < ns; i += nth)
+      if (keys[i] >= t) {
+        const uint32_t pos = atomicAdd(&misc[2], 1u);
+        if (pos < (uint32_t)kBmBins) hist[pos] = (uint32_t)i;
+      }
+    __syncthreads();
+    const uint32_t nsq = misc[2];
+    if (nsq > (uint32_t)kBmBins) {
+      if (tid == 0) misc[0] = (uint32_t)kBmQual + 1;   // too many: the exact fallback below
+    } else {
+      for (uint32_t w = tid; w < 4 * nsq; w += (uint32_t)nth) {
+        const int j = 4 * (int)hist[w >> 2] + (int)(w & 3);
+        if (j < nb && (SC1 ? ld_sc1(brow + j) : brow[j]) >= t) {
+          const uint32_t pos = atomicAdd(&misc[0], 1u);
+          if (pos < (uint32_t)kBmQual) qual[pos] = (uint32_t)j;
+        }
+      }
     }
   }
   __syncthreads();
+  lab_stamp(stamps, 2);
   const uint32_t nqual = misc[0];
   if (nqual <= (uint32_t)kBmQual) {
-    constexpr int U = 4;   // one score per thread per block row, U loads in flight
-    const uint32_t total = nqual * 64;
+    // 4 scores per thread per step (a float4 when the row is 16-B aligned),
+    // U steps of loads in flight: a 64-doc block = 16 threads
+    constexpr int U = 2;
+    const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    const uint32_t total = nqual * 16;
     for (uint32_t w0 = tid; w0 < total; w0 += (uint32_t)nth * U) {
-      float v[U];
-      int64_t idx[U];
+      float v[U][4];
+      int64_t i0[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t w = w0 + (uint32_t)(u * nth);
-        idx[u] = w < total ? (int64_t)qual[w >> 6] * 64 + (w & 63) : n;
-        v[u] = idx[u] < n ? x[idx[u]] : neg_inf();
+        i0[u] = w < total ? (int64_t)qual[w >> 4] * 64 + 4 * (w & 15) : n;
+        if (vec && i0[u] + 3 < n) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(x + i0[u]);
+          v[u][0] = q[0], v[u][1] = q[1], v[u][2] = q[2], v[u][3] = q[3];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[u][e] = i0[u] + e < n ? x[i0[u] + e] : neg_inf();
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (idx[u] < n && f2u(v[u]) >= t) {
-          const uint32_t pos = atomicAdd(&misc[1], 1u);
-          if (pos < (uint32_t)kBmCand) sel[pos] = rank_key(v[u], (uint32_t)idx[u]);
-        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (i0[u] + e < n && f2u(v[u][e]) >= t) {
+            const uint32_t pos = atomicAdd(&misc[1], 1u);
+            if (pos < (uint32_t)kBmCand) sel[pos] = rank_key(v[u][e], (uint32_t)(i0[u] + e));
+          }
     }
   }
   __syncthreads();
+  lab_stamp(stamps, 3);
   const uint32_t ncand = misc[1];
   int m = (int)ncand;
   if (nqual > (uint32_t)kBmQual || ncand < (uint32_t)kk || ncand > (uint32_t)kBmCand) {
@@ -3143,15 +3279,19 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
     m = kk;
   }
   if (m <= kBmRankMax) {   // rank by counting: keys are unique, rank = #greater
-    for (int i = tid; i < m; i += nth) {
-      const uint64_t key = sel[i];
-      int r = 0;
-      for (int j = 0; j < m; ++j) r += sel[j] > key ? 1 : 0;
-      if (r < k) {
-        os[r] = u2f((uint32_t)(key >> 32));
-        oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
-        if (mirror.w != nullptr) mirror.put(r, oi[r]);
-      }
+    // T threads per key (consecutive lanes), each counting m / T of the keys
+    int T = 1;
+    while (T < 64 && 2 * T * m <= nth) T <<= 1;
+    const int i = tid / T, p = tid & (T - 1);
+    const uint64_t key = i < m ? sel[i] : 0ull;
+    int r = 0;
+    if (i < m)
+      for (int j = p; j < m; j += T) r += sel[j] > key ? 1 : 0;
+    for (int o = 1; o < T; o <<= 1) r += __shfl_xor(r, o);
+    if (i < m && p == 0 && r < k) {
+      os[r] = u2f((uint32_t)(key >> 32));
+      oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
+      if (mirror.w != nullptr) mirror.put(r, oi[r]);
     }
     for (int j = m + tid; j < k; j += nth) {
       os[j] = neg_inf();
@@ -3160,6 +3300,11 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
     }
   } else {
     sort_and_write(sel, m, k, id_base, os, oi, mirror);
+  }
+  if (stamps != nullptr) {
+    __syncthreads();
+    lab_stamp(stamps, 4);
+    if (tid == 0) stamps[5] = ((uint64_t)nqual << 32) | ncand;
   }
 }
 
@@ -3187,9 +3332,13 @@ __global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __re
                                                                int64_t bm_ld, uint32_t* __restrict__ sb, int64_t sb_ld,
                                                                int32_t* __restrict__ done, int64_t done_ld,
                                                                float* __restrict__ out_s, int32_t* __restrict__ out_i,
-                                                               Mirror mirror) {
+                                                               Mirror mirror, uint64_t* __restrict__ stamps = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   __shared__ int s_last;
+  // stamps (lab only): [16 + 2x] / [17 + 2x] workgroup x's start / keys
+  // stored, [6] the last arrival
+  if (stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
+    stamps[16 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.y;
   const int64_t nb = (n + 63) >> 6;
@@ -3229,9 +3378,12 @@ __global__ __launch_bounds__(kTkThreads) void bmax_topk_kernel(const float* __re
     if (lane == 0 && b0 + 4 * u < nb) st_sc1(srow + (b0 >> 2) + u, s4);
   }
   // <= 96 workgroups per row (n <= 64 * kBmMaxBlocks): one counter
+  if (stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
+    stamps[17 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   if (!row_last_arrival(done + (size_t)row * done_ld, (int)gridDim.x, 1, &s_last)) return;
+  lab_stamp(stamps, 6);
   topk_bmax_row<true>(x, n, k, id_base, brow, srow, out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn,
-                      mirror.row(row, k));
+                      mirror.row(row, k), stamps);
 }
 
 // ---------------------------------------------------------------------------
@@ -3298,22 +3450,28 @@ __global__ __launch_bounds__(kTkThreads) void select_keys_kernel(const uint64_t*
 // ---------------------------------------------------------------------------
 // Small-row selection (rank counting; rows of C <= 1024).
 // ---------------------------------------------------------------------------
+// fin (w nullable): the row's result also to fin's host words (row b; an id
+// the caller does not take is written -1)
 __device__ void select_from_lds(const float* sc, const uint64_t* keys, int C, int k, const int32_t* ids_row,
-                                float* out_s, int32_t* out_i, int32_t* out_p) {
+                                float* out_s, int32_t* out_i, int32_t* out_p, FinalMirror fin = FinalMirror(),
+                                size_t b = 0) {
   for (int t = threadIdx.x; t < C; t += blockDim.x) {
     const uint64_t kt = keys[t];
     int rank = 0;
     for (int j = 0; j < C; ++j) rank += (keys[j] > kt);
     if (rank < k) {
+      const int32_t id = ids_row ? ids_row[t] : t;
       out_s[rank] = sc[t];
-      if (out_i) out_i[rank] = ids_row ? ids_row[t] : t;
+      if (out_i) out_i[rank] = id;
       if (out_p) out_p[rank] = t;
+      if (fin.w != nullptr) fin.put(b, rank, sc[t], out_i ? id : -1, t);
     }
   }
   for (int j = C + threadIdx.x; j < k; j += blockDim.x) {
     out_s[j] = neg_inf();
     if (out_i) out_i[j] = -1;
     if (out_p) out_p[j] = -1;
+    if (fin.w != nullptr) fin.put(b, j, neg_inf(), -1, -1);
   }
 }
 
@@ -3324,7 +3482,8 @@ __global__ __launch_bounds__(256) void select_small_kernel(const float* __restri
                                                            float* __restrict__ out_s,
                                                            int32_t* __restrict__ out_i,
                                                            int32_t* __restrict__ out_p,
-                                                           const uint64_t* __restrict__ ids_tagged = nullptr) {
+                                                           const uint64_t* __restrict__ ids_tagged = nullptr,
+                                                           FinalMirror fin = FinalMirror()) {
   __shared__ float sc[kSmallMax];
   __shared__ uint64_t keys[kSmallMax];
   __shared__ int32_t tid_ids[kSmallMax];
@@ -3337,7 +3496,7 @@ __global__ __launch_bounds__(256) void select_small_kernel(const float* __restri
   __syncthreads();
   const int32_t* idr = ids_tagged != nullptr ? tid_ids : (ids ? ids + b * C : nullptr);
   select_from_lds(sc, keys, C, k, idr, out_s + b * k, out_i ? out_i + b * k : nullptr,
-                  out_p ? out_p + b * k : nullptr);
+                  out_p ? out_p + b * k : nullptr, fin, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -3664,10 +3823,11 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 // faithful scores, order-preserving bits), done[b] = 0 (the fallback's
 // finished-workgroup counter), the row's arrival counters (arrive: narrive
 // ints per row over kArriveSlotsK slots -- the launches that select in their
-// last workgroup: the block-max select, the band select, the rerank select)
+// last workgroup: the block-max select, the band select, the rerank select;
+// and phase 1's finished-pair count of phase1_collect_kernel)
 // and -- ctr, the search's scan -- the scan's task-counter block: launches
 // fewer than separate memsets.
-constexpr int kArriveSlotsK = 3;   // slots of the faithful workspace's arrival counters (kArriveSlots)
+constexpr int kArriveSlotsK = 4;   // slots of the faithful workspace's arrival counters (kArriveSlots)
 __global__ __launch_bounds__(512) void split_query_kernel(const float* __restrict__ Q, int lq,
                                                           uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
                                                           float E, float M, float* __restrict__ beta,
@@ -3907,19 +4067,23 @@ struct RowSelect {
   const uint32_t* lbu = nullptr; //   its order-preserving bits (the two-pass band's)
   int32_t* status = nullptr;     // kSelBand: the band size (the fallback writes -1 for overflowed rows)
   Mirror ids_mirror;             // kSelBand: [B][k] host mirror of the final ids (w nullable)
+  FinalMirror fin;               // kSelCand: the host words of the call's final result (w nullable)
+  uint64_t* stamps = nullptr;    // lab builds only (LAB_STAMPS): [16 + 2x] / [17 + 2x] workgroup x's start /
+                                 // end of its pairs, [6] the row select's start, [4] its end
 };
 constexpr int kSelNone = 0, kSelCand = 1, kSelBand = 2;
 
 // kSelCand (= select_small_kernel's work): the row's C <= kSmallMax raw
 // scores (stored in this launch: sc1 loads), ranked with the position rule.
 __device__ void select_cand_row(const float* raw, const int32_t* crow, int C, int k, float* os, int32_t* oi,
-                                int32_t* op, float* sc, uint64_t* keys) {
+                                int32_t* op, float* sc, uint64_t* keys, FinalMirror fin = FinalMirror(),
+                                size_t b = 0) {
   for (int t = threadIdx.x; t < C; t += blockDim.x) {
     sc[t] = ld_sc1(raw + t);
     keys[t] = rank_key(sc[t], (uint32_t)t);
   }
   __syncthreads();
-  select_from_lds(sc, keys, C, k, crow, os, oi, op);
+  select_from_lds(sc, keys, C, k, crow, os, oi, op, fin, b);
 }
 
 // kSelBand (= band_select_kernel's result): the exact top-k of the row's cnt
@@ -3938,12 +4102,17 @@ __device__ void select_band_row(const float* F, const int32_t* cand, int cnt, in
   if (tid < 8) misc[tid] = 0;
   __syncthreads();
   const uint32_t ulb = has_lb ? f2u(lbv) : 0u;
-  for (int i = tid; i < cnt; i += nth) {
-    const uint64_t key = key_at(i);
-    if ((uint32_t)(key >> 32) >= ulb) {
-      const uint32_t pos = atomicAdd(&misc[0], 1u);
-      if (pos < (uint32_t)kTopkMax) sel[pos] = key;
-    }
+  constexpr int U = 8;   // U keys' loads in flight per thread, then the filter
+  for (int i0 = tid; i0 < cnt; i0 += nth * U) {
+    uint64_t kv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) kv[u] = i0 + u * nth < cnt ? key_at(i0 + u * nth) : 0ull;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * nth < cnt && (uint32_t)(kv[u] >> 32) >= ulb) {
+        const uint32_t pos = atomicAdd(&misc[0], 1u);
+        if (pos < (uint32_t)kTopkMax) sel[pos] = kv[u];
+      }
   }
   __syncthreads();
   int m = (int)misc[0];
@@ -4017,6 +4186,8 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b = blockIdx.y;
+  if (rs.stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
+    rs.stamps[16 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   if (only_neg != nullptr && only_neg[b] >= 0) return;  // block-uniform
   int64_t lim = limit;
   if (count != nullptr) {
@@ -4058,7 +4229,13 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
     for (int64_t c = c0 + blockIdx.x; c < lim; c += gridDim.x) {   // block-uniform trip count
       int64_t id;
       if (tc.w != nullptr) {   // pre-armed (the latency path's rerank): the host writes the candidate after the launch
-        if (threadIdx.x == 0) s_cid = wait_tagged(tc.w + (size_t)b * ld_c + c, tc.seq);
+        if (threadIdx.x == 0) {
+          s_cid = wait_tagged(tc.w + (size_t)b * ld_c + c, tc.seq);
+          // handed to the row select through device memory (cand: the
+          // caller's device array, unread on this path), not re-read from host
+          if (rs.mode != kSelNone)
+            st_sc1(reinterpret_cast<uint32_t*>(const_cast<int32_t*>(cand)) + (size_t)b * ld_c + c, (uint32_t)s_cid);
+        }
         __syncthreads();
         id = s_cid;
         __syncthreads();   // s_cid is rewritten by the next pair
@@ -4078,18 +4255,22 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
       }
     }
   }
+  if (rs.stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
+    rs.stamps[17 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   if (rs.mode == kSelNone) return;
   if (!row_last_arrival(rs.arrive + (size_t)b * kArriveInts, (int)gridDim.x, 8, &s_last)) return;
+  lab_stamp(rs.stamps, 6);
   if (rs.mode == kSelCand) {   // C = limit candidates, ids = the row's cand
     const int32_t* crow = cand + (size_t)b * ld_c;
-    if (tc.w != nullptr) {       // the tagged words, all present (every workgroup of the row waited for its own)
+    if (tc.w != nullptr) {       // the ids each workgroup stored for its candidate (sc1), not the host words
       int32_t* ids_lds = reinterpret_cast<int32_t*>(hist) + kSmallMax;
-      for (int t = threadIdx.x; t < (int)limit; t += blockDim.x) ids_lds[t] = read_tagged(tc.w + (size_t)b * ld_c + t);
+      for (int t = threadIdx.x; t < (int)limit; t += blockDim.x)
+        ids_lds[t] = (int32_t)ld_sc1(reinterpret_cast<const uint32_t*>(crow) + t);
       crow = ids_lds;            // (published by select_cand_row's barrier)
     }
     select_cand_row(out + (size_t)b * ld_out, crow, (int)limit, rs.k, rs.out_s + (size_t)b * rs.k,
                     rs.out_i + (size_t)b * rs.k, rs.out_p ? rs.out_p + (size_t)b * rs.k : nullptr,
-                    reinterpret_cast<float*>(hist), sel);
+                    reinterpret_cast<float*>(hist), sel, rs.fin, (size_t)b);
   } else {                     // the band: lim keys (count[b] <= limit here)
     const bool has_lb = rs.lb != nullptr || rs.lbu != nullptr;
     const float lbv = rs.lbu != nullptr ? u2f(rs.lbu[b]) : (rs.lb != nullptr ? rs.lb[b] : 0.0f);
@@ -4097,6 +4278,11 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
                     rs.out_s + (size_t)b * rs.k, rs.out_i + (size_t)b * rs.k, sel, hist, misc,
                     rs.ids_mirror.row(b, rs.k));
     if (threadIdx.x == 0) rs.status[b] = (int32_t)lim;
+  }
+  if (rs.stamps != nullptr) {
+    __syncthreads();
+    lab_stamp(rs.stamps, 4);
+    if (threadIdx.x == 0) rs.stamps[5] = (uint64_t)lim;
   }
 }
 
@@ -4481,10 +4667,13 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
                                                            const float* __restrict__ lb,
                                                            const uint32_t* __restrict__ lbu,
                                                            const int32_t* __restrict__ topk_i,
-                                                           const uint32_t* __restrict__ bm) {
+                                                           const uint32_t* __restrict__ bm,
+                                                           uint64_t* __restrict__ stamps = nullptr) {
   __shared__ int32_t s_ids[kBandLds];
   __shared__ int s_n, s_base;
   const int b = blockIdx.y, lane = threadIdx.x & 63;
+  if (stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
+    stamps[16 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   const float thr = band_threshold(b, lb, lbu, topk_s, k, beta);
@@ -4542,25 +4731,34 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
       int q = 0;
       for (uint64_t m = qual; m != 0; m &= m - 1, ++q)
         if (q % nw == wave) mine |= m & (~m + 1);
-      while (mine != 0) {             // wave-uniform; 4 blocks per step
-        int64_t blk = -1;
+      while (mine != 0) {             // wave-uniform; 4 blocks per step, 4 steps' loads in flight
+        int64_t i0[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int64_t bu = mine != 0 ? g0 + (__ffsll((long long)mine) - 1) : -1;
-          if (mine != 0) mine &= mine - 1;
-          if (u == r4) blk = bu;
+        for (int s4 = 0; s4 < 4; ++s4) {
+          int64_t blk = -1;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t bu = mine != 0 ? g0 + (__ffsll((long long)mine) - 1) : -1;
+            if (mine != 0) mine &= mine - 1;
+            if (u == r4) blk = bu;
+          }
+          i0[s4] = blk >= 0 ? (blk << 6) + 4 * c16 : n;
         }
-        const int64_t i0 = blk >= 0 ? (blk << 6) + 4 * c16 : n;
-        float v[4];
-        if (vec && i0 + 3 < n) {
-          const f32x4 x4 = *reinterpret_cast<const f32x4*>(row + i0);
-          v[0] = x4[0], v[1] = x4[1], v[2] = x4[2], v[3] = x4[3];
-        } else {
+        float v[4][4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = i0 + e < n ? row[i0 + e] : 0.0f;
+        for (int s4 = 0; s4 < 4; ++s4) {
+          if (vec && i0[s4] + 3 < n) {
+            const f32x4 x4 = *reinterpret_cast<const f32x4*>(row + i0[s4]);
+            v[s4][0] = x4[0], v[s4][1] = x4[1], v[s4][2] = x4[2], v[s4][3] = x4[3];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[s4][e] = i0[s4] + e < n ? row[i0[s4] + e] : 0.0f;
+          }
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) offer(i0 + e < n ? i0 + e : n, v[e]);
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) offer(i0[s4] + e < n ? i0[s4] + e : n, v[s4][e]);
       }
     }
   } else {
@@ -4583,6 +4781,169 @@ __global__ __launch_bounds__(256) void band_collect_kernel(const float* __restri
   __syncthreads();
   for (int t = threadIdx.x; t < nl; t += blockDim.x)
     if (s_base + t < cap) crow[s_base + t] = s_ids[t];
+  if (stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs) {
+    stamps[17 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(reinterpret_cast<unsigned long long*>(stamps + 5), (unsigned long long)s_n);
+  }
+}
+
+// Phase 1 of the two-pass band and the band collect in ONE launch (the latency
+// path, B <= kBandPairMaxB; band_collect_kernel's block-key path with the
+// bf16 top-k reused): grid (k + S, B), 256 threads.
+//  * workgroups x < k: phase 1's pair x -- the faithful score of the bf16
+//    top-k's doc x into F[b][x] (sc1) and the atomic min into lbu[b] (for the
+//    later launches), then counts it on done1[b]'s 8 replicas (one agent add
+//    per replica);
+//  * workgroups x >= k: the collect of 64-doc blocks [64 (x - k), +64).  While
+//    phase 1 runs they load the 64 block keys and the scores of every block
+//    that can hold a band doc at all (key >= T_k - 2 beta: lb >= T_k - beta,
+//    since each of the k faithful scores is >= its bf16 score - beta); then
+//    they wait for the row's phase 1 (thread 0 polls one replica of done1[b]
+//    with sc1 loads until it reaches k), take lb = the minimum of F[b][0..k) (sc1 loads: the
+//    same bits as the atomic min) and keep, as band_collect_kernel does, the
+//    docs with T >= lb - beta below the k-th bf16 key.
+// The hand-off is MI355X_MICROARCH.md's hand-off table, row 2 (sc1 stores,
+// vmcnt(0), one wave instruction adding to every replica; sc1 poll of one
+// replica, barrier, 4-B sc1 loads).  A collect
+// workgroup waits only for phase-1 workgroups of its row, all of lower
+// linear index -- dispatched before it, and never waiting themselves -- so the
+// launch cannot deadlock whatever the occupancy.  done1 is zeroed by the query
+// split.  Same band (as a set) as phase 1 + band_collect_kernel; the band's
+// order is the collect's append order either way (the select ranks by key).
+constexpr int kP1Replicas = 8;   // done1 replicas (32 ints apart, within one kArriveInts slot)
+static_assert(32 * kP1Replicas <= kArriveInts, "done1's replicas fit one arrival slot");
+__global__ __launch_bounds__(256, 2) void phase1_collect_kernel(
+    const uint8_t* __restrict__ hi, const uint8_t* __restrict__ lo, const int32_t* __restrict__ doclens, int64_t n,
+    int64_t id_base, const uint16_t* __restrict__ qhi, const uint16_t* __restrict__ qlo, int lq,
+    const int32_t* __restrict__ topk_i, const float* __restrict__ topk_s, int k, float* __restrict__ F,
+    int64_t ld_F, uint32_t* __restrict__ lbu, int32_t* __restrict__ done1, int64_t done_ld,
+    const float* __restrict__ T, const float* __restrict__ beta, const uint32_t* __restrict__ bm, int cap,
+    int32_t* __restrict__ cand, int32_t* __restrict__ count, uint64_t* __restrict__ stamps = nullptr) {
+  __shared__ float s_m[4][32];
+  __shared__ int32_t s_ids[kBandLds];
+  __shared__ int s_n, s_base;
+  __shared__ uint32_t s_lb;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  const int x = blockIdx.x;
+  if (stamps != nullptr && threadIdx.x == 0 && x < kLabWgs) stamps[16 + 2 * x] = __builtin_amdgcn_s_memrealtime();
+  if (x < k) {   // ---- phase 1: pair x of row b
+    bf16x8 qh[2][4], ql[2][4];
+    load_qfrag16(qhi, b, b + 1, lq, lane, qh);
+    load_qfrag16(qlo, b, b + 1, lq, lane, ql);
+    const int64_t id = topk_i[(size_t)b * k + x];
+    const int64_t loc = id - id_base;
+    float v = neg_inf();
+    if (id >= 0 && loc >= 0 && loc < n)   // block-uniform
+      v = faithful_doc_split<false, 4>(hi, lo, loc, kLd, doclens[loc], qh, ql, lane, wave, lq, s_m);
+    if (threadIdx.x == 0) {
+      st_sc1(F + (size_t)b * ld_F + x, v);
+      atomicMin(lbu + b, f2u(v));
+    }
+    if (wave == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the F store has landed
+      // done1 in 8 replicas 128 B apart (hand-off table, row 2: one wave
+      // instruction, one lane per replica): each collect workgroup polls one
+      // of them, so ~1/8 of the pollers share a line with the adds
+      if (lane < kP1Replicas)
+        __hip_atomic_fetch_add(done1 + (size_t)b * done_ld + 32 * lane, 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      if (stamps != nullptr && lane == 0 && x < kLabWgs) stamps[17 + 2 * x] = __builtin_amdgcn_s_memrealtime();
+    }
+    return;
+  }
+  // ---- the collect of blocks [64 g, 64 g + 64) of row b
+  if (threadIdx.x == 0) s_n = 0;
+  if (threadIdx.x == 0) s_lb = 0xffffffffu;
+  const float* row = T + (size_t)b * n;
+  int32_t* crow = cand + (size_t)b * cap;
+  const uint64_t kth = rank_key(topk_s[(size_t)b * k + k - 1], (uint32_t)((int64_t)topk_i[(size_t)b * k + k - 1] - id_base));
+  if (x == k)   // the band's slots [0, k): the bf16 top-k, rescored by phase 1 (count[b] starts at k)
+    for (int j = threadIdx.x; j < k; j += blockDim.x) crow[j] = topk_i[(size_t)b * k + j];
+  const int64_t nb = (n + 63) >> 6;
+  const int64_t g0 = (int64_t)(x - k) * 64;
+  const uint32_t uthr0 = f2u(topk_s[(size_t)b * k + k - 1] - 2.0f * beta[b]);   // <= any lb - beta
+  const int nw = blockDim.x >> 6;
+  const int c16 = lane & 15, r4 = lane >> 4;
+  const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(T) & 15) == 0;
+  const int64_t kb = g0 + lane;   // one block key per lane
+  const uint64_t qual = __ballot(kb < nb && bm[(size_t)b * nb + kb] >= uthr0);
+  uint64_t mine = 0;              // this wave's share: qualifying blocks q = wave (mod nw), <= 16
+  {
+    int q = 0;
+    for (uint64_t m = qual; m != 0; m &= m - 1, ++q)
+      if (q % nw == wave) mine |= m & (~m + 1);
+  }
+  int64_t i0[4];
+  float v[4][4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {   // 4 blocks per step, 4 steps: every load in flight before the wait
+    int64_t blk = -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t bu = mine != 0 ? g0 + (__ffsll((long long)mine) - 1) : -1;
+      if (mine != 0) mine &= mine - 1;
+      if (u == r4) blk = bu;
+    }
+    i0[s4] = blk >= 0 ? (blk << 6) + 4 * c16 : n;
+    if (vec && i0[s4] + 3 < n) {
+      const f32x4 x4 = *reinterpret_cast<const f32x4*>(row + i0[s4]);
+      v[s4][0] = x4[0], v[s4][1] = x4[1], v[s4][2] = x4[2], v[s4][3] = x4[3];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[s4][e] = i0[s4] + e < n ? row[i0[s4] + e] : 0.0f;
+    }
+  }
+  // phase 1 of row b done: thread 0 polls (sc1), the barrier releases the rest
+  if (threadIdx.x == 0) {
+    const int32_t* d = done1 + (size_t)b * done_ld + 32 * ((x - k) % kP1Replicas);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k &&
+           __builtin_amdgcn_s_memrealtime() - t0 < kCandWaitTicks)
+      __builtin_amdgcn_s_sleep(4);
+  }
+  __syncthreads();
+  {   // lb = min over the k faithful scores (sc1 loads), as the atomic min has it
+    uint32_t mn = ~0u;
+    for (int j = threadIdx.x; j < k; j += blockDim.x) mn = min(mn, f2u(ld_sc1(F + (size_t)b * ld_F + j)));
+    mn = wave_min_u32(mn);
+    if (lane == 0) atomicMin(&s_lb, mn);
+  }
+  __syncthreads();
+  const float thr = u2f(s_lb) - beta[b];
+  auto offer = [&](int64_t i, float val) {
+    const bool take = i < n && val >= thr && rank_key(val, (uint32_t)i) < kth;
+    const uint64_t mask = __ballot(take);
+    if (mask == 0) return;
+    const int nh = __popcll(mask);
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&s_n, nh);
+    base = __shfl(base, 0);
+    const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+    if (take) {
+      if (pos < kBandLds) {
+        s_ids[pos] = (int32_t)(id_base + i);
+      } else {
+        const int gp = atomicAdd(count + b, 1);
+        if (gp < cap) crow[gp] = (int32_t)(id_base + i);
+      }
+    }
+  };
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) offer(i0[s4] + e < n ? i0[s4] + e : n, v[s4][e]);
+  __syncthreads();
+  const int nl = s_n < kBandLds ? s_n : kBandLds;
+  if (threadIdx.x == 0) s_base = nl > 0 ? atomicAdd(count + b, nl) : 0;
+  __syncthreads();
+  for (int t = threadIdx.x; t < nl; t += blockDim.x)
+    if (s_base + t < cap) crow[s_base + t] = s_ids[t];
+  if (stamps != nullptr && threadIdx.x == 0 && x < kLabWgs) {
+    stamps[17 + 2 * x] = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(reinterpret_cast<unsigned long long*>(stamps + 5), (unsigned long long)s_n);
+  }
 }
 
 // Band collect + rescoring in ONE launch, for batches of at most
@@ -4982,6 +5343,7 @@ struct cbv2_index {
   // MXFP8 its 4 x 1 shape) instead of the streaming scan that skips empty
   // tiles (6.9 TB/s)
   bool dense_docs = false;
+  bool p1_collect_fused = true;  // CBV2_OPT_P1_COLLECT_FUSED (phase1_collect_kernel)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -5227,6 +5589,21 @@ thread_local bool g_ids_mirror_used = false;
 // around its rerank call): a rerank that can take them sets g_cand_tagged_used.
 thread_local TaggedCand g_cand_tagged;
 thread_local bool g_cand_tagged_used = false;
+// The final result's host words (cbv2_set_final_mirror, set by retrieve.cpp
+// around its rerank call): a rerank whose select writes them sets
+// g_final_mirror_used (else the caller copies the result down).
+thread_local FinalMirror g_final_mirror;
+thread_local bool g_final_mirror_used = false;
+// Lab builds (-DCBV2_LAB_STAMPS, tools/chain_lab.py): per-launch phase stamps
+// of the latency path's kernels, kind k at g_lab_stamps + k * kLabStride --
+// 0 block-max select, 1 phase-1 rescoring, 2 band collect, 3 band rescoring +
+// select, 4 rerank + select.  Product builds: no stamps.
+#ifdef CBV2_LAB_STAMPS
+thread_local uint64_t* g_lab_stamps = nullptr;
+#define LAB_STAMPS(kind) (g_lab_stamps != nullptr ? g_lab_stamps + (size_t)(kind) * kLabStride : nullptr)
+#else
+#define LAB_STAMPS(kind) ((uint64_t*)nullptr)
+#endif
 thread_local int g_ctr_policy = kCtrDefault;
 thread_local bool g_ctr_zeroed = false;
 struct CtrPolicy {
@@ -5810,7 +6187,7 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   if (mirror.w != nullptr) g_ids_mirror_used = true;   // every row's ids written to it below
   static std::atomic<bool> attr_set[64] = {};
   if (dev < 0 || dev >= 64 || !attr_set[dev].load(std::memory_order_relaxed)) {   // once per device
-    const int lds_max = (int)(kBmFixedLds + (size_t)(kBmMaxBlocks / 4) * 4);
+    const int lds_max = (int)(kBmFixedLds + (size_t)kBmMaxBlocks * 4);
     CBV2_HIP(hipFuncSetAttribute((const void*)topk_bmax_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
     CBV2_HIP(hipFuncSetAttribute((const void*)bmax_topk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max));
     if (dev >= 0 && dev < 64) attr_set[dev].store(true, std::memory_order_relaxed);
@@ -5818,11 +6195,11 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   const int64_t nb = bm_blocks(n), ns = bm_supers(n);
   uint32_t* sb = bm_super_keys(bm, B, n);
   if (!blocks_ready && done != nullptr && B <= kBmFusedMaxB) {
-    const size_t lds = kBmFixedLds + (size_t)ns * 4;
+    const size_t lds = bm_select_lds(n, k);
     hipLaunchKernelGGL(bmax_topk_kernel, dim3((unsigned)((nb + kBmFusedBlocksPerWg - 1) / kBmFusedBlocksPerWg),
                                                (unsigned)B),
                        dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm, nb, sb, ns, done, done_ld, out_s,
-                       out_i, mirror);
+                       out_i, mirror, LAB_STAMPS(0));
     return launch_check("bmax_topk_kernel");
   }
   if (!blocks_ready) {
@@ -5830,7 +6207,7 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
                        dim3(256), 0, st, scores, n, ld, bm, nb, sb, ns);
     if (int rc = launch_check("block_max_kernel")) return rc;
   }
-  const size_t lds = kBmFixedLds + (size_t)ns * 4;
+  const size_t lds = bm_select_lds(n, k);
   hipLaunchKernelGGL(topk_bmax_kernel, dim3((unsigned)B), dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm,
                      nb, sb, ns, out_s, out_i, mirror);
   return launch_check("topk_bmax_kernel");
@@ -6016,7 +6393,7 @@ struct F32Ws {
 // slot j at (j * B + b) * kArriveInts): the launches whose last workgroup per
 // row runs the row's selection (row_last_arrival).
 constexpr int kArriveSlots = kArriveSlotsK;
-constexpr int kArrBmax = 0, kArrBand = 1, kArrRerank = 2;
+constexpr int kArrBmax = 0, kArrBand = 1, kArrRerank = 2, kArrPhase1 = 3;
 inline int32_t* arrive_row0(const F32Ws& w, int slot, int B) { return w.arrive + (size_t)slot * B * kArriveInts; }
 
 // op SCORE: split queries; RERANK: + F [B][C]; SEARCH: + band [B][cap] + scan.
@@ -6454,6 +6831,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
     case CBV2_OPT_DENSE_DOCS:
       ix->dense_docs = value != 0;
       return CBV2_OK;
+    case CBV2_OPT_P1_COLLECT_FUSED:
+      ix->p1_collect_fused = value != 0;
+      return CBV2_OK;
     case CBV2_OPT_RESCORE_GRID:
       if (value < 0 || value > 65535) return fail(CBV2_EINVAL, "rescore grid must be in [0, 65535]");
       ix->rescore_grid = (int)value;
@@ -6529,8 +6909,10 @@ static int rerank_impl(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, con
                          ix->doclens, ix->n, ix->id_base, Qb, nullptr, lq, cand, C, raw, (int)ix->ld);
     if ((rc = launch_check("rerank_raw_kernel"))) return rc;
     if (k == 0) return CBV2_OK;
+    const FinalMirror fin = g_final_mirror.k == k ? g_final_mirror : FinalMirror();
+    if (fin.w != nullptr) g_final_mirror_used = true;
     hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
-                       out_pos, tc.w);
+                       out_pos, tc.w, fin);
     return launch_check("select_small_kernel");
   }
   if (f8) {
@@ -6648,6 +7030,14 @@ namespace {
 bool band_reuses_topk(const cbv2_index* ix, int32_t B, int32_t k) {
   return ix->band_reuse && ix->rescore_split && ix->n >= k && !(B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused);
 }
+// The two-pass band's phase 1 and band collect in one launch
+// (phase1_collect_kernel): small batches whose band reuses the bf16 top-k, on
+// the block keys of the block-max select, pair by pair with the row select
+// and the fallback in the rescoring launch.
+bool phase1_collect_fused(const cbv2_index* ix, int32_t B, int32_t k) {
+  return ix->p1_collect_fused && B <= kBandPairMaxB && k <= kTopkMax && band_reuses_topk(ix, B, k) &&
+         bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k) && ix->band_block_skip && !ix->band_doc_major;
+}
 
 int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int32_t k, int32_t cap, F32Ws& w,
                       float* out_scores, int32_t* out_ids, int32_t* out_status, bool want_lb, hipStream_t st,
@@ -6684,9 +7074,14 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
   if ((rc = band_mark(ix, false, st))) return rc;
   if (fk_out != nullptr)     // the bf16 top-k's own faithful scores, for the caller's cross-shard bound
     return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, fk_out, k, st);
-  if (want_lb)   // the bf16 top-k's own faithful scores: k docs score at least their minimum
+  if (want_lb && phase1_collect_fused(ix, B, k))   // in phase 2's first launch (phase1_collect_kernel)
+    return CBV2_OK;
+  if (want_lb) {   // the bf16 top-k's own faithful scores: k docs score at least their minimum
+    RowSelect lab;
+    lab.stamps = LAB_STAMPS(1);
     return launch_rescore(ix, &w, B, lq, out_ids, nullptr, k, k, w.F, cap, st, nullptr, 0,
-                          reinterpret_cast<uint32_t*>(w.lb));
+                          reinterpret_cast<uint32_t*>(w.lb), 0, nullptr, nullptr, 0, nullptr, nullptr, lab);
+  }
   return CBV2_OK;
 }
 
@@ -6709,7 +7104,16 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
   const int64_t max_splits = (ix->n + 8191) / 8192;
   splits = splits < max_splits ? splits : max_splits;
   splits = splits < 1 ? 1 : splits;
-  if (B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused) {
+  if (lbu != nullptr && phase1_collect_fused(ix, B, k)) {
+    // phase 1 + the collect in one launch (phase 1 was left out of phase1)
+    const int64_t groups = (bm_blocks(ix->n) + 63) / 64;
+    hipLaunchKernelGGL(phase1_collect_kernel, dim3((unsigned)(k + groups), (unsigned)B), dim3(256), 0, st,
+                       ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w.qhi, w.qlo, lq, out_ids, out_scores,
+                       k, w.F, (int64_t)cap, const_cast<uint32_t*>(lbu), arrive_row0(w, kArrPhase1, B),
+                       (int64_t)kArriveInts, w.T, w.beta, reinterpret_cast<const uint32_t*>(w.tk), cap, w.cand,
+                       w.count, LAB_STAMPS(1));
+    if ((rc = launch_check("phase1_collect_kernel"))) return rc;
+  } else if (B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused) {
     // the latency path: collect + rescore in one launch, one band doc per wave
     const int64_t gx = (ix->n + kBcrDocs - 1) / kBcrDocs;
     hipLaunchKernelGGL(band_collect_rescore_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
@@ -6726,7 +7130,8 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
     }
     hipLaunchKernelGGL(band_collect_kernel, dim3((unsigned)splits, (unsigned)B), dim3(256), 0, st, w.T, ix->n,
                        out_scores, k, w.beta, ix->id_base, cap, w.cand, w.count, lb, lbu,
-                       reuse ? out_ids : nullptr, bkeys ? reinterpret_cast<const uint32_t*>(w.tk) : nullptr);
+                       reuse ? out_ids : nullptr, bkeys ? reinterpret_cast<const uint32_t*>(w.tk) : nullptr,
+                       LAB_STAMPS(2));
     if ((rc = launch_check("band_collect_kernel"))) return rc;
   }
   // pairs grouped by doc (each band doc's tiles read once per batch) pay when
@@ -6780,6 +7185,7 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
       rs.status = out_status;
       rs.ids_mirror = g_ids_mirror;
       if (g_ids_mirror.w != nullptr) g_ids_mirror_used = true;   // selected or fallen back, every row writes it
+      rs.stamps = LAB_STAMPS(3);
     }
     if ((rc = launch_rescore(ix, &w, B, lq, w.cand, w.count, cap, cap, w.F, cap, st, nullptr,
                              B <= kBandPairMaxB ? 1 : 0, nullptr, c0, fb_fused ? w.T : nullptr,
@@ -6839,14 +7245,21 @@ int rerank_f32_split(cbv2_index* ix, F32Ws& w, int32_t B, int32_t lq, const int3
     rs.out_p = out_pos;
     const TaggedCand tc = g_cand_tagged;   // the latency path's pre-armed rerank (cand unused then)
     if (tc.w != nullptr) g_cand_tagged_used = true;
+    if (g_final_mirror.w != nullptr && g_final_mirror.k == k) {
+      rs.fin = g_final_mirror;
+      g_final_mirror_used = true;
+    }
+    rs.stamps = LAB_STAMPS(4);
     return launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
                           nullptr, nullptr, rs, tc);
   }
   if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
   if (k == 0) return CBV2_OK;
   if (C > kSmallMax) return topk_multi(raw, B, C, C, k, 0, cand, C, out_scores, out_ids, out_pos, st);
+  const FinalMirror fin = g_final_mirror.k == k ? g_final_mirror : FinalMirror();
+  if (fin.w != nullptr) g_final_mirror_used = true;
   hipLaunchKernelGGL(select_small_kernel, dim3((unsigned)B), dim3(256), 0, st, raw, cand, C, k, out_scores, out_ids,
-                     out_pos);
+                     out_pos, nullptr, fin);
   return launch_check("select_small_kernel");
 }
 
@@ -6986,6 +7399,14 @@ void cbv2_set_cand_tagged(const void* p, uint32_t seq) {
   g_cand_tagged_used = false;
 }
 int cbv2_cand_tagged_used(void) { return g_cand_tagged_used ? 1 : 0; }
+void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k) {
+  g_final_mirror = p != nullptr ? FinalMirror{(uint64_t*)p, seq, (int)k} : FinalMirror();
+  g_final_mirror_used = false;
+}
+int cbv2_final_mirror_used(void) { return g_final_mirror_used ? 1 : 0; }
+#ifdef CBV2_LAB_STAMPS
+void cbv2_lab_set_stamps(void* p) { g_lab_stamps = (uint64_t*)p; }
+#endif
 
 // Internal (retrieve.cpp): the device an index lives on (-1: null index).
 int cbv2_index_device(const cbv2_index* ix) { return ix ? ix->device : -1; }

@@ -26,8 +26,22 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
   // 200 ids per call: allocation would be most of its cost)
   thread_local std::vector<int32_t> ids, slot;
   thread_local std::vector<double> sc;
-  thread_local std::vector<int> order;
+  struct Entry {
+    double s;
+    int32_t j;   // insertion position
+  };
+  thread_local std::vector<Entry> order;
   thread_local std::vector<uint32_t> used;
+  // 1 / (rrf_k + rank) for ranks 1 .. max(kb, kc): the same division, once
+  // per call instead of once per list entry
+  thread_local std::vector<double> inv;
+  thread_local int32_t inv_k = -1;
+  const int32_t rmax = std::max(kb, kc);
+  if (inv_k != rrf_k || (int32_t)inv.size() < rmax + 1) {
+    inv.resize((size_t)rmax + 1);
+    for (int32_t r = 1; r <= rmax; ++r) inv[r] = 1.0 / (double)(rrf_k + r);
+    inv_k = rrf_k;
+  }
   ids.clear();
   sc.clear();
   ids.reserve(kb + kc);
@@ -49,7 +63,7 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
     for (uint32_t h : used) slot[h] = -1;
     used.clear();
     auto add = [&](int32_t id, int32_t rank) {
-      const double inc = 1.0 / (double)(rrf_k + rank);
+      const double inc = inv[rank];
       uint32_t h = ((uint32_t)id * 2654435761u) >> (32 - bits);
       for (;; h = (h + 1) & mask) {
         const int32_t j = slot[h];
@@ -70,17 +84,18 @@ int cbv2_rrf_fuse(const int32_t* bm25_ids, int32_t kb, const int32_t* colbert_id
       if (id >= 0) add(id, r + 1);
     }
     order.resize(ids.size());
-    for (size_t j = 0; j < ids.size(); ++j) order[j] = (int)j;
+    for (size_t j = 0; j < ids.size(); ++j) order[j] = Entry{sc[j], (int32_t)j};
     // the first C of the STABLE descending sort: (score desc, insertion order
     // asc) is a strict total order, so a partial sort on it yields exactly the
     // stable sort's prefix
     const size_t m = std::min<size_t>((size_t)C, order.size());
-    std::partial_sort(order.begin(), order.begin() + m, order.end(),
-                      [&](int a, int c) { return sc[a] > sc[c] || (sc[a] == sc[c] && a < c); });
+    const auto before = [](const Entry& a, const Entry& c) { return a.s > c.s || (a.s == c.s && a.j < c.j); };
+    if (m < order.size()) std::nth_element(order.begin(), order.begin() + m, order.end(), before);
+    std::sort(order.begin(), order.begin() + m, before);
     for (int32_t j = 0; j < C; ++j) {
-      const bool ok = j < (int32_t)order.size();
-      out_ids[(size_t)b * C + j] = ok ? ids[order[j]] : -1;
-      if (out_scores) out_scores[(size_t)b * C + j] = ok ? sc[order[j]] : 0.0;
+      const bool ok = j < (int32_t)m;
+      out_ids[(size_t)b * C + j] = ok ? ids[order[j].j] : -1;
+      if (out_scores) out_scores[(size_t)b * C + j] = ok ? order[j].s : 0.0;
     }
     if (out_count) out_count[b] = (int32_t)ids.size();
   }

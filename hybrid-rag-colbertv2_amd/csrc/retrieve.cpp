@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -36,6 +37,8 @@ extern "C" void cbv2_set_ids_mirror(void* p, uint32_t seq);
 extern "C" int cbv2_ids_mirror_used(void);
 extern "C" void cbv2_set_cand_tagged(const void* p, uint32_t seq);
 extern "C" int cbv2_cand_tagged_used(void);
+extern "C" void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k);
+extern "C" int cbv2_final_mirror_used(void);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -172,12 +175,20 @@ bool take_mapped(int dev, size_t bytes, MappedBuf* out) {
   return true;
 }
 
-void give_mapped(int dev, MappedBuf b, hipStream_t st) {
+// Marks the buffer's last reader (an event after it on st) ...
+void mark_mapped(MappedBuf& b, hipStream_t st) {
   b.recorded = hipEventRecord(b.ev, st) == hipSuccess;
   if (!b.recorded) (void)hipStreamSynchronize(st);   // cannot mark the reader: wait for it instead
+}
+// ... and puts it back in the pool (reusable once that event completed).
+void pool_mapped(int dev, const MappedBuf& b) {
   MappedPool& P = mapped_pool();
   std::lock_guard<std::mutex> lk(P.mu);
   P.free_buf[dev].push_back(b);
+}
+void give_mapped(int dev, MappedBuf b, hipStream_t st) {
+  mark_mapped(b, st);
+  pool_mapped(dev, b);
 }
 
 // begin -> finish: the mapped buffer a one-shard begin took for its call
@@ -327,6 +338,10 @@ int rerank_call(cbv2_index* ix, cbv2_comm* c, Kind kd, const void* Q, int32_t B,
   return cbv2_rerank_ws(ix, Q, B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
 }
 
+// finish_host calls whose results came from the final select's host words
+// (cbv2_retrieve_pool_stats [2]: the tests check that path is the one taken)
+std::atomic<int64_t> g_final_words_calls{0};
+
 // Lab knob (cbv2_set_prearm, internal): 0 = the rerank is launched after the
 // fusion (no tagged candidates), 1 = pre-armed (default).
 int g_prearm = 1;
@@ -335,7 +350,7 @@ int g_prearm = 1;
 // search's last kernel writes them; written whole, in any order).  Never
 // waits forever: a GPU that never writes them (a fault) fails the call after
 // 2 s.
-int wait_words(const uint64_t* w, size_t n, uint32_t seq) {
+int wait_words(const uint64_t* w, size_t n, uint32_t seq, const char* what = "stage-2 results") {
   const volatile uint64_t* vw = w;
   const auto t0 = std::chrono::steady_clock::now();
   for (size_t i = 0; i < n;) {
@@ -344,7 +359,7 @@ int wait_words(const uint64_t* w, size_t n, uint32_t seq) {
       continue;
     }
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
-      return err(CBV2_EHIP, "stage-2 results did not arrive (2 s)");
+      return err(CBV2_EHIP, "%s did not arrive (2 s)", what);
   }
   return CBV2_OK;
 }
@@ -400,6 +415,7 @@ int cbv2_retrieve_pool_stats(int64_t* out, int32_t max) {
     for (int d = 0; d < kMaxDev; ++d) idle += (int64_t)P.free_buf[d].size();
     out[1] = idle;
   }
+  if (max > 2) out[2] = g_final_words_calls.load(std::memory_order_relaxed);
   return CBV2_OK;
 }
 
@@ -447,10 +463,18 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   return rc;
 }
 
-int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
-                         int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
-                         int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
-                         size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+}  // extern "C"
+
+namespace {
+// finish; host_s (nullable): the final top-k also to the host arrays host_s /
+// host_i / host_p ([B][final_k]) before the call returns -- read from the
+// final select's tagged words when it wrote them (one-shard calls), else
+// copied down and waited for
+int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq, int32_t k,
+                const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k, int32_t C,
+                int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage, size_t host_bytes,
+                float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream, float* host_s,
+                int32_t* host_i, int32_t* host_p) {
   mark(0);
   Kind kd;
   if (int rc = check_common(ix, &kd, c, Q, q_dtype, B, lq, k, kb)) return rc;
@@ -499,6 +523,13 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
   // and polls its candidates' words (the host writes them after the fusion),
   // so the host -> GPU hop after the fusion is a PCIe read, not a launch
   const bool prearm = mirrored && g_prearm && B <= kSpinMaxB && (kd.faithful || kd.dtype == CBV2_DTYPE_BF16);
+  // host results: the final select's words after the candidate words, when the
+  // buffer holds them (pool buffers are >= 64 KiB)
+  const size_t fin_words = (size_t)3 * B * final_k;
+  uint64_t* const fw = mapped && host_s && (size_t)(B * (size_t)(k + C)) * 8 + fin_words * 8 <= pd.mb.bytes
+                           ? cw + (size_t)B * C : nullptr;
+  uint64_t* const fwd = fw ? (uint64_t*)pd.mb.d + (size_t)B * (k + C) : nullptr;
+  bool fin_used = false;
   rc = CBV2_OK;
   if (!mirrored && hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
     rc = err(CBV2_EHIP, "stage-2 ids copy failed");
@@ -506,9 +537,12 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
   bool armed = false;
   if (!rc && prearm) {
     cbv2_set_cand_tagged(cwd, pd.seq);
+    if (fwd) cbv2_set_final_mirror(fwd, pd.seq, final_k);
     rc = rerank_call(ix, c, kd, Q, B, lq, k, L, L.cand, C, final_k, out_scores, out_ids, out_pos, st);
     armed = cbv2_cand_tagged_used() != 0;   // else it read L.cand (any ids are range-checked): rerun below
+    fin_used = armed && fwd && cbv2_final_mirror_used() != 0;
     cbv2_set_cand_tagged(nullptr, 0);
+    cbv2_set_final_mirror(nullptr, 0, 0);
   }
   // the one host round trip: the ColBERT (and merged BM25) top-k are here
   if (!rc) rc = mirrored && B <= kSpinMaxB ? wait_words(idw, (size_t)B * k, pd.seq) : wait_copy(st, B);
@@ -540,12 +574,62 @@ int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_
     } else if (hipMemcpyAsync(L.cand, H.cand, (size_t)B * C * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
       rc = err(CBV2_EHIP, "candidate upload failed");
     }
-    if (!rc) rc = rerank_call(ix, c, kd, Q, B, lq, k, L, cand_d, C, final_k, out_scores, out_ids, out_pos, st);
+    if (!rc) {
+      if (fwd) cbv2_set_final_mirror(fwd, pd.seq, final_k);
+      rc = rerank_call(ix, c, kd, Q, B, lq, k, L, cand_d, C, final_k, out_scores, out_ids, out_pos, st);
+      fin_used = fwd && cbv2_final_mirror_used() != 0;
+      cbv2_set_final_mirror(nullptr, 0, 0);
+    }
   }
   mark(4);
-  if (mapped) give_mapped(ds.dev, pd.mb, st);   // free again once the rerank that reads it ran
+  if (mapped) mark_mapped(pd.mb, st);   // free again once the rerank that reads it ran ...
+  if (!rc && host_s) {
+    const size_t n = (size_t)B * final_k;
+    if (fin_used) {   // the final select's words, row by row: [k] scores | [k] ids | [k] positions
+      rc = wait_words(fw, fin_words, pd.seq, "final results");
+      if (!rc) g_final_words_calls.fetch_add(1, std::memory_order_relaxed);
+      for (size_t i = 0; !rc && i < n; ++i) {
+        const uint64_t* row = fw + (i / final_k) * 3 * final_k;
+        const size_t r = i % final_k;
+        const uint32_t sb = (uint32_t)row[r];
+        std::memcpy(host_s + i, &sb, 4);
+        host_i[i] = (int32_t)(uint32_t)row[final_k + r];
+        host_p[i] = (int32_t)(uint32_t)row[2 * final_k + r];
+      }
+    } else if (hipMemcpyAsync(host_s, out_scores, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(host_i, out_ids, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(host_p, out_pos, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess) {
+      rc = err(CBV2_EHIP, "final results copy failed");
+    } else {
+      rc = wait_copy(st, B);
+    }
+  }
+  if (mapped) pool_mapped(ds.dev, pd.mb);   // ... and not before its host words were read
   mark(5);
   return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int cbv2_retrieve_finish(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                         int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
+                         int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
+                         size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream) {
+  return finish_impl(ix, c, Q, q_dtype, B, lq, k, lex_ids, lex_scores, kb, rrf_k, C, final_k, workspace,
+                     workspace_bytes, host_stage, host_bytes, out_scores, out_ids, out_pos, stream, nullptr, nullptr,
+                     nullptr);
+}
+
+int cbv2_retrieve_finish_host(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
+                              int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
+                              int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
+                              size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                              float* host_scores, int32_t* host_ids, int32_t* host_pos, void* stream) {
+  if (!host_scores || !host_ids || !host_pos) return err(CBV2_EINVAL, "null host outputs");
+  return finish_impl(ix, c, Q, q_dtype, B, lq, k, lex_ids, lex_scores, kb, rrf_k, C, final_k, workspace,
+                     workspace_bytes, host_stage, host_bytes, out_scores, out_ids, out_pos, stream, host_scores,
+                     host_ids, host_pos);
 }
 
 }  // extern "C"

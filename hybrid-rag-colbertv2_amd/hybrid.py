@@ -372,7 +372,11 @@ class OneTripRetriever:
     MXFP8 shards).  ``lexical`` per call: a callable
     returning (ids [B, kb] int32, scores [B, kb] float32) of this rank's BM25
     (host), or a host id array [B, kb] (one shard only), or None (no stage 1).
-    Returns device (scores [B, final_k], ids [B, final_k], positions [B, final_k])."""
+    Returns device (scores [B, final_k], ids [B, final_k], positions [B, final_k]);
+    with ``host=True`` the same three as numpy arrays, on the host when the
+    call returns (``cbv2_retrieve_finish_host``: one shard reads them from the
+    final select's host words, no copy or stream wait -- the reference's
+    ``retrieve`` returns host results, LRC:935)."""
 
     def __init__(self, searcher, colbert_k: int = 100, fused: int = 50, final_k: int = 10, rrf_k: int = 60,
                  lexical_k: int = 100):
@@ -398,6 +402,7 @@ class OneTripRetriever:
         self._sized = None        # (B, lq, kb) -> (ws pointer, bytes): the sizes of the last call
         self.record_marks = False   # latency lab: host timestamps of the last call in self.marks
         self.marks = None
+        self._dev_out = None        # host=True: (B, device scores, ids, positions), reused call to call
 
     def _buffers(self, B: int, lq: int, kb: int):
         if self._sized is not None and self._sized[0] == (B, lq, kb):
@@ -421,12 +426,13 @@ class OneTripRetriever:
         self._sized = ((B, lq, kb), out)
         return out
 
-    def __call__(self, Q: torch.Tensor, lexical=None):
+    def __call__(self, Q: torch.Tensor, lexical=None, host: bool = False):
         t_enter = time.monotonic_ns() if self.record_marks else 0
         L = _lib.lib()
         shape = Q.shape
         if len(shape) == 3 and shape[1] > _LQ_MAX and self.comm is None:
-            return self._stages(Q, lexical)     # long queries: the index sums blocks of <= 32 tokens
+            out = self._stages(Q, lexical)      # long queries: the index sums blocks of <= 32 tokens
+            return tuple(x.cpu().numpy() for x in out) if host else out
         if (len(shape) == 3 and 1 <= shape[1] <= _LQ_MAX and shape[2] == 128 and Q.dtype == self._qdtype()
                 and Q.is_cuda and Q.get_device() == self._dev_index
                 and Q.is_contiguous()):   # the index's query layout: no conversion
@@ -441,12 +447,12 @@ class OneTripRetriever:
                                          ws, wsb, st))
         t_begun = time.monotonic_ns() if self.record_marks else 0
         try:
-            return self._finish(L, Q, lexical, qptr, qdt, B, lq, kb_cap, ws, wsb, st, t_enter, t_prep, t_begun)
+            return self._finish(L, Q, lexical, qptr, qdt, B, lq, kb_cap, ws, wsb, st, t_enter, t_prep, t_begun, host)
         except BaseException:
             L.cbv2_retrieve_cancel(self.index._h, ws, st)   # begin's host buffer back to its pool
             raise
 
-    def _finish(self, L, Q, lexical, qptr, qdt, B, lq, kb_cap, ws, wsb, st, t_enter, t_prep, t_begun):
+    def _finish(self, L, Q, lexical, qptr, qdt, B, lq, kb_cap, ws, wsb, st, t_enter, t_prep, t_begun, host=False):
         lex_i = lex_s = None
         kb = 0
         if lexical is not None:       # stage 1 on the host while the GPU scans
@@ -461,20 +467,37 @@ class OneTripRetriever:
             kb = int(lex_i.shape[1])
             if lex_i.shape[0] != B or kb > kb_cap:
                 raise ValueError(f"stage-1 lists must be [B, <= {kb_cap}] (got {lex_i.shape})")
-        out_s = torch.empty((B, self.final_k), dtype=torch.float32, device=self.device)
-        out_i = torch.empty((B, self.final_k), dtype=torch.int32, device=self.device)
-        out_p = torch.empty((B, self.final_k), dtype=torch.int32, device=self.device)
-        _lib.check(L.cbv2_retrieve_finish(
-            self.index._h, self.comm, qptr, qdt, B, lq, self.k,
-            lex_i.ctypes.data if kb else None, lex_s.ctypes.data if (kb and lex_s is not None) else None, kb,
-            self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
-            out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), st))
+        lex_ip = lex_i.ctypes.data if kb else None
+        lex_sp = lex_s.ctypes.data if (kb and lex_s is not None) else None
+        if host:   # device outputs as call-to-call scratch; the results come back as host arrays
+            if self._dev_out is None or self._dev_out[0] != B:
+                self._dev_out = (B,) + tuple(torch.empty((B, self.final_k), dtype=dt, device=self.device)
+                                             for dt in (torch.float32, torch.int32, torch.int32))
+            _, out_s, out_i, out_p = self._dev_out
+            hs = np.empty((B, self.final_k), np.float32)
+            hi = np.empty((B, self.final_k), np.int32)
+            hp = np.empty((B, self.final_k), np.int32)
+            _lib.check(L.cbv2_retrieve_finish_host(
+                self.index._h, self.comm, qptr, qdt, B, lq, self.k, lex_ip, lex_sp, kb,
+                self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
+                out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), hs.ctypes.data, hi.ctypes.data, hp.ctypes.data,
+                st))
+            out = (hs, hi, hp)
+        else:
+            out_s = torch.empty((B, self.final_k), dtype=torch.float32, device=self.device)
+            out_i = torch.empty((B, self.final_k), dtype=torch.int32, device=self.device)
+            out_p = torch.empty((B, self.final_k), dtype=torch.int32, device=self.device)
+            _lib.check(L.cbv2_retrieve_finish(
+                self.index._h, self.comm, qptr, qdt, B, lq, self.k, lex_ip, lex_sp, kb,
+                self.rrf_k, self.C, self.final_k, ws, wsb, self._host.data_ptr(), self._host.numel(),
+                out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), st))
+            out = (out_s, out_i, out_p)
         if self.record_marks:
             c_marks = (ctypes.c_int64 * 6)()
             L.cbv2_retrieve_host_marks(c_marks, 6)
             self.marks = {"enter": t_enter, "prep": t_prep, "begun": t_begun, "finish": list(c_marks),
                           "exit": time.monotonic_ns()}
-        return out_s, out_i, out_p
+        return out
 
     def _qdtype(self):
         """The torch dtype a query of this index is passed as without conversion

@@ -167,6 +167,11 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        every 64-doc block, and ONE select launch reads only
  *                        the blocks that can reach the top-k (0: the sampled
  *                        filter + select).  Identical results.
+ *  CBV2_OPT_P1_COLLECT_FUSED 1: the two-pass band of cbv2_search_f32 on at
+ *                        most 8 queries runs its phase 1 (the bf16 top-k's
+ *                        faithful scores) and the band collect in ONE launch
+ *                        (the collect's loads overlap phase 1; 0: two
+ *                        launches).  Identical results.
  * cbv2_index_last_scan_plan: the work split of this handle's latest scan
  * launch: {workgroups, static chunk docs, static docs, dynamic tail 0/1}.
  * Thread safety: one handle may be used from several host threads and
@@ -183,6 +188,7 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_BAND_BLOCK_SKIP 9
 #define CBV2_OPT_RESCORE_GRID 10
 #define CBV2_OPT_DENSE_DOCS 11
+#define CBV2_OPT_P1_COLLECT_FUSED 12
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the
@@ -572,6 +578,13 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    (the search's final select writes the ids into it, the fused candidates
  *    go into it and the rerank reads them in place) and returns it at finish,
  *    reusable once that rerank has run.
+ * cbv2_retrieve_finish_host: finish, and the final top-k also in the HOST
+ *    arrays host_scores / host_ids / host_pos ([B][final_k], any host memory)
+ *    when it returns (the reference's retrieve returns host results,
+ *    LRC:935).  One shard: the final select writes them into the call's
+ *    mapped buffer as tagged words and the host polls them (no D2H copy, no
+ *    stream wait); otherwise they are copied down and waited for.  The
+ *    device outputs are written as by finish.
  * cbv2_retrieve_cancel: a begin that will not be finished (the caller's
  *    stage 1 failed): returns its host buffer to the pool (no-op otherwise).
  * cbv2_retrieve_host_marks (diagnostic): host timestamps (steady_clock ns) of
@@ -579,7 +592,8 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    rerank enqueued, exit (max entries written, up to 6).
  * cbv2_retrieve_pool_stats (diagnostic): [0] mapped buffers created in this
  *    process, [1] buffers idle in the pools (at most the number of calls that
- *    ever ran at once).
+ *    ever ran at once), [2] finish_host calls whose results were read from the
+ *    final select's host words.
  * cbv2_index_kind: the index's dtype (CBV2_DTYPE_*) and whether a residual is
  *    attached (fp32-faithful, 1) or not (0).                                */
 #define CBV2_RETRIEVE_BAND_CAP 16384
@@ -596,6 +610,12 @@ int cbv2_retrieve_finish(cbv2_index* index, cbv2_comm* comm, const void* Q, int3
                          int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb, int32_t rrf_k,
                          int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes, void* host_stage,
                          size_t host_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
+int cbv2_retrieve_finish_host(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t B,
+                              int32_t lq, int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb,
+                              int32_t rrf_k, int32_t C, int32_t final_k, void* workspace, size_t workspace_bytes,
+                              void* host_stage, size_t host_bytes, float* out_scores, int32_t* out_ids,
+                              int32_t* out_pos, float* host_scores, int32_t* host_ids, int32_t* host_pos,
+                              void* stream);
 
 #ifdef __cplusplus
 }

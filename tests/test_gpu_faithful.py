@@ -402,6 +402,27 @@ def test_band_block_skip_equals_full_row(dev, bmax_corpus, B):
             assert torch.equal(a, b), (key, name)
 
 
+@pytest.mark.parametrize("B", [1, 3, 8])
+def test_phase1_collect_fused_equals_two_launches(dev, bmax_corpus, B):
+    """CBV2_OPT_P1_COLLECT_FUSED: phase 1 (the bf16 top-k's faithful scores)
+    and the band collect in one launch, the collect's workgroups waiting in
+    the launch for their row's phase 1 -- top-k, scores and band sizes equal
+    the two launches' bit for bit, for k = 40 / 100 / 400 (threshold over
+    superblock and block keys)."""
+    ix, Q = bmax_corpus
+    Qb = Q[:B].contiguous()
+    got = {}
+    for k in (40, 100, 400):
+        for fused in (1, 0):
+            ix.set_option(_lib.OPT_P1_COLLECT_FUSED, fused)
+            s, i = ix.search(Qb, k)
+            got[(k, fused)] = (s.clone(), i.clone(), ix.last_band.clone())
+        assert (got[(k, 0)][2] > k).all()          # a real band beyond the top-k
+        for a, b, name in zip(got[(k, 1)], got[(k, 0)], ("s", "i", "band")):
+            assert torch.equal(a, b), (k, name)
+    ix.set_option(_lib.OPT_P1_COLLECT_FUSED, 1)
+
+
 @pytest.mark.parametrize("B", [1, 12])
 def test_rescore_grid_equals_default(dev, B):
     """CBV2_OPT_RESCORE_GRID: fewer workgroups per row grid-stride over the

@@ -6,14 +6,18 @@ Done = scores, ids and positions equal bit for bit, for bf16, MXFP8 and
 fp32-faithful shards, B = 1 / 5 / 40, with a BM25 callable, a host id array
 and no stage 1; and at G = 2 / 4 / 8 through the test-only loopback
 communicator, bf16, MXFP8 and fp32-faithful shards (every rank equals the
-unsharded composed path)."""
+unsharded composed path).  The host results (``host=True``,
+cbv2_retrieve_finish_host) equal the device ones, and one-shard bf16 /
+faithful calls read them from the final select's host words (counted by
+cbv2_retrieve_pool_stats [2])."""
+import ctypes
 import threading
 
 import numpy as np
 import pytest
 import torch
 
-from hybrid_rag_colbertv2_amd import synth
+from hybrid_rag_colbertv2_amd import _lib, synth
 from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
 from hybrid_rag_colbertv2_amd.distributed import NativeExchange, loopback_comms
 from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, rrf_fuse
@@ -42,6 +46,12 @@ def _composed(index, Q, lex_ids):
     return index.rerank(Q, torch.from_numpy(cand).to(index.device), KF)
 
 
+def _final_words_calls():
+    st = (ctypes.c_int64 * 3)()
+    _lib.lib().cbv2_retrieve_pool_stats(st, 3)
+    return int(st[2])
+
+
 @pytest.mark.parametrize("kind", ["bf16", "fp8", "fp32"])
 @pytest.mark.parametrize("B", [1, 5, 40])
 def test_one_trip_equals_composed(dev, kind, B):
@@ -63,6 +73,12 @@ def test_one_trip_equals_composed(dev, kind, B):
         want = [x.cpu() for x in _composed(ix, Q, lex_ids)]
         for g, w, name in zip(got, want, ("scores", "ids", "positions")):
             assert torch.equal(g, w), f"{kind} B={B}: {name} differ from the composed stages"
+        n0 = _final_words_calls()
+        goth = one(Q, lexical, host=True)
+        for g, w, name in zip(goth, want, ("scores", "ids", "positions")):
+            assert isinstance(g, np.ndarray) and np.array_equal(g, w.numpy()), f"{kind} B={B}: host {name} differ"
+        if kind == "fp32" or (kind == "bf16" and B <= 32):   # from the final select's host words
+            assert _final_words_calls() == n0 + 1, f"{kind} B={B}: host results were copied, not mirrored"
     for b in range(B):                     # the planted docs win stage 3
         assert set(got[1][b].tolist()) == set(planted[b].tolist())
 
@@ -130,12 +146,15 @@ def test_one_trip_sharded_loopback_equals_unsharded(dev, G, B, kind, kb_ret):
     ones = [OneTripRetriever(NativeExchange(shards[r], comm=comms[r]), colbert_k=K, fused=C, final_k=KF)
             for r in range(G)]
     outs = _run_ranks(G, lambda r: [x.cpu() for x in ones[r](Q, lambda: lex[r].search(qt, qo, kb_ret))])
+    hosts = _run_ranks(G, lambda r: ones[r](Q, lambda: lex[r].search(qt, qo, kb_ret), host=True))
     torch.cuda.synchronize()
     bi, _ = lex_full.search(qt, qo, kb_ret)
     want = [x.cpu() for x in _composed(full, Q, bi)]
     for r, got in enumerate(outs):
         for g, w, name in zip(got, want, ("scores", "ids", "positions")):
             assert torch.equal(g, w), f"rank {r}: {name} differ from the unsharded composed stages"
+        for g, w, name in zip(hosts[r], want, ("scores", "ids", "positions")):
+            assert np.array_equal(g, w.numpy()), f"rank {r}: host {name} differ"
     for b in range(B):
         assert set(outs[0][1][b].tolist()) == set(planted[b].tolist())
     del ones

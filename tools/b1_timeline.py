@@ -64,10 +64,13 @@ def run(a):
             torch.cuda.synchronize()
             time.sleep(0.002)          # the GPU idles between queries, as in the bench's latency loop
             t = time.perf_counter()
-            one(Q1, bm_one)
+            one(Q1, bm_one, host=bool(a.host))
+            if not a.host:
+                torch.cuda.synchronize()
+            t1 = time.perf_counter()
             torch.cuda.synchronize()
             if it >= 5:
-                lat[name].append((time.perf_counter() - t) * 1e3)
+                lat[name].append((t1 - t) * 1e3)
                 if a.marks:
                     marks.append(dict(one.marks, leg=name, it=it, synced=time.monotonic_ns()))
     if a.marks:
@@ -154,12 +157,50 @@ def parse(d, scan_key, marks_path=None):
     for kind, per in per_kind.items():
         print(f"[{kind}]")
         _fold(per, scan_key)
+    af = glob.glob(os.path.join(d, "**", "*hip_api_trace.csv"), recursive=True)
+    if af and marks:
+        _api(af, marks, groups, scan_key)
     for leg, rows in host.items():
         print(f"[host marks, {leg}: {len(rows)} calls; medians in us]")
         for key in rows[0]:
             vals = [r[key] for r in rows if r[key] is not None]
             if vals:
                 print(f"  {key:45s} {statistics.median(vals) / 1e3:9.1f}")
+
+
+def _api(files, marks, groups, scan_key):
+    """HIP runtime calls of each timed call (a --hip-runtime-trace run), from
+    the Python entry to the call's exit: start offset from the entry and
+    duration, medians over the calls of the modal call sequence, with the
+    iteration's first kernel start and the scan's end on the same axis."""
+    api = []
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            api.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Function") or r.get("Operation", "?")))
+    api.sort()
+    per_leg = {}
+    for g in groups:
+        if not any(scan_key in e[2] for e in g):
+            continue
+        t0 = g[0][0]
+        near = [m for m in marks if 0 <= t0 - m["enter"] < 1_000_000]
+        if not near:
+            continue
+        m = max(near, key=lambda m: m["enter"])
+        calls = [(a - m["enter"], b - a, nm) for (a, b, nm) in api if m["enter"] <= a <= m["exit"]]
+        scan_end = max(e[1] for e in g if scan_key in e[2])
+        per_leg.setdefault(m["leg"], []).append((calls, t0 - m["enter"], scan_end - m["enter"], m["exit"] - m["enter"]))
+    for leg, per in per_leg.items():
+        L = statistics.mode(len(c) for c, *_ in per)
+        same = [p for p in per if len(p[0]) == L]
+        print(f"[HIP calls, {leg}: {len(same)} of {len(per)} calls with the modal {L}; us from the Python entry]")
+        for k in range(L):
+            nm = same[0][0][k][2]
+            st = statistics.median(p[0][k][0] for p in same) / 1e3
+            du = statistics.median(p[0][k][1] for p in same) / 1e3
+            print(f"  {st:9.1f} +{du:7.1f}  {nm}")
+        for lab, j in (("first kernel start", 1), ("scan end", 2), ("python exit", 3)):
+            print(f"  {statistics.median(p[j] for p in same) / 1e3:9.1f}           <{lab}>")
 
 
 def _fold(per, scan_key):
@@ -191,6 +232,7 @@ if __name__ == "__main__":
     ap.add_argument("--parse", default=None, help="a rocprofv3 output directory to fold")
     ap.add_argument("--scan", default="maxsim_scan", help="substring naming the scan kernel")
     ap.add_argument("--marks", default=None, help="host timestamps file (run: written; parse: read)")
+    ap.add_argument("--host", type=int, default=1, help="1: the call returns host results (cbv2_retrieve_finish_host)")
     a = ap.parse_args()
     if a.parse:
         parse(a.parse, a.scan, a.marks)
