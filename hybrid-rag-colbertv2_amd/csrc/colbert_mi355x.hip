@@ -2673,14 +2673,19 @@ __device__ void topk_exact_row(const float* __restrict__ x, int64_t n, int kk, u
 // The words are 8 bytes, {id, seq} (seq in the high half), LL-style: a word
 // is whole or absent, so the host polling them needs no ordering between the
 // stores -- every word of the call carries the call's seq once written.
+// soff (words, > 0): the score of word i also at w[soff + i] ({score bits,
+// seq}; the latency path's host rerank takes stage 2's scores from there).
 struct Mirror {
   uint64_t* w = nullptr;
   uint32_t seq = 0;
-  __device__ __forceinline__ void put(size_t i, int32_t id) const {
-    __hip_atomic_store(w + i, ((uint64_t)seq << 32) | (uint32_t)id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  int64_t soff = 0;
+  __device__ __forceinline__ void put(size_t i, int32_t id, float s) const {
+    const uint64_t t = (uint64_t)seq << 32;
+    __hip_atomic_store(w + i, t | (uint32_t)id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (soff > 0) __hip_atomic_store(w + soff + i, t | __float_as_uint(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __device__ __host__ __forceinline__ Mirror row(size_t b, int k) const {
-    return Mirror{w ? w + b * (size_t)k : nullptr, seq};
+    return Mirror{w ? w + b * (size_t)k : nullptr, seq, soff};
   }
 };
 
@@ -2726,6 +2731,36 @@ __device__ __forceinline__ int32_t wait_tagged(const uint64_t* w, uint32_t seq) 
     __builtin_amdgcn_s_sleep(2);
   }
 }
+// The latency path's final top-k picked by the HOST (retrieve.cpp's host
+// rerank: every fused candidate's score is already known -- stage 2's own, or
+// stage 1's prescore -- so the host selects it): this one-workgroup kernel is
+// launched before the host has the result, polls its tagged words in the
+// call's mapped buffer (FinalMirror's layout: per row [k] score, [k] id, [k]
+// position words) and writes the device outputs.  A word that never comes
+// (kCandWaitTicks) is written -inf / -1.
+__global__ __launch_bounds__(256) void host_result_kernel(const uint64_t* __restrict__ w, uint32_t seq, int B, int k,
+                                                          float* __restrict__ out_s, int32_t* __restrict__ out_i,
+                                                          int32_t* __restrict__ out_p) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = threadIdx.x; i < 3 * B * k; i += blockDim.x) {
+    const int b = i / (3 * k), r = i - b * 3 * k;
+    uint64_t v;
+    bool ok;
+    for (;;) {
+      v = __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok = (uint32_t)(v >> 32) == seq;
+      if (ok || __builtin_amdgcn_s_memrealtime() - t0 > kCandWaitTicks) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    const uint32_t x = (uint32_t)v;
+    if (r < k)
+      out_s[(size_t)b * k + r] = ok ? __uint_as_float(x) : neg_inf();
+    else if (r < 2 * k)
+      out_i[(size_t)b * k + r - k] = ok ? (int32_t)x : -1;
+    else
+      out_p[(size_t)b * k + r - 2 * k] = ok ? (int32_t)x : -1;
+  }
+}
 __device__ __forceinline__ int32_t read_tagged(const uint64_t* w) {
   return (int32_t)(uint32_t)__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2747,7 +2782,7 @@ __device__ void sort_and_write(uint64_t* sel, int cnt, int k, int64_t id_base, f
     }
     out_s[j] = s;
     out_i[j] = id;
-    if (mirror.w != nullptr) mirror.put(j, id);
+    if (mirror.w != nullptr) mirror.put(j, id, s);
   }
 }
 
@@ -2755,7 +2790,8 @@ __global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __re
                                                                int64_t ld, int k, int64_t id_base,
                                                                float* __restrict__ out_s,
                                                                int32_t* __restrict__ out_i,
-                                                               const int32_t* __restrict__ only_neg = nullptr) {
+                                                               const int32_t* __restrict__ only_neg = nullptr,
+                                                               Mirror mirror = Mirror()) {
   __shared__ uint32_t hist[2048];
   __shared__ uint64_t sel[kTopkMax];
   __shared__ uint32_t s_bin, s_above, s_bincount, s_cnt;
@@ -2763,7 +2799,8 @@ __global__ __launch_bounds__(kTkThreads) void topk_rows_kernel(const float* __re
   const float* x = scores + (size_t)blockIdx.x * ld;
   const int kk = (int)((int64_t)k < n ? k : n);
   topk_exact_row(x, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
-  sort_and_write(sel, kk, k, id_base, out_s + (size_t)blockIdx.x * k, out_i + (size_t)blockIdx.x * k);
+  sort_and_write(sel, kk, k, id_base, out_s + (size_t)blockIdx.x * k, out_i + (size_t)blockIdx.x * k,
+                 mirror.row(blockIdx.x, k));
 }
 
 // ---------------------------------------------------------------------------
@@ -3291,12 +3328,12 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
     if (i < m && p == 0 && r < k) {
       os[r] = u2f((uint32_t)(key >> 32));
       oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
-      if (mirror.w != nullptr) mirror.put(r, oi[r]);
+      if (mirror.w != nullptr) mirror.put(r, oi[r], os[r]);
     }
     for (int j = m + tid; j < k; j += nth) {
       os[j] = neg_inf();
       oi[j] = -1;
-      if (mirror.w != nullptr) mirror.put(j, -1);
+      if (mirror.w != nullptr) mirror.put(j, -1, neg_inf());
     }
   } else {
     sort_and_write(sel, m, k, id_base, os, oi, mirror);
@@ -3679,7 +3716,7 @@ __global__ __launch_bounds__(kRrWaves * 64) void rerank_raw_kernel(
 __global__ __launch_bounds__(256, 2) void rerank_split_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n, int64_t id_base,
     const uint16_t* __restrict__ Q, int lq, const int32_t* __restrict__ cand, int C, float* __restrict__ raw, int ld,
-    TaggedCand tc = TaggedCand()) {
+    TaggedCand tc = TaggedCand(), Mirror raw_words = Mirror()) {
   __shared__ float s_m[4][32];
   __shared__ int32_t s_cid;
   const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
@@ -3695,7 +3732,10 @@ __global__ __launch_bounds__(256, 2) void rerank_split_kernel(
   }
   const int64_t loc = (int64_t)id - id_base;
   if (id < 0 || loc < 0 || loc >= n) {   // block-uniform
-    if (threadIdx.x == 0) raw[(size_t)b * C + c] = neg_inf();
+    if (threadIdx.x == 0) {
+      raw[(size_t)b * C + c] = neg_inf();
+      if (raw_words.w != nullptr) raw_words.put((size_t)b * C + c, (int32_t)__float_as_uint(neg_inf()), 0.0f);
+    }
     return;
   }
   bf16x8 qf[1][2][4];
@@ -3729,7 +3769,10 @@ __global__ __launch_bounds__(256, 2) void rerank_split_kernel(
     const float m0 = fmaxf(fmaxf(s_m[0][c16], s_m[1][c16]), fmaxf(s_m[2][c16], s_m[3][c16]));
     const float m1 = fmaxf(fmaxf(s_m[0][16 + c16], s_m[1][16 + c16]), fmaxf(s_m[2][16 + c16], s_m[3][16 + c16]));
     const float v = dpp_row_sum16((c16 < lq ? m0 : 0.0f) + (16 + c16 < lq ? m1 : 0.0f));
-    if (lane == 0) raw[(size_t)b * C + c] = v;
+    if (lane == 0) {
+      raw[(size_t)b * C + c] = v;
+      if (raw_words.w != nullptr) raw_words.put((size_t)b * C + c, (int32_t)__float_as_uint(v), 0.0f);
+    }
   }
 }
 
@@ -3828,6 +3871,8 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 // and -- ctr, the search's scan -- the scan's task-counter block: launches
 // fewer than separate memsets.
 constexpr int kArriveSlotsK = 4;   // slots of the faithful workspace's arrival counters (kArriveSlots)
+constexpr int kArrPhase1K = 3;     // (kArrPhase1) the phase-1 slot: done1's replicas, then at
+constexpr int kSplitReady = 256;   // int 256 of a row's slot the split's ready flag
 __global__ __launch_bounds__(512) void split_query_kernel(const float* __restrict__ Q, int lq,
                                                           uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
                                                           float E, float M, float* __restrict__ beta,
@@ -3835,7 +3880,8 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
                                                           uint32_t* __restrict__ lbu = nullptr,
                                                           int32_t* __restrict__ done = nullptr, int count0 = 0,
                                                           int32_t* __restrict__ arrive = nullptr, int narrive = 0,
-                                                          int* __restrict__ ctr = nullptr, int nctr = 0) {
+                                                          int* __restrict__ ctr = nullptr, int nctr = 0,
+                                                          uint32_t ready_seq = 0) {
   // one 16-lane group per query token (lq <= 32: one pass, no loop -- the B=1
   // latency path waits on this launch); the per-token bound terms are summed
   // in the order of the round-3 one-wave kernel (4 strided partial sums, then
@@ -3872,6 +3918,20 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
   }
   if (ctr != nullptr && b == 0)   // the scan's task counters (the scan that follows skips its memset)
     for (int i = tid; i < nctr; i += blockDim.x) ctr[i] = 0;
+  if (ready_seq != 0 && arrive != nullptr) {
+    // the row's split is published (kSplitReady of its phase-1 arrival slot):
+    // plain stores -> agent release -> relaxed flag (MI355X_MICROARCH.md, the
+    // handoff-flag row; the vmcnt(0) after the fence: its compiler-hazard fix),
+    // read by the latency path's stage-1 prescore on another stream
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int per = narrive / kArriveSlotsK;
+      __hip_atomic_store(arrive + ((size_t)kArrPhase1K * gridDim.x + b) * per + kSplitReady, (int32_t)ready_seq,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // One row tile, faithful product: acc = init + lo.qhi + hi.qlo + hi.qhi.
@@ -4068,6 +4128,10 @@ struct RowSelect {
   int32_t* status = nullptr;     // kSelBand: the band size (the fallback writes -1 for overflowed rows)
   Mirror ids_mirror;             // kSelBand: [B][k] host mirror of the final ids (w nullable)
   FinalMirror fin;               // kSelCand: the host words of the call's final result (w nullable)
+  const int32_t* ready = nullptr;   // (nullable) row b's ready flag at ready[b * kArriveInts]: wait for
+  uint32_t ready_seq = 0;           //   it to read ready_seq before reading the split queries
+  Mirror raw;                    // kSelNone (w nullable): every pair's score also as the host word
+                                 // raw.w[b * ld_c + c] ({score bits, seq}; the latency path's stage-1 prescore)
   uint64_t* stamps = nullptr;    // lab builds only (LAB_STAMPS): [16 + 2x] / [17 + 2x] workgroup x's start /
                                  // end of its pairs, [6] the row select's start, [4] its end
 };
@@ -4157,13 +4221,13 @@ __device__ void select_band_row(const float* F, const int32_t* cand, int cnt, in
     if (r < k) {
       os[r] = u2f((uint32_t)(key >> 32));
       oi[r] = (int32_t)(id_base + (int64_t)(~(uint32_t)key));
-      if (mirror.w != nullptr) mirror.put(r, oi[r]);
+      if (mirror.w != nullptr) mirror.put(r, oi[r], os[r]);
     }
   }
   for (int j = m + tid; j < k; j += nth) {
     os[j] = neg_inf();
     oi[j] = -1;
-    if (mirror.w != nullptr) mirror.put(j, -1);
+    if (mirror.w != nullptr) mirror.put(j, -1, neg_inf());
   }
 }
 
@@ -4188,6 +4252,18 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
   const int b = blockIdx.y;
   if (rs.stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
     rs.stamps[16 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  if (rs.ready != nullptr) {   // another stream's split: one relaxed poll, one agent acquire (handoff-flag row)
+    if (threadIdx.x == 0) {
+      const int32_t* f = rs.ready + (size_t)b * kArriveInts;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((uint32_t)__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != rs.ready_seq &&
+             __builtin_amdgcn_s_memrealtime() - t0 < kCandWaitTicks)
+        __builtin_amdgcn_s_sleep(4);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
   if (only_neg != nullptr && only_neg[b] >= 0) return;  // block-uniform
   int64_t lim = limit;
   if (count != nullptr) {
@@ -4251,6 +4327,7 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
           st_sc1(out + (size_t)b * ld_out + c, v);   // handed to the row's last workgroup
         else
           out[(size_t)b * ld_out + c] = v;
+        if (rs.raw.w != nullptr) rs.raw.put((size_t)b * ld_c + c, (int32_t)__float_as_uint(v), 0.0f);
         if (lb_min != nullptr) atomicMin(lb_min + b, f2u(v));
       }
     }
@@ -5594,6 +5671,17 @@ thread_local bool g_cand_tagged_used = false;
 // g_final_mirror_used (else the caller copies the result down).
 thread_local FinalMirror g_final_mirror;
 thread_local bool g_final_mirror_used = false;
+// ... and the raw scores of a k = 0 rerank as host words (cbv2_set_raw_mirror,
+// around the latency path's stage-1 prescore): a rerank that writes them sets
+// g_raw_mirror_used.
+thread_local Mirror g_raw_mirror;
+thread_local bool g_raw_mirror_used = false;
+// The latency path's split-ready flag (cbv2_set_split_ready around begin's
+// search: its query split publishes this seq when done) and the stage-1
+// prescore that waits for it on another stream (cbv2_set_prescore_ready).
+thread_local uint32_t g_split_ready_seq = 0;
+thread_local uint32_t g_prescore_ready_seq = 0;
+thread_local const int32_t* g_prescore_ready = nullptr;
 // Lab builds (-DCBV2_LAB_STAMPS, tools/chain_lab.py): per-launch phase stamps
 // of the latency path's kernels, kind k at g_lab_stamps + k * kLabStride --
 // 0 block-max select, 1 phase-1 rescoring, 2 band collect, 3 band rescoring +
@@ -6341,8 +6429,10 @@ int topk_impl(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   if (k > kTopkMax) return topk_multi(scores, B, n, ld, k, id_base, nullptr, 0, out_s, out_i, nullptr, st);
   const size_t need = topk_ws_bytes(B, n);
   if (need == 0 || ws == nullptr || ws_bytes < need || B > 65535) {  // grid.y of the filter launch
+    const Mirror mirror = g_ids_mirror;   // the search's final ids (the latency path's host mirror)
+    if (mirror.w != nullptr) g_ids_mirror_used = true;
     hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)B), dim3(kTkThreads), 0, st, scores, n, ld, k, id_base,
-                       out_s, out_i, nullptr);
+                       out_s, out_i, nullptr, mirror);
     return launch_check("topk_rows_kernel");
   }
   uint64_t* cand = (uint64_t*)ws;
@@ -6393,7 +6483,7 @@ struct F32Ws {
 // slot j at (j * B + b) * kArriveInts): the launches whose last workgroup per
 // row runs the row's selection (row_last_arrival).
 constexpr int kArriveSlots = kArriveSlotsK;
-constexpr int kArrBmax = 0, kArrBand = 1, kArrRerank = 2, kArrPhase1 = 3;
+constexpr int kArrBmax = 0, kArrBand = 1, kArrRerank = 2, kArrPhase1 = kArrPhase1K;
 inline int32_t* arrive_row0(const F32Ws& w, int slot, int B) { return w.arrive + (size_t)slot * B * kArriveInts; }
 
 // op SCORE: split queries; RERANK: + F [B][C]; SEARCH: + band [B][cap] + scan.
@@ -6490,7 +6580,8 @@ int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipSt
   note_split(ix, Q, B, lq, w->qhi);
   hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(512), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
                      ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0,
-                     w->arrive, kArriveSlots * kArriveInts, zero_ctr ? w->ctr : nullptr, zero_ctr ? kRingInts : 0);
+                     w->arrive, kArriveSlots * kArriveInts, zero_ctr ? w->ctr : nullptr, zero_ctr ? kRingInts : 0,
+                     w->arrive != nullptr ? g_split_ready_seq : 0u);
   return launch_check("split_query_kernel");
 }
 
@@ -6898,8 +6989,10 @@ static int rerank_impl(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, con
     if (!f8 && ix->rescore_split) {   // one candidate per workgroup, its rows over the 4 waves
       tc = g_cand_tagged;             // the latency path's pre-armed rerank (cand unused then)
       if (tc.w != nullptr) g_cand_tagged_used = true;
+      const Mirror rw = k == 0 ? g_raw_mirror : Mirror();
+      if (rw.w != nullptr) g_raw_mirror_used = true;
       hipLaunchKernelGGL(rerank_split_kernel, dim3((unsigned)C, (unsigned)B), dim3(256), 0, st, ix->tokens,
-                         ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, raw, (int)ix->ld, tc);
+                         ix->doclens, ix->n, ix->id_base, (const uint16_t*)Q, lq, cand, C, raw, (int)ix->ld, tc, rw);
       if ((rc = launch_check("rerank_split_kernel"))) return rc;
     } else if (f8)
       hipLaunchKernelGGL(rerank_raw_kernel<true>, grid, dim3(kRrWaves * 64), 0, st, ix->tokens, ix->scales,
@@ -7253,7 +7346,18 @@ int rerank_f32_split(cbv2_index* ix, F32Ws& w, int32_t B, int32_t lq, const int3
     return launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
                           nullptr, nullptr, rs, tc);
   }
-  if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st))) return rc;
+  RowSelect rw;
+  if (k == 0 && g_raw_mirror.w != nullptr) {   // the raw scores also as host words
+    rw.raw = g_raw_mirror;
+    g_raw_mirror_used = true;
+  }
+  if (k == 0 && g_prescore_ready != nullptr) {   // the split it reads is another stream's
+    rw.ready = g_prescore_ready;
+    rw.ready_seq = g_prescore_ready_seq;
+  }
+  if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
+                           nullptr, nullptr, rw)))
+    return rc;
   if (k == 0) return CBV2_OK;
   if (C > kSmallMax) return topk_multi(raw, B, C, C, k, 0, cand, C, out_scores, out_ids, out_pos, st);
   const FinalMirror fin = g_final_mirror.k == k ? g_final_mirror : FinalMirror();
@@ -7377,6 +7481,11 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
     w.qhi = sw.qhi;
     w.qlo = sw.qlo;
     arrive = arrive_row0(sw, kArrRerank, B);
+    if (g_prescore_ready_seq != 0) {   // on another stream than the split: wait for its flag
+      g_prescore_ready = arrive_row0(sw, kArrPhase1, B) + kSplitReady;
+    }
+  } else if (g_prescore_ready_seq != 0) {
+    return fail(CBV2_ESTATE, "stage-1 prescore: the search's query split is not in the workspace");
   } else {
     CBV2_REQUIRE(Q != nullptr, "null queries");
     int rc = split_queries(ix, Q, B, lq, &w, st);
@@ -7389,8 +7498,8 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
 // Internal (retrieve.cpp): the host mirror of the next search's final ids on
 // this thread (nullptr: none); cbv2_ids_mirror_used: whether the search just
 // issued writes it (then it holds every row's ids once the stream gets there).
-void cbv2_set_ids_mirror(void* p, uint32_t seq) {
-  g_ids_mirror = Mirror{(uint64_t*)p, seq};
+void cbv2_set_ids_mirror(void* p, uint32_t seq, int64_t score_off) {
+  g_ids_mirror = Mirror{(uint64_t*)p, seq, p != nullptr ? score_off : 0};
   g_ids_mirror_used = false;
 }
 int cbv2_ids_mirror_used(void) { return g_ids_mirror_used ? 1 : 0; }
@@ -7404,6 +7513,22 @@ void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k) {
   g_final_mirror_used = false;
 }
 int cbv2_final_mirror_used(void) { return g_final_mirror_used ? 1 : 0; }
+int cbv2_host_result_copy(const void* words, uint32_t seq, int32_t B, int32_t k, float* out_s, int32_t* out_i,
+                          int32_t* out_p, void* stream) {
+  hipLaunchKernelGGL(host_result_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (const uint64_t*)words, seq, B, k,
+                     out_s, out_i, out_p);
+  return launch_check("host_result_kernel");
+}
+void cbv2_set_split_ready(uint32_t seq) { g_split_ready_seq = seq; }
+void cbv2_set_prescore_ready(uint32_t seq) {
+  g_prescore_ready_seq = seq;
+  g_prescore_ready = nullptr;
+}
+void cbv2_set_raw_mirror(void* p, uint32_t seq) {
+  g_raw_mirror = Mirror{(uint64_t*)p, seq, 0};
+  g_raw_mirror_used = false;
+}
+int cbv2_raw_mirror_used(void) { return g_raw_mirror_used ? 1 : 0; }
 #ifdef CBV2_LAB_STAMPS
 void cbv2_lab_set_stamps(void* p) { g_lab_stamps = (uint64_t*)p; }
 #endif

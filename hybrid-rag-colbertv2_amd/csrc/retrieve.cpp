@@ -18,8 +18,10 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <climits>
 #include <cstring>
 #include <algorithm>
+#include <limits>
 #include <atomic>
 #include <mutex>
 #include <thread>
@@ -33,12 +35,18 @@ extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_w
                                             size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
                                             const float* Q, void* stream);
 extern "C" int cbv2_index_device(const cbv2_index* ix);
-extern "C" void cbv2_set_ids_mirror(void* p, uint32_t seq);
+extern "C" void cbv2_set_ids_mirror(void* p, uint32_t seq, int64_t score_off);
 extern "C" int cbv2_ids_mirror_used(void);
 extern "C" void cbv2_set_cand_tagged(const void* p, uint32_t seq);
 extern "C" int cbv2_cand_tagged_used(void);
 extern "C" void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k);
 extern "C" int cbv2_final_mirror_used(void);
+extern "C" void cbv2_set_raw_mirror(void* p, uint32_t seq);
+extern "C" void cbv2_set_split_ready(uint32_t seq);
+extern "C" void cbv2_set_prescore_ready(uint32_t seq);
+extern "C" int cbv2_raw_mirror_used(void);
+extern "C" int cbv2_host_result_copy(const void* words, uint32_t seq, int32_t B, int32_t k, float* out_s, int32_t* out_i,
+                                     int32_t* out_p, void* stream);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -198,7 +206,27 @@ struct Pending {
   MappedBuf mb;
   bool ids_mirrored = false;
   uint32_t seq = 0;
+  uint32_t ready_seq = 0;   // the faithful search's split-ready flag value (0: none)
 };
+
+// Process-wide call tags of the split-ready flags (never 0): the flag lives in
+// the caller's workspace, which calls through different mapped buffers share.
+std::atomic<uint32_t> g_ready_seq{0};
+uint32_t next_ready_seq() {
+  uint32_t v = g_ready_seq.fetch_add(1, std::memory_order_relaxed) + 1;
+  if (v == 0) v = g_ready_seq.fetch_add(1, std::memory_order_relaxed) + 1;
+  return v;
+}
+
+// The host rerank's second stream (per host thread and device; never
+// destroyed, like the mapped buffers): the stage-1 prescore runs on it
+// concurrently with stage 2's scan instead of after it.
+hipStream_t side_stream(int dev) {
+  thread_local hipStream_t s[kMaxDev] = {};
+  if (dev < 0 || dev >= kMaxDev) return nullptr;
+  if (s[dev] == nullptr && hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking) != hipSuccess) s[dev] = nullptr;
+  return s[dev];
+}
 std::mutex g_pending_mu;
 std::vector<std::pair<const void*, Pending>> g_pending;
 
@@ -280,10 +308,10 @@ Layout layout(const cbv2_index* ix, const cbv2_comm* c, Kind kd, int32_t B, int3
   if (c)        // cbv2_rerank_sharded: raw [B][C] (+ a faithful shard's rerank workspace after it)
     L.rerank = a256((size_t)B * C * 4) +
                (kd.faithful ? a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, C)) : 0);
-  else if (kd.faithful)
-    L.rerank = a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, C));
+  else if (kd.faithful)   // (C or kb: the host rerank's stage-1 prescore rescores kb per row in it)
+    L.rerank = a256(cbv2_f32_workspace_bytes(ix, CBV2_F32_RERANK, B, lq, kb > C ? kb : C));
   else
-    L.rerank = a256(cbv2_rerank_workspace_bytes(B, C));
+    L.rerank = a256(cbv2_rerank_workspace_bytes(B, kb > C ? kb : C));
   const size_t bk = a256((size_t)B * k * 4), bkb = a256((size_t)B * (kb > 0 ? kb : 1) * 4),
                bc = a256((size_t)B * C * 4), bs = a256((size_t)B * 4);
   L.total = L.stage2 + 2 * bk + bkb + bc + bs + L.rerank;
@@ -341,6 +369,8 @@ int rerank_call(cbv2_index* ix, cbv2_comm* c, Kind kd, const void* Q, int32_t B,
 // finish_host calls whose results came from the final select's host words
 // (cbv2_retrieve_pool_stats [2]: the tests check that path is the one taken)
 std::atomic<int64_t> g_final_words_calls{0};
+// ... and finish calls that took the host rerank (cbv2_retrieve_pool_stats [3])
+std::atomic<int64_t> g_host_rerank_calls{0};
 
 // Lab knob (cbv2_set_prearm, internal): 0 = the rerank is launched after the
 // fusion (no tagged candidates), 1 = pre-armed (default).
@@ -362,6 +392,29 @@ int wait_words(const uint64_t* w, size_t n, uint32_t seq, const char* what = "st
       return err(CBV2_EHIP, "%s did not arrive (2 s)", what);
   }
   return CBV2_OK;
+}
+
+// A one-shard call's mapped buffer, in 8-byte words: [B][k] stage-2 id words
+// | [B][k] their score words | [B][C] fused candidate words | [B][3 fk] final
+// words | [B][kb] stage-1 prescore words | [B][kb] stage-1 ids (int32) +
+// [B][kb] raw prescores (float), one word per pair.
+size_t mapped_words(int32_t B, int32_t k, int32_t C, int32_t fk, int32_t kb) {
+  return (size_t)B * (2 * (size_t)k + (size_t)C + 3 * (size_t)fk + 2 * (size_t)kb);
+}
+
+constexpr int kHostRerankDeclined = 1;   // host_rerank: not taken, nothing enqueued
+
+// Lab knob (cbv2_set_host_rerank, internal): 1 = the host rerank (default),
+// 0 = the GPU rerank after the fusion (pre-armed or launched).
+int g_host_rerank = 1;
+
+// The host rerank's select of one row: the C fused candidates' scores (stage
+// 2's for its own ids, stage 1's prescore for the others), the best fk by
+// (score desc, position asc) -- select_from_lds's keys and tie rule.
+inline uint32_t key_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
 int check_common(const cbv2_index* ix, Kind* kd, const cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B,
@@ -393,6 +446,7 @@ int cbv2_retrieve_host_marks(int64_t* out, int32_t max) {
 }
 
 void cbv2_set_wait_mode(int32_t mode) { g_wait_mode = mode; }
+void cbv2_set_host_rerank(int32_t on) { g_host_rerank = on; }
 void cbv2_set_prearm(int32_t on) { g_prearm = on; }
 
 int cbv2_retrieve_cancel(cbv2_index* ix, void* workspace, void* stream) {
@@ -416,6 +470,7 @@ int cbv2_retrieve_pool_stats(int64_t* out, int32_t max) {
     out[1] = idle;
   }
   if (max > 2) out[2] = g_final_words_calls.load(std::memory_order_relaxed);
+  if (max > 3) out[3] = g_host_rerank_calls.load(std::memory_order_relaxed);
   return CBV2_OK;
 }
 
@@ -440,20 +495,30 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   // mirrors the ids into it (no D2H copy in finish) and the fusion writes the
   // candidates the rerank reads from it
   Pending pd;
-  const bool mapped = ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, (size_t)B * (k + C) * 8, &pd.mb);
+  const bool mapped =
+      ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, mapped_words(B, k, C, C, kb) * 8, &pd.mb);
   if (mapped) {
     pd.seq = ++pd.mb.seq;
     if (pd.seq == 0) pd.seq = ++pd.mb.seq;
   }
-  cbv2_set_ids_mirror(mapped ? pd.mb.d : nullptr, pd.seq);
+  // the stage-2 ids and (faithful: the host rerank takes them), B * k words
+  // further, their scores
+  cbv2_set_ids_mirror(mapped ? pd.mb.d : nullptr, pd.seq, kd.faithful ? (int64_t)B * k : 0);
   int rc;
-  if (kd.faithful)
+  if (kd.faithful) {
+    // the query split publishes a ready flag (the host rerank's prescore
+    // reads the split from another stream)
+    pd.ready_seq = mapped && B <= kSpinMaxB ? next_ready_seq() : 0;
+    cbv2_set_split_ready(pd.ready_seq);
     rc = cbv2_search_f32(ix, (const float*)Q, B, lq, k, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
                          L.base, L.stage2, L.s, L.ids, L.status, stream);
-  else
+    cbv2_set_split_ready(0);
+  }
+  else {
     rc = cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
+  }
   pd.ids_mirrored = mapped && cbv2_ids_mirror_used() != 0;
-  cbv2_set_ids_mirror(nullptr, 0);
+  cbv2_set_ids_mirror(nullptr, 0, 0);
   if (mapped) {
     if (rc == CBV2_OK)
       put_pending(workspace, pd, ds.dev, (hipStream_t)stream);
@@ -466,6 +531,144 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
 }  // extern "C"
 
 namespace {
+// The host rerank of one-shard small batches (finish_impl): the stage-1
+// prescore and the device outputs' copy enqueued first (the copy polls the
+// final words the host writes at the end), then the round trip's wait (the
+// stage-2 id and score words, the prescore words), the RRF, and per row the
+// select over the candidates' known scores.  Marks the mapped buffer after
+// its last reader; the caller pools it.
+int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, int32_t k, const int32_t* lex_ids,
+                int32_t kb, int32_t rrf_k, int32_t C, int32_t fk, const Layout& L, Pending& pd, float* out_scores,
+                int32_t* out_ids, int32_t* out_pos, hipStream_t st, float* host_s, int32_t* host_i, int32_t* host_p) {
+  const size_t Bk = (size_t)B * k, Bkb = (size_t)B * kb;
+  uint64_t* const idw = (uint64_t*)pd.mb.h;
+  uint64_t* const sw = idw + Bk;
+  uint64_t* const fw = sw + Bk + (size_t)B * C;
+  uint64_t* const lxw = fw + (size_t)3 * B * fk;
+  int32_t* const lxi = (int32_t*)(lxw + Bkb);
+  auto dev = [&](const void* h) { return (uint8_t*)pd.mb.d + ((const uint8_t*)h - (const uint8_t*)pd.mb.h); };
+  int rc = CBV2_OK;
+  // 1. stage 1's prescore: the rerank's raw scores of the whole stage-1 list
+  if (kb > 0) {
+    std::memcpy(lxi, lex_ids, Bkb * 4);
+    cbv2_set_raw_mirror(dev(lxw), pd.seq);
+    const int32_t* lxi_d = (const int32_t*)dev(lxi);
+    float* lxf_d = (float*)dev(lxi + Bkb);
+    // on the second stream, waiting in the kernel for the split's flag: it
+    // runs while stage 2 scans.  Everything it reads or writes is done when
+    // the host has seen its last word (each workgroup's word is its last
+    // store), so neither stream needs to wait for the other.
+    cbv2_set_prescore_ready(pd.ready_seq);
+    rc = cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP, B,
+                                      lq, lxi_d, kb, 0, L.rr, L.rerank, lxf_d, nullptr, nullptr, (const float*)Q,
+                                      side_stream(cbv2_index_device(ix)));
+    cbv2_set_prescore_ready(0);
+    const bool used = cbv2_raw_mirror_used() != 0;
+    cbv2_set_raw_mirror(nullptr, 0);
+    // refused before anything was enqueued (the workspace holds another
+    // split: the stage-1 callable searched into it): the caller takes the
+    // GPU rerank instead
+    if (rc == CBV2_ESTATE) return kHostRerankDeclined;
+    if (!rc && !used) rc = err(CBV2_ESTATE, "stage-1 prescore without host words");
+  }
+  // 2. the device outputs: a copy launched now, polling the final words
+  if (!rc) rc = cbv2_host_result_copy(dev(fw), pd.seq, B, fk, out_scores, out_ids, out_pos, st);
+  const bool copy_armed = rc == CBV2_OK;
+  mark_mapped(pd.mb, st);   // every reader of the buffer is enqueued
+  mark(1);
+  // 3. the round trip: stage 2's ids and scores, stage 1's prescores
+  if (!rc) rc = wait_words(idw, 2 * Bk, pd.seq);
+  if (!rc && kb > 0) rc = wait_words(lxw, Bkb, pd.seq, "stage-1 prescores");
+  mark(2);
+  thread_local std::vector<int32_t> ids_s, cand_s;
+  ids_s.resize(Bk);
+  cand_s.resize((size_t)B * C);
+  if (!rc) {
+    for (size_t i = 0; i < Bk; ++i) ids_s[i] = (int32_t)(uint32_t)idw[i];
+    rc = cbv2_rrf_fuse(lex_ids, kb, ids_s.data(), k, B, rrf_k, C, cand_s.data(), nullptr, nullptr);
+  }
+  mark(3);
+  // 4. per row: the candidates' scores (id -> score by open addressing over
+  //    the row's stage-2 and stage-1 lists), the best fk of them
+  const uint64_t tag = (uint64_t)pd.seq << 32;
+  volatile uint64_t* const vf = fw;
+  const float ninf = -std::numeric_limits<float>::infinity();
+  uint32_t ninf_bits;
+  std::memcpy(&ninf_bits, &ninf, 4);
+  if (rc) {   // the armed copy must not wait for its timeout: publish -inf / -1
+    if (copy_armed)
+      for (size_t i = 0; i < (size_t)3 * B * fk; ++i)
+        vf[i] = tag | ((i / fk) % 3 == 0 ? ninf_bits : 0xffffffffu);
+    return rc;
+  }
+  int bits = 4;
+  while ((1 << bits) < 2 * (k + kb)) ++bits;
+  const uint32_t hmask = (1u << bits) - 1;
+  thread_local std::vector<int32_t> tab_id;
+  thread_local std::vector<float> tab_sc;
+  thread_local std::vector<uint32_t> used;
+  thread_local std::vector<uint64_t> keys;
+  thread_local std::vector<int> order;
+  tab_id.assign((size_t)hmask + 1, INT32_MIN);
+  tab_sc.resize((size_t)hmask + 1);
+  keys.resize((size_t)C);
+  order.resize((size_t)C);
+  for (int32_t b = 0; b < B && !rc; ++b) {
+    for (uint32_t h : used) tab_id[h] = INT32_MIN;
+    used.clear();
+    auto put = [&](int32_t id, uint64_t word) {
+      if (id < 0) return;
+      uint32_t h = ((uint32_t)id * 2654435761u) >> (32 - bits);
+      for (; tab_id[h] != INT32_MIN; h = (h + 1) & hmask)
+        if (tab_id[h] == id) return;   // already there (the same score: the same doc's MaxSim)
+      tab_id[h] = id;
+      const uint32_t sb = (uint32_t)word;
+      std::memcpy(&tab_sc[h], &sb, 4);
+      used.push_back(h);
+    };
+    for (int32_t j = 0; j < k; ++j) put(ids_s[(size_t)b * k + j], sw[(size_t)b * k + j]);
+    for (int32_t j = 0; j < kb; ++j) put(lex_ids[(size_t)b * kb + j], lxw[(size_t)b * kb + j]);
+    for (int32_t t = 0; t < C; ++t) {
+      const int32_t id = cand_s[(size_t)b * C + t];
+      float v = ninf;
+      if (id >= 0) {
+        uint32_t h = ((uint32_t)id * 2654435761u) >> (32 - bits);
+        while (tab_id[h] != INT32_MIN && tab_id[h] != id) h = (h + 1) & hmask;
+        if (tab_id[h] != id) {
+          rc = err(CBV2_ESTATE, "fused candidate %d is in neither list", id);
+          break;
+        }
+        v = tab_sc[h];
+      }
+      keys[t] = ((uint64_t)key_bits(v) << 32) | (uint32_t)~(uint32_t)t;
+      order[t] = t;
+    }
+    if (rc) break;
+    const int m = fk < C ? fk : C;
+    std::partial_sort(order.begin(), order.begin() + m, order.end(), [&](int x, int y) { return keys[x] > keys[y]; });
+    volatile uint64_t* row = vf + (size_t)b * 3 * fk;
+    for (int32_t r = 0; r < fk; ++r) {
+      const int t = r < m ? order[r] : -1;
+      const uint32_t sb = t >= 0 ? (uint32_t)(keys[t] >> 32) : key_bits(ninf);
+      const uint32_t vb = (sb & 0x80000000u) ? (sb & 0x7fffffffu) : ~sb;   // back from the key to the float bits
+      const int32_t id = t >= 0 ? cand_s[(size_t)b * C + t] : -1;
+      if (host_s) {
+        std::memcpy(host_s + (size_t)b * fk + r, &vb, 4);
+        host_i[(size_t)b * fk + r] = id;
+        host_p[(size_t)b * fk + r] = t;
+      }
+      row[r] = tag | vb;
+      row[fk + r] = tag | (uint32_t)id;
+      row[2 * (size_t)fk + r] = tag | (uint32_t)t;
+    }
+  }
+  if (rc)   // (a row failed: every word still gets published)
+    for (size_t i = 0; i < (size_t)3 * B * fk; ++i) vf[i] = tag | ((i / fk) % 3 == 0 ? ninf_bits : 0xffffffffu);
+  else
+    g_host_rerank_calls.fetch_add(1, std::memory_order_relaxed);
+  return rc;
+}
+
 // finish; host_s (nullable): the final top-k also to the host arrays host_s /
 // host_i / host_p ([B][final_k]) before the call returns -- read from the
 // final select's tagged words when it wrote them (one-shard calls), else
@@ -513,12 +716,30 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
   // collectives read device memory)
   Pending pd;
   const bool mapped = !c && take_pending(workspace, &pd);
-  // the call's tagged words in the mapped buffer: [B][k] stage-2 ids (the
-  // search's select wrote them, ids_mirrored) | [B][C] fused candidates
+  // the call's tagged words in the mapped buffer (mapped_words): [B][k]
+  // stage-2 ids and [B][k] their scores (the search's select wrote them,
+  // ids_mirrored) | [B][C] fused candidates | [B][3 final_k] final result | ...
   uint64_t* const idw = mapped ? (uint64_t*)pd.mb.h : nullptr;
-  uint64_t* const cw = mapped ? idw + (size_t)B * k : nullptr;
-  const uint64_t* const cwd = mapped ? (const uint64_t*)pd.mb.d + (size_t)B * k : nullptr;
+  uint64_t* const cw = mapped ? idw + 2 * (size_t)B * k : nullptr;
+  const uint64_t* const cwd = mapped ? (const uint64_t*)pd.mb.d + 2 * (size_t)B * k : nullptr;
   const bool mirrored = mapped && pd.ids_mirrored;
+  // small batches on bf16 / faithful shards: the host rerank -- every fused
+  // candidate's rerank score is stage 2's own (the same MaxSim of the same
+  // doc, bit for bit) or, for stage-1-only candidates, the prescore of the
+  // whole stage-1 list enqueued now (it runs right after stage 2 on the
+  // stream, while the host waits and fuses), so the top final_k is picked
+  // on the host: no rerank launch after the fusion, no round trip back
+  if (mirrored && g_host_rerank && B <= kSpinMaxB && kd.faithful && pd.ready_seq != 0 &&
+      mapped_words(B, k, C, final_k, kb) * 8 <= pd.mb.bytes && side_stream(ds.dev) != nullptr) {
+    rc = host_rerank(ix, kd, Q, B, lq, k, lex_ids, kb, rrf_k, C, final_k, L, pd, out_scores, out_ids, out_pos, st,
+                     host_s, host_i, host_p);
+    if (rc != kHostRerankDeclined) {
+      pool_mapped(ds.dev, pd.mb);   // (marked by host_rerank after its last reader)
+      mark(5);
+      return rc;
+    }
+    rc = CBV2_OK;
+  }
   // small batches pre-arm the rerank: it is launched now, before the wait,
   // and polls its candidates' words (the host writes them after the fusion),
   // so the host -> GPU hop after the fusion is a PCIe read, not a launch
@@ -526,9 +747,9 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
   // host results: the final select's words after the candidate words, when the
   // buffer holds them (pool buffers are >= 64 KiB)
   const size_t fin_words = (size_t)3 * B * final_k;
-  uint64_t* const fw = mapped && host_s && (size_t)(B * (size_t)(k + C)) * 8 + fin_words * 8 <= pd.mb.bytes
+  uint64_t* const fw = mapped && host_s && ((size_t)B * (2 * (size_t)k + C) + fin_words) * 8 <= pd.mb.bytes
                            ? cw + (size_t)B * C : nullptr;
-  uint64_t* const fwd = fw ? (uint64_t*)pd.mb.d + (size_t)B * (k + C) : nullptr;
+  uint64_t* const fwd = fw ? (uint64_t*)pd.mb.d + (size_t)B * (2 * (size_t)k + C) : nullptr;
   bool fin_used = false;
   rc = CBV2_OK;
   if (!mirrored && hipMemcpyAsync(H.ids, L.ids, (size_t)B * k * 4, hipMemcpyDeviceToHost, st) != hipSuccess)

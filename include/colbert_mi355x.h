@@ -593,7 +593,9 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  * cbv2_retrieve_pool_stats (diagnostic): [0] mapped buffers created in this
  *    process, [1] buffers idle in the pools (at most the number of calls that
  *    ever ran at once), [2] finish_host calls whose results were read from the
- *    final select's host words.
+ *    final select's host words, [3] finish calls that picked the final top-k
+ *    on the host (one shard, B <= 8, bf16 / fp32-faithful: every fused
+ *    candidate's score is stage 2's own or stage 1's prescore).
  * cbv2_index_kind: the index's dtype (CBV2_DTYPE_*) and whether a residual is
  *    attached (fp32-faithful, 1) or not (0).                                */
 #define CBV2_RETRIEVE_BAND_CAP 16384

@@ -47,9 +47,17 @@ def _composed(index, Q, lex_ids):
 
 
 def _final_words_calls():
-    st = (ctypes.c_int64 * 3)()
-    _lib.lib().cbv2_retrieve_pool_stats(st, 3)
-    return int(st[2])
+    """finish_host calls served from host words: the final select's (GPU
+    rerank) or the host rerank's."""
+    st = (ctypes.c_int64 * 4)()
+    _lib.lib().cbv2_retrieve_pool_stats(st, 4)
+    return int(st[2]) + int(st[3])
+
+
+def _host_rerank_calls():
+    st = (ctypes.c_int64 * 4)()
+    _lib.lib().cbv2_retrieve_pool_stats(st, 4)
+    return int(st[3])
 
 
 @pytest.mark.parametrize("kind", ["bf16", "fp8", "fp32"])
@@ -69,7 +77,10 @@ def test_one_trip_equals_composed(dev, kind, B):
     bm_i, bm_s = lex.search(qt, qo, KB)
     one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
     for lexical, lex_ids in ((lambda: (bm_i, bm_s), bm_i), (bm_i, bm_i), (None, None)):
+        h0 = _host_rerank_calls()
         got = [x.cpu() for x in one(Q, lexical)]
+        if kind == "fp32" and B <= 8:      # the host rerank (stage 2's scores + stage 1's prescore)
+            assert _host_rerank_calls() == h0 + 1, f"{kind} B={B}: not the host rerank"
         want = [x.cpu() for x in _composed(ix, Q, lex_ids)]
         for g, w, name in zip(got, want, ("scores", "ids", "positions")):
             assert torch.equal(g, w), f"{kind} B={B}: {name} differ from the composed stages"
