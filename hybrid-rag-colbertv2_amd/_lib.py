@@ -23,8 +23,8 @@ SCORERS = {"maxsim": SCORER_MAXSIM, "ref_meanpool_cosine": SCORER_REF_MEANPOOL_C
 ERR_EINVAL, ERR_EUNSUPPORTED, ERR_EHIP, ERR_ESTATE = -1, -2, -3, -4
 F32_SCORE, F32_SEARCH, F32_RERANK = 0, 1, 2
 (OPT_FUSED_TOPK, OPT_DYNAMIC_TAIL, OPT_BAND_DOC_MAJOR, OPT_BAND_LOWER_BOUND, OPT_TOPK_BMAX, OPT_BAND_FUSED,
- OPT_RESCORE_SPLIT, OPT_BAND_REUSE, OPT_BAND_BLOCK_SKIP, OPT_RESCORE_GRID, OPT_DENSE_DOCS, OPT_P1_COLLECT_FUSED) = (
-    1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)
+ OPT_RESCORE_SPLIT, OPT_BAND_REUSE, OPT_BAND_BLOCK_SKIP, OPT_RESCORE_GRID, OPT_DENSE_DOCS, OPT_P1_COLLECT_FUSED,
+ OPT_FOLD_KEYS) = (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13)
 
 _p, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
 _SIGS = {

@@ -66,6 +66,26 @@ __device__ __forceinline__ uint64_t rank_key(float s, uint32_t idx) {
   return ((uint64_t)f2u(s) << 32) | (uint32_t)(~idx);
 }
 
+// Max / min over the 64 lanes, wave-uniform: 16-lane rows by DPP, then the
+// four rows' lane 0.  Full EXEC.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+  return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+  return min(min((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             min((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+
+
 __device__ __forceinline__ float max16(const f32x16& a) {
   float m0 = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
   float m1 = fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]));
@@ -861,15 +881,22 @@ constexpr bool kScanQSkip = CBV2_SCAN_QSKIP != 0;
 // AUX: the doc stream's cache policy (0 cached: the query groups of a chunk
 // share its tiles through L2; 2 non-temporal, for a launch of ONE query
 // group, where every byte is read once).
+// BMK: the block-max top-k's 64-doc block keys and 256-doc superblock keys
+// folded in (bmk [B][bmk_ld], sbk [B][sbk_ld], zeroed before the launch): at
+// each 64-doc group's store, the wave's max of the group's keys by atomic max
+// -- a group of a range that does not start on a block boundary spans two
+// blocks (and at most two superblocks), so its two parts go separately.  The
+// keys equal block_max_kernel's.
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
           bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd,
-          int MORDER = 0, int AUX = 0>
+          int MORDER = 0, int AUX = 0, bool BMK = false>
 __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
     const uint8_t* __restrict__ tokens, const int32_t* __restrict__ doclens, int64_t n,
     const uint16_t* __restrict__ Q, int B, int lq, float* __restrict__ out, int64_t ld_out,
     int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr, int task_docs,
     uint64_t* __restrict__ stamps, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0,
-    int tail_slices = 1) {
+    int tail_slices = 1, uint32_t* __restrict__ bmk = nullptr, int64_t bmk_ld = 0, uint32_t* __restrict__ sbk = nullptr,
+    int64_t sbk_ld = 0) {
   // TPI tokens of 4 docs per iteration (32: 32 KiB, 64: 64 KiB), IPG per group
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kRowBytes;
@@ -1136,6 +1163,32 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
                 if (qi < B && c <= (G & 15) && dd < nd) out[(size_t)qi * ld_out + d_begin + dd] = sc[q];
               }
               stored = true;
+              if constexpr (BMK) {
+                const int64_t d0 = d_begin + 64 * (G >> 4);   // the group's first doc
+                const int64_t bb = ((d0 >> 6) + 1) << 6;       // the next block boundary
+                const bool valid = c <= (G & 15) && dd < nd;
+#pragma unroll
+                for (int q = 0; q < QW; ++q) {
+                  const int qi = qg * QPB + wave * QW + q;
+                  if (qi >= B) continue;   // wave-uniform
+                  const uint32_t v = valid ? f2u(sc[q]) : 0u;
+                  const uint32_t ulo = wave_max_u32(d_begin + dd < bb ? v : 0u);
+                  const uint32_t uhi = wave_max_u32(d_begin + dd >= bb ? v : 0u);
+                  if (lane == 0) {
+                    uint32_t* br = bmk + (size_t)qi * bmk_ld;
+                    uint32_t* sr = sbk + (size_t)qi * sbk_ld;
+                    const int64_t b0 = d0 >> 6, s0 = d0 >> 8;
+                    if (ulo != 0u) atomicMax(br + b0, ulo);
+                    if (uhi != 0u) atomicMax(br + b0 + 1, uhi);
+                    if ((bb & 255) == 0) {   // the block boundary is a superblock boundary
+                      if (ulo != 0u) atomicMax(sr + s0, ulo);
+                      if (uhi != 0u) atomicMax(sr + s0 + 1, uhi);
+                    } else if ((ulo | uhi) != 0u) {
+                      atomicMax(sr + s0, max(ulo, uhi));
+                    }
+                  }
+                }
+              }
             }
           }
         }
@@ -2456,25 +2509,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void maxsim_scan_f8_stream_kernel(
 // the lowest indices), then a bitonic sort of the k winners in LDS.
 // ---------------------------------------------------------------------------
 constexpr int kTkThreads = 1024;
-
-// Max / min over the 64 lanes, wave-uniform: 16-lane rows by DPP, then the
-// four rows' lane 0.  Full EXEC.
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
-  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
-  return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
-             max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
-}
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
-  return min(min((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
-             min((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
-}
 
 // Wave 0 finds bin b with count(bins > b) < kleft <= count(bins >= b).
 __device__ void find_bin(const uint32_t* hist, int nb, uint32_t kleft, uint32_t* s_bin,
@@ -3873,6 +3907,7 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 constexpr int kArriveSlotsK = 4;   // slots of the faithful workspace's arrival counters (kArriveSlots)
 constexpr int kArrPhase1K = 3;     // (kArrPhase1) the phase-1 slot: done1's replicas, then at
 constexpr int kSplitReady = 256;   // int 256 of a row's slot the split's ready flag
+constexpr int64_t kSplitZeroInts = 16384;   // block keys zeroed per extra workgroup of the query split
 __global__ __launch_bounds__(512) void split_query_kernel(const float* __restrict__ Q, int lq,
                                                           uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
                                                           float E, float M, float* __restrict__ beta,
@@ -3881,13 +3916,24 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
                                                           int32_t* __restrict__ done = nullptr, int count0 = 0,
                                                           int32_t* __restrict__ arrive = nullptr, int narrive = 0,
                                                           int* __restrict__ ctr = nullptr, int nctr = 0,
-                                                          uint32_t ready_seq = 0) {
+                                                          uint32_t ready_seq = 0, int nrows = 0,
+                                                          uint32_t* __restrict__ zkeys = nullptr, int64_t nz = 0) {
   // one 16-lane group per query token (lq <= 32: one pass, no loop -- the B=1
   // latency path waits on this launch); the per-token bound terms are summed
   // in the order of the round-3 one-wave kernel (4 strided partial sums, then
   // pairwise), so beta keeps its bits
   __shared__ float s_t[kLqMax];
   const int b = blockIdx.x, tid = threadIdx.x, r = tid >> 4, sub = tid & 15;
+  if (nrows > 0 && b >= nrows) {   // workgroups past the rows: zero the scan-folded block keys (zkeys, 16-B aligned)
+    const int64_t per = kSplitZeroInts, i0 = (int64_t)(b - nrows) * per;
+    for (int64_t i = i0 + 4 * tid; i < i0 + per && i < nz; i += 4 * blockDim.x) {
+      if (i + 3 < nz)
+        *reinterpret_cast<uint4*>(zkeys + i) = make_uint4(0u, 0u, 0u, 0u);
+      else
+        for (int64_t e = i; e < nz; ++e) zkeys[e] = 0u;
+    }
+    return;
+  }
   if (r < lq) {
     const size_t row = (size_t)b * lq + r;
     float xx, rr, hh;
@@ -3913,7 +3959,7 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
     const int per = narrive / kArriveSlotsK;
     for (int i = tid; i < narrive; i += blockDim.x) {
       const int j = i / per, e = i - j * per;
-      arrive[((size_t)j * gridDim.x + b) * per + e] = 0;
+      arrive[((size_t)j * nrows + b) * per + e] = 0;
     }
   }
   if (ctr != nullptr && b == 0)   // the scan's task counters (the scan that follows skips its memset)
@@ -3928,7 +3974,7 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
       __threadfence();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int per = narrive / kArriveSlotsK;
-      __hip_atomic_store(arrive + ((size_t)kArrPhase1K * gridDim.x + b) * per + kSplitReady, (int32_t)ready_seq,
+      __hip_atomic_store(arrive + ((size_t)kArrPhase1K * nrows + b) * per + kSplitReady, (int32_t)ready_seq,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -5421,6 +5467,7 @@ struct cbv2_index {
   // tiles (6.9 TB/s)
   bool dense_docs = false;
   bool p1_collect_fused = true;  // CBV2_OPT_P1_COLLECT_FUSED (phase1_collect_kernel)
+  bool fold_keys = true;         // CBV2_OPT_FOLD_KEYS (scan_folds_bmax_zeroed)
   std::mutex mu;  // ring_ev_used, scan_ev / scan_ev_used
   // fp32-faithful index: bf16 residual lo = bf16(x - hi) of the fp32 corpus
   // whose rounding hi is `tokens`, and the split's bounds (max ||x - hi||,
@@ -5776,10 +5823,10 @@ int64_t scan_chunks(const cbv2_index* ix, int nq_groups, int64_t target) {
 
 template <int WAVES, int QW, int PER_CU, int D, int NBUF, bool STAMPS, int TPI = 32, int OCC = 2, bool SPREAD = false,
           int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd, int MORDER = 0,
-          int AUX = 0>
+          int AUX = 0, bool BMK = false>
 int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                     float dyn_frac = kScanDynFrac, int task_docs = kScanTaskDocs, uint64_t* stamps = nullptr,
-                    int* ctr_ws = nullptr, FusedTopk* ft = nullptr) {
+                    int* ctr_ws = nullptr, FusedTopk* ft = nullptr, uint32_t* bm = nullptr) {
   constexpr int QPB = WAVES * QW;
   const int nq_groups = (B + QPB - 1) / QPB;
   ScanSplit sp;
@@ -5790,11 +5837,13 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
       return fail(CBV2_EINVAL, "fused top-k: bad k or slot count");
     ft->slots = sp.n_chunks;
   }
+  if (BMK && bm == nullptr) return fail(CBV2_EINVAL, "block-key scan without keys");
   hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD, MORDER,
-                                             AUX>),
+                                             AUX, BMK>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
                      ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
-                     ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
+                     ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices, bm,
+                     bm_blocks(ix->n), bm != nullptr ? bm_super_keys(bm, B, ix->n) : nullptr, bm_supers(ix->n));
   if ((rc = launch_check("maxsim_scan16x4_kernel"))) return rc;
   return finish_split(ix, sp, st);
 }
@@ -5906,6 +5955,12 @@ bool scan_folds_bmax(const cbv2_index* ix, int B) {
   return ix->dtype == CBV2_DTYPE_BF16 && ix->ld == kLd && B <= kDirectMaxB && kDefaultScan == kScanAuto &&
          !ix->dense_docs;
 }
+// ... and the dense-doc 4 x 1 scan (B <= 4) folds them by atomic max into keys
+// its caller zeroed (the faithful search's query split does)
+bool scan_folds_bmax_zeroed(const cbv2_index* ix, int B) {
+  return ix->dtype == CBV2_DTYPE_BF16 && ix->ld == kLd && B <= 4 && kDefaultScan == kScanAuto && ix->dense_docs &&
+         ix->fold_keys && pick_shape(kBf16Shapes, B) == kScan16x4W4Q1;
+}
 int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, int64_t ld_out, hipStream_t st,
                 int variant = kDefaultScan, int* ctr_ws = nullptr, FusedTopk* ft = nullptr, uint32_t* bm = nullptr) {
   if (ix->n == 0) return CBV2_OK;
@@ -5979,6 +6034,9 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan16x4<8, 1, 2, 2, 2, false, 32, 4>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB,
                                                           kScanTaskDocs, nullptr, ctr_ws);
     case kScan16x4W4Q1:     // 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
+      if (B <= 4 && bm != nullptr)   // the block keys folded in (zeroed by the caller: scan_folds_bmax_zeroed)
+        return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2, true>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws, nullptr, bm);
       if (B <= 4)           // one query group: every doc byte is read once (non-temporal)
         return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
             ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
@@ -6575,13 +6633,16 @@ bool split_holds(const cbv2_index* ix, const float* Q, int B, int lq, const void
 
 // zero_ctr: the split also zeroes the scan's task-counter block (w->ctr; the
 // search's scan then runs under CtrPrezeroed and skips its memset launch).
+// zkeys (nullable, 16-B aligned): nz ints zeroed by extra workgroups (the
+// block keys the next scan folds in with atomic max)
 int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipStream_t st, int count0 = 0,
-                  bool zero_ctr = false) {
+                  bool zero_ctr = false, uint32_t* zkeys = nullptr, int64_t nz = 0) {
   note_split(ix, Q, B, lq, w->qhi);
-  hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)B), dim3(512), 0, st, Q, lq, w->qhi, w->qlo, ix->resid_max,
-                     ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done, count0,
-                     w->arrive, kArriveSlots * kArriveInts, zero_ctr ? w->ctr : nullptr, zero_ctr ? kRingInts : 0,
-                     w->arrive != nullptr ? g_split_ready_seq : 0u);
+  const int64_t extra = zkeys != nullptr ? (nz + kSplitZeroInts - 1) / kSplitZeroInts : 0;
+  hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)(B + extra)), dim3(512), 0, st, Q, lq, w->qhi, w->qlo,
+                     ix->resid_max, ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done,
+                     count0, w->arrive, kArriveSlots * kArriveInts, zero_ctr ? w->ctr : nullptr,
+                     zero_ctr ? kRingInts : 0, w->arrive != nullptr ? g_split_ready_seq : 0u, B, zkeys, nz);
   return launch_check("split_query_kernel");
 }
 
@@ -6925,6 +6986,9 @@ int cbv2_index_set_option(cbv2_index* ix, int32_t option, int64_t value) {
     case CBV2_OPT_P1_COLLECT_FUSED:
       ix->p1_collect_fused = value != 0;
       return CBV2_OK;
+    case CBV2_OPT_FOLD_KEYS:
+      ix->fold_keys = value != 0;
+      return CBV2_OK;
     case CBV2_OPT_RESCORE_GRID:
       if (value < 0 || value > 65535) return fail(CBV2_EINVAL, "rescore grid must be in [0, 65535]");
       ix->rescore_grid = (int)value;
@@ -7141,7 +7205,15 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     if ((rc = topk_impl_empty(B, k, out_scores, out_ids, st))) return rc;
     return 1;
   }
-  if ((rc = split_queries(ix, Q, B, lq, &w, st, want_lb && band_reuses_topk(ix, B, k) ? k : 0, true))) return rc;
+  // the block-max select's keys: folded into the scan -- by the streaming
+  // scans directly, by the dense 4 x 1 scan with atomic max into keys the
+  // query split zeroes
+  const bool bmax = k <= kBandCapMax && bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k);
+  const bool fold0 = bmax && !scan_folds_bmax(ix, B) && scan_folds_bmax_zeroed(ix, B);
+  if ((rc = split_queries(ix, Q, B, lq, &w, st, want_lb && band_reuses_topk(ix, B, k) ? k : 0, true,
+                          fold0 ? (uint32_t*)w.tk : nullptr,
+                          fold0 ? (int64_t)B * (bm_blocks(ix->n) + bm_supers(ix->n)) : 0)))
+    return rc;
   if (k > kBandCapMax) {   // no band can hold k: every row takes the full faithful scan (status -1)
     CBV2_HIP(hipMemsetAsync(out_status, 0xff, (size_t)B * sizeof(int32_t), st));
     if ((rc = launch_rescore(ix, &w, B, lq, nullptr, nullptr, ix->n, 0, w.T, ix->n, st))) return rc;
@@ -7150,8 +7222,7 @@ int search_f32_phase1(cbv2_index* ix, const float* Q, int32_t B, int32_t lq, int
     return 1;
   }
   // 1. bf16 scan of hi, top-k of T (its k-th score anchors the band)
-  const bool bmax = bmax_eligible(ix, CBV2_SCORER_MAXSIM, B, k);
-  const bool fold = bmax && scan_folds_bmax(ix, B);
+  const bool fold = bmax && (scan_folds_bmax(ix, B) || fold0);
   {
     CtrPolicy cp(kCtrPrezeroed);   // the split zeroed the scan's counters
     if ((rc = scan_maxsim_timed(ix, w.qhi, B, lq, w.T, ix->n, st, w.ctr, nullptr, fold ? (uint32_t*)w.tk : nullptr)))

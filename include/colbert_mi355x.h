@@ -172,6 +172,11 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
  *                        faithful scores) and the band collect in ONE launch
  *                        (the collect's loads overlap phase 1; 0: two
  *                        launches).  Identical results.
+ *  CBV2_OPT_FOLD_KEYS     1: cbv2_search_f32 on at most 4 queries of a
+ *                        dense-doc index folds the block-max select's block
+ *                        keys into its 4 x 1 scan (atomic max into keys the
+ *                        query split zeroes; 0: a pass over the scores).
+ *                        Identical results.
  * cbv2_index_last_scan_plan: the work split of this handle's latest scan
  * launch: {workgroups, static chunk docs, static docs, dynamic tail 0/1}.
  * Thread safety: one handle may be used from several host threads and
@@ -189,6 +194,7 @@ int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* co
 #define CBV2_OPT_RESCORE_GRID 10
 #define CBV2_OPT_DENSE_DOCS 11
 #define CBV2_OPT_P1_COLLECT_FUSED 12
+#define CBV2_OPT_FOLD_KEYS 13
 int cbv2_index_set_option(cbv2_index* index, int32_t option, int64_t value);
 int cbv2_index_last_scan_plan(const cbv2_index* index, int64_t* out4);
 /* Per-query workgroup lists a cbv2_search of (B, k, scorer) keeps with the

@@ -423,6 +423,34 @@ def test_phase1_collect_fused_equals_two_launches(dev, bmax_corpus, B):
     ix.set_option(_lib.OPT_P1_COLLECT_FUSED, 1)
 
 
+@pytest.mark.parametrize("B", [1, 2, 4])
+def test_fold_keys_equals_block_max_pass(dev, B):
+    """CBV2_OPT_FOLD_KEYS: on a dense-doc index the 4 x 1 scan folds the
+    block-max select's block / superblock keys in by atomic max (keys the
+    query split zeroes; scan ranges of any alignment) -- top-k, scores and
+    band sizes equal the separate block-max pass's bit for bit (k = 40 / 100
+    / 400, twice in a row: the keys are zeroed per call)."""
+    from hybrid_rag_colbertv2_amd import synth
+    n = 70_003
+    Qf = synth.make_queries(B, 32, seed=41)
+    planted = synth.planted_ids(B, n, 10, seed=42)
+    x, dl = synth.make_shard(0, n, Qf, planted, dev, seed=43, dtype=torch.float32)
+    ix = ColbertIndex.faithful_f32(x, dl, id_base=5)
+    del x
+    assert ix.dense_docs
+    Q = Qf.to(dev).contiguous()
+    got = {}
+    for k in (40, 100, 400):
+        for fold in (1, 0, 1):
+            ix.set_option(_lib.OPT_FOLD_KEYS, fold)
+            s, i = ix.search(Q, k)
+            got.setdefault((k, fold), []).append((s.clone(), i.clone(), ix.last_band.clone()))
+        for run in got[(k, 1)]:
+            for a, b, name in zip(run, got[(k, 0)][0], ("s", "i", "band")):
+                assert torch.equal(a, b), (k, name)
+    ix.set_option(_lib.OPT_FOLD_KEYS, 1)
+
+
 @pytest.mark.parametrize("B", [1, 12])
 def test_rescore_grid_equals_default(dev, B):
     """CBV2_OPT_RESCORE_GRID: fewer workgroups per row grid-stride over the

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--docs", type=int, default=125000)
     ap.add_argument("--iters", type=int, default=60)
     ap.add_argument("--build", action="store_true")
+    ap.add_argument("--grid", type=int, default=0, help="CBV2_OPT_RESCORE_GRID for the run (0: automatic)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -63,6 +64,8 @@ def main():
     tokens, doclens = synth.make_shard(0, n, Qf, planted, dev, seed=0, dtype=torch.float32)
     ix = ColbertIndex.faithful_f32(tokens, doclens)
     del tokens
+    if a.grid:
+        ix.set_option(_lib.OPT_RESCORE_GRID, a.grid)
     Q1 = Qf[:1].to(dev).contiguous()
     one = OneTripRetriever(ix)
     stamps = torch.zeros((len(KINDS), STRIDE), dtype=torch.int64, device=dev)
@@ -106,7 +109,7 @@ def main():
                 r[name + ":count"] = int(S[k, 5])
         rows.append(r)
     keys = sorted({k for r in rows for k in r}, key=lambda k: statistics.median(r[k] for r in rows if k in r))
-    out = {"docs": n, "iters": a.iters, "p50_us": round(statistics.median(lat), 1),
+    out = {"docs": n, "iters": a.iters, "grid": a.grid, "p50_us": round(statistics.median(lat), 1),
            "timeline_us_from_bmax_start": {k: round(statistics.median(r[k] for r in rows if k in r), 2) for k in keys}}
     print(json.dumps(out), flush=True)
 
