@@ -3256,9 +3256,15 @@ __device__ void topk_bmax_row(const float* __restrict__ x, int64_t n, int k, int
   //    minimum pass.  (Lab, B=1 at 125k docs: 7.2 us for two exact radix
   //    passes over the block keys in L2; 24 us for one wave bisecting them.)
   const uint32_t khi = misc[8];
-  const uint64_t span = (uint64_t)(khi - misc[9]) + 1;
-  // larger key -> higher bin (find_bin counts from the top bin down)
-  auto bin_of = [&](uint32_t u) { return (uint32_t)(kBmBins - 1) - (uint32_t)(((uint64_t)(khi - u) * kBmBins) / span); };
+  // larger key -> higher bin (find_bin counts from the top bin down); the
+  // bin index in float arithmetic (no 64-bit division): only its
+  // monotonicity matters, and float conversion, scaling and truncation are
+  // monotone
+  const float bscale = (float)kBmBins / ((float)(khi - misc[9]) + 1.0f);
+  auto bin_of = [&](uint32_t u) {
+    const uint32_t d = (uint32_t)((float)(khi - u) * bscale);
+    return (uint32_t)(kBmBins - 1) - (d < (uint32_t)kBmBins ? d : (uint32_t)(kBmBins - 1));
+  };
   for (int i = tid; i < nk; i += nth) atomicAdd(&hist[bin_of(keys[i])], 1u);   // linear bins: few collisions
   __syncthreads();
   if (wave == 0) find_bin1024(hist, kleft, &misc[4], &misc[5], &misc[6]);
@@ -3384,11 +3390,19 @@ __global__ __launch_bounds__(kTkThreads) void topk_bmax_kernel(const float* __re
                                                                int64_t bm_ld, const uint32_t* __restrict__ sb,
                                                                int64_t sb_ld, float* __restrict__ out_s,
                                                                int32_t* __restrict__ out_i,
-                                                               Mirror mirror = Mirror()) {
+                                                               Mirror mirror = Mirror(),
+                                                               uint64_t* __restrict__ stamps = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t bm_dyn[];
   const int row = blockIdx.x;
+  if (stamps != nullptr && row == 0 && threadIdx.x == 0) {   // lab: row 0 (start = its select's start)
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    stamps[16] = t;
+    stamps[17] = t;
+    stamps[6] = t;
+  }
   topk_bmax_row(scores + (size_t)row * ld, n, k, id_base, bm + (size_t)row * bm_ld, sb + (size_t)row * sb_ld,
-                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn, mirror.row(row, k));
+                out_s + (size_t)row * k, out_i + (size_t)row * k, bm_dyn, mirror.row(row, k),
+                row == 0 ? stamps : nullptr);
 }
 
 // Block-max top-k in ONE launch (small batches, the latency path): grid (P, B)
@@ -6355,7 +6369,7 @@ int topk_bmax(const float* scores, int32_t B, int64_t n, int64_t ld, int32_t k, 
   }
   const size_t lds = bm_select_lds(n, k);
   hipLaunchKernelGGL(topk_bmax_kernel, dim3((unsigned)B), dim3(kTkThreads), lds, st, scores, n, ld, k, id_base, bm,
-                     nb, sb, ns, out_s, out_i, mirror);
+                     nb, sb, ns, out_s, out_i, mirror, LAB_STAMPS(0));
   return launch_check("topk_bmax_kernel");
 }
 
