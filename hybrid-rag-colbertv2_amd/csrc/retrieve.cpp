@@ -221,10 +221,17 @@ uint32_t next_ready_seq() {
 // The host rerank's second stream (per host thread and device; never
 // destroyed, like the mapped buffers): the stage-1 prescore runs on it
 // concurrently with stage 2's scan instead of after it.
+// High priority: its queue's workgroups are dispatched ahead of the scan's
+// (lab: at normal priority they waited for the scan's own to retire).
 hipStream_t side_stream(int dev) {
   thread_local hipStream_t s[kMaxDev] = {};
   if (dev < 0 || dev >= kMaxDev) return nullptr;
-  if (s[dev] == nullptr && hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking) != hipSuccess) s[dev] = nullptr;
+  if (s[dev] == nullptr) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&s[dev], hipStreamNonBlocking, greatest) != hipSuccess)
+      s[dev] = nullptr;
+  }
   return s[dev];
 }
 std::mutex g_pending_mu;
