@@ -4,6 +4,8 @@ its host buffers come from, and when the fp32-faithful rerank may reuse
 begin's query split (HybridRetriever.retrieve, LRC:894-935).
 
 Done =
+* the faithful host rerank is thread-safe (8 threads, host and device
+  results, every call the host rerank);
 * a B = 256 finish sleeps in its wait: the process CPU time of a whole
   one-trip call (begin + finish, no stage 1) stays <= 5 ms while the GPU
   scans for tens of ms (a polling wait would burn the whole scan);
@@ -107,6 +109,59 @@ def test_mapped_buffers_pooled_and_device_restored(dev):
     assert created <= 16, f"1,000 calls on 8 threads created {created} mapped buffers"
     assert int(st1[1]) == int(st1[0]), "a mapped buffer was not returned to its pool"
     assert devs == [dev.index or 0] * 8
+
+
+def test_faithful_host_rerank_threads(dev):
+    """The faithful host rerank (stage 2's scores + the stage-1 prescore on
+    each thread's second stream, the split-ready flag in each workspace)
+    under 8 threads x 40 calls, B = 1 and 4, host and device results: every
+    call equals the composed stages, and every one took the host rerank."""
+    N = 6000
+    L = _lib.lib()
+    Qf, _, tokens, doclens = _index(dev, N, 4, seed=13, dtype=torch.float32)
+    ix = ColbertIndex.faithful_f32(tokens, doclens)
+    Q1, Q4 = Qf[:1].to(dev).contiguous(), Qf.to(dev).contiguous()
+    bm = [np.stack([np.random.default_rng(b + 7 * B).permutation(N)[:K] for b in range(B)]).astype(np.int32)
+          for B in (1, 4)]
+    want = []
+    for Q, bi in ((Q1, bm[0]), (Q4, bm[1])):
+        _, ids = ix.search(Q, K)
+        cand = rrf_fuse(bi, ids.cpu().numpy(), rrf_k=60, C=C)
+        want.append([x.cpu() for x in ix.rerank(Q, torch.from_numpy(cand).to(dev), KF)])
+    st0 = (ctypes.c_int64 * 4)()
+    L.cbv2_retrieve_pool_stats(st0, 4)
+    errs = []
+
+    def body(t):
+        try:
+            one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+            s = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(s):
+                for i in range(40):
+                    j = (i + t) % 2
+                    Q, bi = ((Q1, bm[0]), (Q4, bm[1]))[j]
+                    if i % 3 == 0:
+                        got = [torch.from_numpy(x) for x in one(Q, bi, host=True)]
+                    else:
+                        got = [x.cpu() for x in one(Q, bi)]
+                    if not all(torch.equal(g, w) for g, w in zip(got, want[j])):
+                        raise AssertionError(f"thread {t} call {i}: results differ from the composed stages")
+        except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
+            errs.append(e)
+
+    ts = [threading.Thread(target=body, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a thread hung"
+    if errs:
+        raise errs[0]
+    torch.cuda.synchronize()
+    st1 = (ctypes.c_int64 * 4)()
+    L.cbv2_retrieve_pool_stats(st1, 4)
+    assert int(st1[3] - st0[3]) == 8 * 40, "not every call took the host rerank"
+    assert int(st1[1]) == int(st1[0]), "a mapped buffer was not returned to its pool"
 
 
 def test_faithful_finish_resplits_after_foreign_split(dev):
