@@ -3920,7 +3920,6 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 // fewer than separate memsets.
 constexpr int kArriveSlotsK = 4;   // slots of the faithful workspace's arrival counters (kArriveSlots)
 constexpr int kArrPhase1K = 3;     // (kArrPhase1) the phase-1 slot: done1's replicas, then at
-constexpr int kSplitReady = 256;   // int 256 of a row's slot the split's ready flag
 constexpr int64_t kSplitZeroInts = 16384;   // block keys zeroed per extra workgroup of the query split
 __global__ __launch_bounds__(512) void split_query_kernel(const float* __restrict__ Q, int lq,
                                                           uint16_t* __restrict__ qhi, uint16_t* __restrict__ qlo,
@@ -3931,7 +3930,8 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
                                                           int32_t* __restrict__ arrive = nullptr, int narrive = 0,
                                                           int* __restrict__ ctr = nullptr, int nctr = 0,
                                                           uint32_t ready_seq = 0, int nrows = 0,
-                                                          uint32_t* __restrict__ zkeys = nullptr, int64_t nz = 0) {
+                                                          uint32_t* __restrict__ zkeys = nullptr, int64_t nz = 0,
+                                                          int32_t* __restrict__ ready_words = nullptr) {
   // one 16-lane group per query token (lq <= 32: one pass, no loop -- the B=1
   // latency path waits on this launch); the per-token bound terms are summed
   // in the order of the round-3 one-wave kernel (4 strided partial sums, then
@@ -3978,18 +3978,17 @@ __global__ __launch_bounds__(512) void split_query_kernel(const float* __restric
   }
   if (ctr != nullptr && b == 0)   // the scan's task counters (the scan that follows skips its memset)
     for (int i = tid; i < nctr; i += blockDim.x) ctr[i] = 0;
-  if (ready_seq != 0 && arrive != nullptr) {
-    // the row's split is published (kSplitReady of its phase-1 arrival slot):
-    // plain stores -> agent release -> relaxed flag (MI355X_MICROARCH.md, the
-    // handoff-flag row; the vmcnt(0) after the fence: its compiler-hazard fix),
-    // read by the latency path's stage-1 prescore on another stream
+  if (ready_seq != 0 && ready_words != nullptr) {
+    // the row's split is published to the host (ready_words[b], a word of the
+    // call's mapped buffer): plain stores -> agent release -> relaxed flag
+    // (MI355X_MICROARCH.md, the handoff-flag row; the vmcnt(0) after the
+    // fence: its compiler-hazard fix).  The host launches the stage-1
+    // prescore on another stream only once it has seen every row's flag.
     __syncthreads();
     if (tid == 0) {
       __threadfence();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int per = narrive / kArriveSlotsK;
-      __hip_atomic_store(arrive + ((size_t)kArrPhase1K * nrows + b) * per + kSplitReady, (int32_t)ready_seq,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ready_words + b, (int32_t)ready_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -4188,8 +4187,6 @@ struct RowSelect {
   int32_t* status = nullptr;     // kSelBand: the band size (the fallback writes -1 for overflowed rows)
   Mirror ids_mirror;             // kSelBand: [B][k] host mirror of the final ids (w nullable)
   FinalMirror fin;               // kSelCand: the host words of the call's final result (w nullable)
-  const int32_t* ready = nullptr;   // (nullable) row b's ready flag at ready[b * kArriveInts]: wait for
-  uint32_t ready_seq = 0;           //   it to read ready_seq before reading the split queries
   Mirror raw;                    // kSelNone (w nullable): every pair's score also as the host word
                                  // raw.w[b * ld_c + c] ({score bits, seq}; the latency path's stage-1 prescore)
   uint64_t* stamps = nullptr;    // lab builds only (LAB_STAMPS): [16 + 2x] / [17 + 2x] workgroup x's start /
@@ -4312,18 +4309,6 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
   const int b = blockIdx.y;
   if (rs.stamps != nullptr && threadIdx.x == 0 && blockIdx.x < kLabWgs)
     rs.stamps[16 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  if (rs.ready != nullptr) {   // another stream's split: one relaxed poll, one agent acquire (handoff-flag row)
-    if (threadIdx.x == 0) {
-      const int32_t* f = rs.ready + (size_t)b * kArriveInts;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((uint32_t)__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != rs.ready_seq &&
-             __builtin_amdgcn_s_memrealtime() - t0 < kCandWaitTicks)
-        __builtin_amdgcn_s_sleep(4);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
   if (only_neg != nullptr && only_neg[b] >= 0) return;  // block-uniform
   int64_t lim = limit;
   if (count != nullptr) {
@@ -5737,12 +5722,19 @@ thread_local bool g_final_mirror_used = false;
 // g_raw_mirror_used.
 thread_local Mirror g_raw_mirror;
 thread_local bool g_raw_mirror_used = false;
-// The latency path's split-ready flag (cbv2_set_split_ready around begin's
-// search: its query split publishes this seq when done) and the stage-1
-// prescore that waits for it on another stream (cbv2_set_prescore_ready).
+// The latency path's ready flags (cbv2_set_split_ready_begin around begin's
+// search: its first launch publishes this seq to words of the call's mapped
+// buffer when the queries / their split are complete; the host launches the
+// stage-1 prescore on another stream only after it has seen them -- an
+// in-kernel wait on another queue's kernel could starve it of the CUs it
+// needs) and the prescore itself (cbv2_set_prescore_ready).
 thread_local uint32_t g_split_ready_seq = 0;
-thread_local uint32_t g_prescore_ready_seq = 0;
-thread_local const int32_t* g_prescore_ready = nullptr;
+thread_local uint32_t g_prescore_ready_seq = 0;   // (only: the prescore must use the search's split)
+// where the search just issued wrote its ready flag (row b at
+// g_ready_flag[b * g_ready_flag_ld]; nullptr: it wrote none)
+thread_local int32_t* g_ready_flag = nullptr;
+thread_local int64_t g_ready_flag_ld = 0;
+thread_local int32_t* g_split_ready_word = nullptr;   // the bf16 search's flag word (the call's mapped buffer)
 // Lab builds (-DCBV2_LAB_STAMPS, tools/chain_lab.py): per-launch phase stamps
 // of the latency path's kernels, kind k at g_lab_stamps + k * kLabStride --
 // 0 block-max select, 1 phase-1 rescoring, 2 band collect, 3 band rescoring +
@@ -5763,6 +5755,35 @@ struct CtrPolicy {
   }
   ~CtrPolicy() { g_ctr_policy = prev; }
 };
+
+// (zero_ctr_block below: the memset, or this kernel with the flag)
+// The bf16 search's counter block zeroed by a kernel instead of a memset when
+// the latency path asked for a ready flag (cbv2_set_split_ready_begin): after
+// the zeroing, the flag word = seq (plain stores -> agent release -> relaxed
+// flag, as the faithful query split publishes its own) -- the host sees it
+// before it launches the stage-1 prescore on another stream (the queries were
+// complete when this first launch of the search ran).  The word is the
+// call's own (its mapped buffer): no later search can overwrite it.
+__global__ __launch_bounds__(256) void ctr_zero_ready_kernel(int* __restrict__ ctr, int n, int* __restrict__ flag,
+                                                             uint32_t seq) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) ctr[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, (int)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t zero_ctr_block(int* ctr, hipStream_t st) {
+  if (g_split_ready_seq == 0 || g_split_ready_word == nullptr || g_ready_flag != nullptr)
+    return hipMemsetAsync(ctr, 0, kCtrBytes, st);
+  hipLaunchKernelGGL(ctr_zero_ready_kernel, dim3(1), dim3(256), 0, st, ctr, kRingInts, g_split_ready_word,
+                     g_split_ready_seq);
+  g_ready_flag = g_split_ready_word;   // one flag for every row
+  g_ready_flag_ld = 0;
+  return hipGetLastError();
+}
 
 int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, int task_docs, hipStream_t st,
                ScanSplit* sp, int* ctr_ws) {
@@ -5796,12 +5817,12 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
     if (ctr_ws == nullptr || g_ctr_policy == kCtrDefault) {
       CBV2_HIP(hipMemsetAsync(sp->ctr, 0, (size_t)nq_groups * sp->slices * sizeof(int), st));
     } else if (g_ctr_policy == kCtrZeroAll) {
-      CBV2_HIP(hipMemsetAsync(sp->ctr, 0, kCtrBytes, st));
+      CBV2_HIP(zero_ctr_block(sp->ctr, st));
       g_ctr_zeroed = true;
     }
   } else {
     if (ctr_ws != nullptr && g_ctr_policy == kCtrZeroAll) {
-      CBV2_HIP(hipMemsetAsync(ctr_ws, 0, kCtrBytes, st));
+      CBV2_HIP(zero_ctr_block(ctr_ws, st));
       g_ctr_zeroed = true;
     }
     sp->chunk_docs = (ix->n + n_chunks - 1) / n_chunks;
@@ -6653,10 +6674,16 @@ int split_queries(cbv2_index* ix, const float* Q, int B, int lq, F32Ws* w, hipSt
                   bool zero_ctr = false, uint32_t* zkeys = nullptr, int64_t nz = 0) {
   note_split(ix, Q, B, lq, w->qhi);
   const int64_t extra = zkeys != nullptr ? (nz + kSplitZeroInts - 1) / kSplitZeroInts : 0;
+  const bool publish = g_split_ready_seq != 0 && g_split_ready_word != nullptr;
+  if (publish) {   // the flags this split publishes: one word per row
+    g_ready_flag = g_split_ready_word;
+    g_ready_flag_ld = 1;
+  }
   hipLaunchKernelGGL(split_query_kernel, dim3((unsigned)(B + extra)), dim3(512), 0, st, Q, lq, w->qhi, w->qlo,
                      ix->resid_max, ix->norm_max, w->beta, w->count, reinterpret_cast<uint32_t*>(w->lb), w->done,
                      count0, w->arrive, kArriveSlots * kArriveInts, zero_ctr ? w->ctr : nullptr,
-                     zero_ctr ? kRingInts : 0, w->arrive != nullptr ? g_split_ready_seq : 0u, B, zkeys, nz);
+                     zero_ctr ? kRingInts : 0, publish ? g_split_ready_seq : 0u, B, zkeys, nz,
+                     publish ? g_split_ready_word : nullptr);
   return launch_check("split_query_kernel");
 }
 
@@ -7436,10 +7463,7 @@ int rerank_f32_split(cbv2_index* ix, F32Ws& w, int32_t B, int32_t lq, const int3
     rw.raw = g_raw_mirror;
     g_raw_mirror_used = true;
   }
-  if (k == 0 && g_prescore_ready != nullptr) {   // the split it reads is another stream's
-    rw.ready = g_prescore_ready;
-    rw.ready_seq = g_prescore_ready_seq;
-  }
+
   if ((rc = launch_rescore(ix, &w, B, lq, cand, nullptr, C, C, raw, C, st, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
                            nullptr, nullptr, rw)))
     return rc;
@@ -7566,9 +7590,6 @@ int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t s
     w.qhi = sw.qhi;
     w.qlo = sw.qlo;
     arrive = arrive_row0(sw, kArrRerank, B);
-    if (g_prescore_ready_seq != 0) {   // on another stream than the split: wait for its flag
-      g_prescore_ready = arrive_row0(sw, kArrPhase1, B) + kSplitReady;
-    }
   } else if (g_prescore_ready_seq != 0) {
     return fail(CBV2_ESTATE, "stage-1 prescore: the search's query split is not in the workspace");
   } else {
@@ -7604,10 +7625,24 @@ int cbv2_host_result_copy(const void* words, uint32_t seq, int32_t B, int32_t k,
                      out_s, out_i, out_p);
   return launch_check("host_result_kernel");
 }
-void cbv2_set_split_ready(uint32_t seq) { g_split_ready_seq = seq; }
-void cbv2_set_prescore_ready(uint32_t seq) {
-  g_prescore_ready_seq = seq;
-  g_prescore_ready = nullptr;
+void cbv2_set_split_ready(uint32_t seq) {
+  g_split_ready_seq = seq;
+  if (seq == 0) g_split_ready_word = nullptr;
+}
+// around the stage-1 prescore (its queries' split must still be the search's)
+void cbv2_set_prescore_ready(uint32_t seq) { g_prescore_ready_seq = seq; }
+// before a search: publish seq to words (device pointer into the call's
+// mapped buffer: the faithful split one per row, a bf16 search word 0),
+// record where (cbv2_last_ready_flag)
+void cbv2_set_split_ready_begin(uint32_t seq, void* word) {
+  g_split_ready_seq = seq;
+  g_split_ready_word = (int32_t*)word;
+  g_ready_flag = nullptr;
+  g_ready_flag_ld = 0;
+}
+const void* cbv2_last_ready_flag(int64_t* ld) {
+  if (ld != nullptr) *ld = g_ready_flag_ld;
+  return g_ready_flag;
 }
 void cbv2_set_raw_mirror(void* p, uint32_t seq) {
   g_raw_mirror = Mirror{(uint64_t*)p, seq, 0};

@@ -43,6 +43,8 @@ extern "C" void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k);
 extern "C" int cbv2_final_mirror_used(void);
 extern "C" void cbv2_set_raw_mirror(void* p, uint32_t seq);
 extern "C" void cbv2_set_split_ready(uint32_t seq);
+extern "C" void cbv2_set_split_ready_begin(uint32_t seq, void* word);
+extern "C" const void* cbv2_last_ready_flag(int64_t* ld);
 extern "C" void cbv2_set_prescore_ready(uint32_t seq);
 extern "C" int cbv2_raw_mirror_used(void);
 extern "C" int cbv2_host_result_copy(const void* words, uint32_t seq, int32_t B, int32_t k, float* out_s, int32_t* out_i,
@@ -206,11 +208,13 @@ struct Pending {
   MappedBuf mb;
   bool ids_mirrored = false;
   uint32_t seq = 0;
-  uint32_t ready_seq = 0;   // the faithful search's split-ready flag value (0: none)
+  uint32_t ready_seq = 0;   // the search's ready-flag value (0: none) ...
+  const int32_t* ready = nullptr;   // ... and the host words it wrote it to (ready[0 .. ready_n))
+  int32_t ready_n = 0;
 };
 
-// Process-wide call tags of the split-ready flags (never 0): the flag lives in
-// the caller's workspace, which calls through different mapped buffers share.
+// Process-wide call tags of the ready flags (never 0): a pooled buffer's flag
+// words keep an earlier call's tag, which never equals a later call's.
 std::atomic<uint32_t> g_ready_seq{0};
 uint32_t next_ready_seq() {
   uint32_t v = g_ready_seq.fetch_add(1, std::memory_order_relaxed) + 1;
@@ -404,9 +408,28 @@ int wait_words(const uint64_t* w, size_t n, uint32_t seq, const char* what = "st
 // A one-shard call's mapped buffer, in 8-byte words: [B][k] stage-2 id words
 // | [B][k] their score words | [B][C] fused candidate words | [B][3 fk] final
 // words | [B][kb] stage-1 prescore words | [B][kb] stage-1 ids (int32) +
-// [B][kb] raw prescores (float), one word per pair.
+// [B][kb] raw prescores (float), one word per pair | ... | the search's ready
+// flags (int32, row b's at the last B words' first int) at the buffer's end.
 size_t mapped_words(int32_t B, int32_t k, int32_t C, int32_t fk, int32_t kb) {
-  return (size_t)B * (2 * (size_t)k + (size_t)C + 3 * (size_t)fk + 2 * (size_t)kb);
+  return (size_t)B * (2 * (size_t)k + (size_t)C + 3 * (size_t)fk + 2 * (size_t)kb + 1);
+}
+size_t ready_word_off(const MappedBuf& b, int32_t B) { return b.bytes / 8 - (size_t)B; }   // in 8-byte words
+
+// Whether the search has published its ready flags (every one reads seq),
+// polled for at most bound: the stage-1 prescore may then run on the second
+// stream (what it reads is complete) with no wait of its own in the kernel.
+bool flags_seen(const int32_t* f, int32_t n, uint32_t seq, std::chrono::microseconds bound) {
+  const volatile int32_t* vf = f;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int32_t i = 0; i < n;) {
+    if ((uint32_t)vf[i] == seq) {
+      ++i;
+      continue;
+    }
+    if (std::chrono::steady_clock::now() - t0 > bound) return false;
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return true;
 }
 
 constexpr int kHostRerankDeclined = 1;   // host_rerank: not taken, nothing enqueued
@@ -508,22 +531,28 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
     pd.seq = ++pd.mb.seq;
     if (pd.seq == 0) pd.seq = ++pd.mb.seq;
   }
-  // the stage-2 ids and (faithful: the host rerank takes them), B * k words
-  // further, their scores
-  cbv2_set_ids_mirror(mapped ? pd.mb.d : nullptr, pd.seq, kd.faithful ? (int64_t)B * k : 0);
+  // small batches on bf16 / faithful shards (the host rerank's candidates):
+  // the stage-2 ids and, B * k words further, their scores; the search's
+  // first launch publishes ready flags to the buffer's end (once the host has
+  // seen them, the stage-1 prescore can read the queries from another stream)
+  const bool host_rr = mapped && B <= kSpinMaxB && (kd.faithful || kd.dtype == CBV2_DTYPE_BF16);
+  cbv2_set_ids_mirror(mapped ? pd.mb.d : nullptr, pd.seq, host_rr ? (int64_t)B * k : 0);
+  pd.ready_seq = host_rr ? next_ready_seq() : 0;
+  cbv2_set_split_ready_begin(pd.ready_seq, host_rr ? (uint64_t*)pd.mb.d + ready_word_off(pd.mb, B) : nullptr);
   int rc;
-  if (kd.faithful) {
-    // the query split publishes a ready flag (the host rerank's prescore
-    // reads the split from another stream)
-    pd.ready_seq = mapped && B <= kSpinMaxB ? next_ready_seq() : 0;
-    cbv2_set_split_ready(pd.ready_seq);
+  if (kd.faithful)
     rc = cbv2_search_f32(ix, (const float*)Q, B, lq, k, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
                          L.base, L.stage2, L.s, L.ids, L.status, stream);
-    cbv2_set_split_ready(0);
-  }
-  else {
+  else
     rc = cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
+  int64_t ld = 0;
+  if (cbv2_last_ready_flag(&ld) != nullptr) {   // one flag per row (ld 1) or one for all (ld 0)
+    pd.ready = (const int32_t*)((const uint64_t*)pd.mb.h + ready_word_off(pd.mb, B));
+    pd.ready_n = ld != 0 ? B : 1;
+  } else {
+    pd.ready_seq = 0;   // this search's path wrote no flag: the GPU rerank
   }
+  cbv2_set_split_ready(0);
   pd.ids_mirrored = mapped && cbv2_ids_mirror_used() != 0;
   cbv2_set_ids_mirror(nullptr, 0, 0);
   if (mapped) {
@@ -561,14 +590,23 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
     cbv2_set_raw_mirror(dev(lxw), pd.seq);
     const int32_t* lxi_d = (const int32_t*)dev(lxi);
     float* lxf_d = (float*)dev(lxi + Bkb);
-    // on the second stream, waiting in the kernel for the split's flag: it
-    // runs while stage 2 scans.  Everything it reads or writes is done when
-    // the host has seen its last word (each workgroup's word is its last
-    // store), so neither stream needs to wait for the other.
+    // on the second stream once the host has seen the search's ready flags
+    // (the search is then past its first launch: the queries and their split
+    // are complete), so it runs while stage 2 scans; else after the search on
+    // its own stream.  No kernel waits for another stream's (an in-kernel
+    // wait there can hold the CUs the awaited kernel needs).  Everything it
+    // reads or writes is done when the host has seen its last word (each
+    // workgroup's word is its last store), so neither stream waits for the
+    // other.  The bound costs no latency: a flag still missing means stage
+    // 2's scan has not started, and the host waits for its results anyway.
+    const bool seen = flags_seen(pd.ready, pd.ready_n, pd.ready_seq, std::chrono::microseconds(2000));
     cbv2_set_prescore_ready(pd.ready_seq);
-    rc = cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP, B,
-                                      lq, lxi_d, kb, 0, L.rr, L.rerank, lxf_d, nullptr, nullptr, (const float*)Q,
-                                      side_stream(cbv2_index_device(ix)));
+    hipStream_t side = seen ? side_stream(cbv2_index_device(ix)) : st;
+    rc = kd.faithful ? cbv2_rerank_f32_after_search(ix, L.base, L.stage2,
+                                                    k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP, B, lq,
+                                                    lxi_d, kb, 0, L.rr, L.rerank, lxf_d, nullptr, nullptr,
+                                                    (const float*)Q, side)
+                     : cbv2_rerank_ws(ix, Q, B, lq, lxi_d, kb, 0, L.rr, L.rerank, lxf_d, nullptr, nullptr, side);
     cbv2_set_prescore_ready(0);
     const bool used = cbv2_raw_mirror_used() != 0;
     cbv2_set_raw_mirror(nullptr, 0);
@@ -736,7 +774,8 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
   // whole stage-1 list enqueued now (it runs right after stage 2 on the
   // stream, while the host waits and fuses), so the top final_k is picked
   // on the host: no rerank launch after the fusion, no round trip back
-  if (mirrored && g_host_rerank && B <= kSpinMaxB && kd.faithful && pd.ready_seq != 0 &&
+  if (mirrored && g_host_rerank && B <= kSpinMaxB && (kd.faithful || kd.dtype == CBV2_DTYPE_BF16) &&
+      pd.ready_seq != 0 &&
       mapped_words(B, k, C, final_k, kb) * 8 <= pd.mb.bytes && side_stream(ds.dev) != nullptr) {
     rc = host_rerank(ix, kd, Q, B, lq, k, lex_ids, kb, rrf_k, C, final_k, L, pd, out_scores, out_ids, out_pos, st,
                      host_s, host_i, host_p);

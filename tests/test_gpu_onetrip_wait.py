@@ -111,16 +111,21 @@ def test_mapped_buffers_pooled_and_device_restored(dev):
     assert devs == [dev.index or 0] * 8
 
 
-def test_faithful_host_rerank_threads(dev):
-    """The faithful host rerank (stage 2's scores + the stage-1 prescore on
-    each thread's second stream, the split-ready flag in each workspace)
-    under 8 threads x 40 calls, B = 1 and 4, host and device results: every
-    call equals the composed stages, and every one took the host rerank."""
-    N = 6000
+@pytest.mark.parametrize("kind", ["fp32", "bf16"])
+def test_host_rerank_threads(dev, kind):
+    """The host rerank (stage 2's scores + the stage-1 prescore on each
+    thread's second stream, waiting for the search's ready flag: the
+    faithful split's in the workspace, the bf16 search's in the call's
+    mapped buffer) under 8 threads x 40 calls, B = 1 and 4, host and device
+    results: every call equals the composed stages, and every one took the
+    host rerank.  (bf16: 70,000 dense docs -- the block-max select's one
+    launch, whose counter zeroing publishes the flag.)"""
+    N = 6000 if kind == "fp32" else 70_000
     L = _lib.lib()
-    Qf, _, tokens, doclens = _index(dev, N, 4, seed=13, dtype=torch.float32)
-    ix = ColbertIndex.faithful_f32(tokens, doclens)
-    Q1, Q4 = Qf[:1].to(dev).contiguous(), Qf.to(dev).contiguous()
+    Qf, _, tokens, doclens = _index(dev, N, 4, seed=13, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+    ix = ColbertIndex.faithful_f32(tokens, doclens) if kind == "fp32" else ColbertIndex(tokens, doclens)
+    qdt = torch.float32 if kind == "fp32" else torch.bfloat16
+    Q1, Q4 = Qf[:1].to(dev, qdt).contiguous(), Qf.to(dev, qdt).contiguous()
     bm = [np.stack([np.random.default_rng(b + 7 * B).permutation(N)[:K] for b in range(B)]).astype(np.int32)
           for B in (1, 4)]
     want = []
