@@ -435,7 +435,9 @@ bool flags_seen(const int32_t* f, int32_t n, uint32_t seq, std::chrono::microsec
 constexpr int kHostRerankDeclined = 1;   // host_rerank: not taken, nothing enqueued
 
 // Lab knob (cbv2_set_host_rerank, internal): 1 = the host rerank (default),
-// 0 = the GPU rerank after the fusion (pre-armed or launched).
+// 0 = the GPU rerank after the fusion (pre-armed or launched), 2 = the host
+// rerank with its prescore behind the search on the call's stream (the path
+// a late ready flag takes; the tests pin it).
 int g_host_rerank = 1;
 
 // The host rerank's select of one row: the C fused candidates' scores (stage
@@ -599,7 +601,8 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
     // workgroup's word is its last store), so neither stream waits for the
     // other.  The bound costs no latency: a flag still missing means stage
     // 2's scan has not started, and the host waits for its results anyway.
-    const bool seen = flags_seen(pd.ready, pd.ready_n, pd.ready_seq, std::chrono::microseconds(2000));
+    const bool seen =
+        g_host_rerank != 2 && flags_seen(pd.ready, pd.ready_n, pd.ready_seq, std::chrono::microseconds(2000));
     cbv2_set_prescore_ready(pd.ready_seq);
     hipStream_t side = seen ? side_stream(cbv2_index_device(ix)) : st;
     rc = kd.faithful ? cbv2_rerank_f32_after_search(ix, L.base, L.stage2,

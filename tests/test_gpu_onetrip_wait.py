@@ -113,13 +113,14 @@ def test_mapped_buffers_pooled_and_device_restored(dev):
 
 @pytest.mark.parametrize("kind", ["fp32", "bf16"])
 def test_host_rerank_threads(dev, kind):
-    """The host rerank (stage 2's scores + the stage-1 prescore on each
-    thread's second stream, waiting for the search's ready flag: the
-    faithful split's in the workspace, the bf16 search's in the call's
-    mapped buffer) under 8 threads x 40 calls, B = 1 and 4, host and device
-    results: every call equals the composed stages, and every one took the
-    host rerank.  (bf16: 70,000 dense docs -- the block-max select's one
-    launch, whose counter zeroing publishes the flag.)"""
+    """The host rerank (stage 2's scores + the stage-1 prescore, launched on
+    each thread's second stream once the host has seen the search's ready
+    flags in the call's mapped buffer: the faithful split's, one per row, or
+    the bf16 counter zeroing's) under 8 threads x 40 calls, B = 1 and 4, host
+    and device results: every call equals the composed stages, and every one
+    took the host rerank.  (bf16: 70,000 dense docs -- the block-max select's
+    one launch, whose counter zeroing publishes the flag.)  An in-kernel wait
+    for the flag on the second stream starved the search here (bf16)."""
     N = 6000 if kind == "fp32" else 70_000
     L = _lib.lib()
     Qf, _, tokens, doclens = _index(dev, N, 4, seed=13, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
@@ -197,3 +198,37 @@ def test_faithful_finish_resplits_after_foreign_split(dev):
         assert torch.equal(g, w), f"{name}: the rerank did not re-split Q after a foreign split"
     for b in range(B):
         assert set(got[1][b].tolist()) == set(planted[b].tolist())
+
+
+@pytest.mark.parametrize("kind", ["fp32", "bf16"])
+def test_host_rerank_late_flag_path(dev, kind):
+    """The host rerank's other prescore placement -- behind the search on the
+    call's own stream, the path a ready flag not seen within its bound takes
+    (lab knob cbv2_set_host_rerank(2) forces it): the same results as the
+    composed stages, host and device, and the host rerank counted."""
+    N = 6000 if kind == "fp32" else 70_000
+    L = _lib.lib()
+    Qf, _, tokens, doclens = _index(dev, N, 4, seed=17, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+    ix = ColbertIndex.faithful_f32(tokens, doclens) if kind == "fp32" else ColbertIndex(tokens, doclens)
+    qdt = torch.float32 if kind == "fp32" else torch.bfloat16
+    one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+    L.cbv2_set_host_rerank(2)
+    try:
+        for B in (1, 4):
+            Q = Qf[:B].to(dev, qdt).contiguous()
+            bi = np.stack([np.random.default_rng(b + 3 * B).permutation(N)[:K] for b in range(B)]).astype(np.int32)
+            _, ids = ix.search(Q, K)
+            cand = rrf_fuse(bi, ids.cpu().numpy(), rrf_k=60, C=C)
+            want = [x.cpu() for x in ix.rerank(Q, torch.from_numpy(cand).to(dev), KF)]
+            for host in (False, True):
+                st0 = (ctypes.c_int64 * 4)()
+                L.cbv2_retrieve_pool_stats(st0, 4)
+                out = one(Q, bi, host=host)
+                got = [torch.from_numpy(x) for x in out] if host else [x.cpu() for x in out]
+                for g, w, name in zip(got, want, ("scores", "ids", "positions")):
+                    assert torch.equal(g, w), f"{kind} B={B} host={host}: {name} differ"
+                st1 = (ctypes.c_int64 * 4)()
+                L.cbv2_retrieve_pool_stats(st1, 4)
+                assert int(st1[3]) == int(st0[3]) + 1, f"{kind} B={B}: not the host rerank"
+    finally:
+        L.cbv2_set_host_rerank(1)
