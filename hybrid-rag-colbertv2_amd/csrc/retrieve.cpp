@@ -714,6 +714,7 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
     for (size_t i = 0; i < (size_t)3 * B * fk; ++i) vf[i] = tag | ((i / fk) % 3 == 0 ? ninf_bits : 0xffffffffu);
   else
     g_host_rerank_calls.fetch_add(1, std::memory_order_relaxed);
+  mark(4);   // (the GPU rerank's "rerank enqueued" slot: the host select published)
   return rc;
 }
 

@@ -87,7 +87,7 @@ def run(a):
                 "finish_to_D2H_issued": med(lambda m: m["finish"][1] - m["finish"][0]),
                 "D2H_issued_to_wait_done": med(lambda m: m["finish"][2] - m["finish"][1]),
                 "fusion": med(lambda m: m["finish"][3] - m["finish"][2]),
-                "rerank_enqueue": med(lambda m: m["finish"][4] - m["finish"][3]),
+                "rerank_enqueue_or_host_select": med(lambda m: m["finish"][4] - m["finish"][3]),
                 "finish_tail": med(lambda m: m["finish"][5] - m["finish"][4]),
                 "finish_exit_to_python_exit": med(lambda m: m["exit"] - m["finish"][5]),
                 "python_exit_to_synced": med(lambda m: m["synced"] - m["exit"]),
@@ -141,7 +141,7 @@ def parse(d, scan_key, marks_path=None):
                        "begin returned (from first kernel start)": m["begun"] - t0,
                        "finish entered": f[0] - t0, "D2H issued": f[1] - t0,
                        "wait done - D2H copy end": f[2] - max(copies) if copies else None,
-                       "fusion": f[3] - f[2], "rerank enqueued - wait done": f[4] - f[2],
+                       "fusion": f[3] - f[2], "rerank enqueued / host select done - wait done": f[4] - f[2],
                        "finish exit - wait done": f[5] - f[2], "python exit - last kernel end": m["exit"] - last_end,
                        "synchronize returned - last kernel end": m["synced"] - last_end}
                 host.setdefault(m["leg"], []).append(row)
