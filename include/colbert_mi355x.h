@@ -565,7 +565,12 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    host (cbv2_rrf_fuse with rrf_k, first C), uploads the candidates and
  *    enqueues the rerank + select: out_scores f32 [B][final_k], out_ids
  *    int32 [B][final_k] (global ids), out_pos int32 [B][final_k] (position
- *    in the fused list), device, best first, -inf / -1 padded.
+ *    in the fused list), device, best first, -inf / -1 padded.  One shard,
+ *    B <= 8, bf16 / fp32-faithful: the rerank's scores are already known
+ *    (stage 2's own for its ids; a stage-1 prescore of the kb lists, launched
+ *    at finish entry on a second stream of the calling thread), so the host
+ *    picks the top final_k itself and a one-workgroup kernel copies it into
+ *    the device outputs (same results, bit for bit).
  *  workspace: device, 256-B aligned, cbv2_retrieve_workspace_bytes(index,
  *    comm, B, lq, k, kb, C) bytes, the same one for begin and finish;
  *    host_stage: host (pinned for asynchronous copies),
@@ -595,7 +600,8 @@ int cbv2_comm_loopback_init(int32_t nranks, cbv2_comm** out);
  *    stage 1 failed): returns its host buffer to the pool (no-op otherwise).
  * cbv2_retrieve_host_marks (diagnostic): host timestamps (steady_clock ns) of
  *    this thread's last finish: enter, D2H issued, wait done, fusion done,
- *    rerank enqueued, exit (max entries written, up to 6).
+ *    rerank enqueued (the host rerank: its select done), exit (max entries
+ *    written, up to 6).
  * cbv2_retrieve_pool_stats (diagnostic): [0] mapped buffers created in this
  *    process, [1] buffers idle in the pools (at most the number of calls that
  *    ever ran at once), [2] finish_host calls whose results were read from the
