@@ -48,6 +48,7 @@ if os.path.exists(out_path):
     with open(out_path) as f:
         old = json.load(f)
     key = (kernel, dtype, batch, docs, variant)
+    doc.update({k: v for k, v in old.items() if k != "entries"})   # other sections kept as they are
     doc["entries"] = [x for x in old.get("entries", [])
                       if (x["kernel"], x.get("dtype"), x.get("batch"), x.get("docs_per_gpu"),
                           x.get("variant", "unfused")) != key]
