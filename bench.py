@@ -70,6 +70,7 @@ PEAK_FP8_TFLOPS = 5000.0                   # MI355X dense fp8 (block-scaled MFMA
 FLOP_PER_PAIR = 2 * LQ * LD * DIM          # 1,048,576 algorithmic FLOP per (query, doc)
 PEAK_BF16_TFLOPS = 2500.0                  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+NOMINAL_GHZ = 2.4                          # the clock the dense peaks are quoted at (MI355X_MICROARCH.md: max clock)
 JSON_FD = 1                                # set in main(): the real stdout, for the JSON line only
 SCAN_KERNEL = "maxsim_scan16x4_kernel"    # the B=256 scan (auto dispatch: doc-interleaved tiles, 32 queries / workgroup)
 
@@ -186,6 +187,22 @@ def timed_steps(run_steps, K, W, world, on_start=None):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     return outs, elapsed
+
+
+def clock_view(flop_per_launch, avg_ms, peak_tflops, clock_ghz, nominal_ghz=NOMINAL_GHZ):
+    """The roofline fraction split into this run's held clock and the MFMA
+    busy fraction at that clock: frac = (clock / nominal) x busy, so
+    flop_per_launch / (busy x peak x clock / nominal) reproduces avg_ms.
+    clock_ghz: the scans' in-kernel clock probe of the timed region
+    (cbv2_index_scan_clock); None -> no split."""
+    achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
+    if not clock_ghz:
+        return {"clock_ghz_this_run": None, "mfma_busy_this_run": None}
+    peak_at_clock = peak_tflops * clock_ghz / nominal_ghz
+    busy = achieved / peak_at_clock
+    return {"clock_ghz_this_run": round(clock_ghz, 4), "peak_tflops_at_this_clock": round(peak_at_clock, 1),
+            "mfma_busy_this_run": round(busy, 4),
+            "avg_ms_from_clock_and_busy": round(flop_per_launch / (busy * peak_at_clock * 1e12) * 1e3, 3)}
 
 
 def main_line(qps, ms_per_step, p50, p99, native, native_is_main):
@@ -431,11 +448,11 @@ def main():
 
     def step(srch, Qb, lexical):
         """One batch, unpipelined (used for the B=1 latency)."""
-        _, ids, bm = srch.search_hybrid(Qb, args.k, lexical)
+        _, ids, bm, pool = srch.search_hybrid(Qb, args.k, lexical, return_pool=True)
         bm = bm.cpu().numpy() if isinstance(bm, torch.Tensor) else bm
         cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=args.fused)
         cand_d = torch.from_numpy(cand).to(dev, non_blocking=False)
-        return srch.rerank(Qb, cand_d, args.final_k)
+        return srch.rerank(Qb, cand_d, args.final_k, pool=pool)   # sharded: scores from the pool, no collective
 
     def stepper(srch, Qb):
         # K batches through the software-pipelined path (batch j+1's scan runs on
@@ -479,9 +496,13 @@ def main():
     # each search's band work) are bracketed by HIP events recorded on their own
     # stream by the C ABI (cbv2_index_time_scans); the collective times are
     # read from a separate untimed pass below, not from the timed region
-    ix.time_scans(True)
-    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world)
+    # (+ the doc-interleaved scans' in-kernel clock probe, reset after the
+    # warmup: the clock the K timed scans held)
+    ix.time_scans(True, clock=True)
+    outs, elapsed = timed_steps(stepper(searcher, Q), args.steps, args.warmup, world,
+                                on_start=lambda: ix.scan_clock(reset=True))
     scan_ms = ix.scan_times()                           # the warmup + K scans; keep the K of the timed region
+    scan_clk = ix.scan_clock()
     scan_ms = scan_ms[-args.steps:] if len(scan_ms) >= args.steps else scan_ms
     band_ms = ix.band_times()[-args.steps:] if faithful else []
     qps = B * args.steps / elapsed
@@ -530,7 +551,7 @@ def main():
     fused_topk = ix.fused_topk_slots(B, args.k) > 0
     # HBM bytes per launch from the committed PMC passes of the same kernel and
     # shape (tools/profile_round.sh -> tools/pmc_summary.py); null otherwise
-    traffic = clock = traffic_src = mfma_busy = None
+    traffic = clock = traffic_src = mfma_busy = pmc_ref = None
     pmc = os.path.join(ROOT, "profiles", "pmc_scan.json")
     want = "maxsim_scan_f8x4_kernel" if fp8 else SCAN_KERNEL
     variant = "fused" if fused_topk else "unfused"
@@ -547,6 +568,10 @@ def main():
                     mfma_busy = busy / (1024 * gui / 8)
                 traffic_src = (f"committed PMC pass profiles/pmc_scan.json ({want}, {variant}, batch {B}, "
                                f"{n_local} docs/GPU, one MI355X), not this run")
+                pmc_ref = {"clock_ghz": round(clock, 3) if clock else None,
+                           "mfma_busy": round(mfma_busy, 4) if mfma_busy else None, "source": traffic_src}
+    clk_view = clock_view(B * n_local * FLOP_PER_PAIR, scan_avg, PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS,
+                          scan_clk["clock_ghz"])
     # every rank's scan time and collective time per step (max-over-ranks view of N > 1)
     names = ("all_gather", "all_reduce_max")
     mine = [scan_avg] + [coll.get(k, {}).get(f, 0.0) for k in names for f in ("device_ms", "host_ms")] \
@@ -736,8 +761,12 @@ def main():
                          "band_ms_note": ("fp32-faithful band work per step (HIP events in the timed region: end "
                                           "of the bf16 top-k -> end of the band select), rank 0; not part of avg_ms"
                                           if faithful else None),
-                         "clock_ghz_under_load": round(clock, 3) if clock else None,
-                         "mfma_busy_at_that_clock": round(mfma_busy, 4) if mfma_busy else None},
+                         **clk_view,
+                         "clock_source": (f"in-kernel probe of the {len(scan_ms)} timed scans: sum of workgroup "
+                                          f"s_memtime cycles / s_memrealtime ticks over {scan_clk['workgroups']} "
+                                          "workgroups (cbv2_index_scan_clock)"
+                                          if scan_clk["clock_ghz"] else None),
+                         "pmc_reference": pmc_ref},
             "cpu_baseline": cpu,
             "checks": {"top10_equals_planted": top10_planted, "sorted": sorted_ok, "oracle_mismatch_queries": bad,
                        "oracle_checked_queries": len(check_rows), "oracle_tolerance": tol},

@@ -40,6 +40,7 @@ _SIGS = {
     "cbv2_index_time_scans": (ctypes.c_int, [_p, _i32]),
     "cbv2_index_scan_times": (ctypes.c_int, [_p, _p, _i32, ctypes.POINTER(ctypes.c_int32)]),
     "cbv2_index_band_times": (ctypes.c_int, [_p, _p, _i32, ctypes.POINTER(ctypes.c_int32)]),
+    "cbv2_index_scan_clock": (ctypes.c_int, [_p, _p, _i32]),
     "cbv2_index_create_mxfp8": (ctypes.c_int, [ctypes.c_int, _p, _p, _i64, _i32, _i32, _p, _i64,
                                                ctypes.POINTER(ctypes.c_void_p)]),
     "cbv2_quantize_mxfp8": (ctypes.c_int, [_p, _i32, _i64, _p, _p, _p]),
@@ -90,8 +91,12 @@ _SIGS = {
     "cbv2_search_sharded": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _sz, _p, _p,
                                            _p, _p]),
     "cbv2_search_sharded_local": (ctypes.c_int, [_p, _p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _sz, _p]),
-    "cbv2_search_sharded_exchange": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _p, _i32, _p, _sz, _p, _p, _p, _p]),
+    "cbv2_search_sharded_exchange": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p, _sz, _p,
+                                                    _p, _p, _p]),
     "cbv2_rerank_sharded": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p, _p]),
+    "cbv2_rerank_sharded_prescored": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _i32, _i32, _p, _sz, _p, _p, _p,
+                                                     _p, _p]),
+    "cbv2_comm_stats": (ctypes.c_int, [_p, _p]),
     "cbv2_bm25_destroy": (ctypes.c_int, [_p]),
     "cbv2_split_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _p]),
     "cbv2_index_attach_residual": (ctypes.c_int, [_p, _p, ctypes.c_float, ctypes.c_float]),

@@ -874,6 +874,9 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // A wave waits only for what it reads or overwrites, so the partner waves
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
+#ifndef CBV2_F8_D47
+#define CBV2_F8_D47 1   // lab A/B builds set 3
+#endif
 #ifndef CBV2_SCAN_QSKIP
 #define CBV2_SCAN_QSKIP 1   // lab A/B builds set 0
 #endif
@@ -887,6 +890,21 @@ constexpr bool kScanQSkip = CBV2_SCAN_QSKIP != 0;
 // -- a group of a range that does not start on a block boundary spans two
 // blocks (and at most two superblocks), so its two parts go separately.  The
 // keys equal block_max_kernel's.
+// The bench's clock probe (cbv2_index_time_scans(ix, 2), product kernels,
+// a runtime-null pointer otherwise): each workgroup adds (end - start) of
+// s_memtime (shader clock) and s_memrealtime (100 MHz) to p[0] / p[1] (start
+// subtracted at entry, end added at exit: nothing held across the loop) and
+// counts its entry / exit in p[2] / p[3]; sum(dt) / sum(dr) x 0.1 GHz is the
+// clock the launch's workgroups held, weighted by their run time.  The stamp
+// waits its own lgkmcnt inside the asm (no LDS read is in flight here).
+__device__ __forceinline__ void clock_probe(uint64_t* p, bool end) {
+  unsigned long long t, r;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "=s"(r)::"memory");
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), end ? t : 0ull - t);
+  atomicAdd(reinterpret_cast<unsigned long long*>(p) + 1, end ? r : 0ull - r);
+  atomicAdd(reinterpret_cast<unsigned long long*>(p) + (end ? 3 : 2), 1ull);
+}
+
 template <int WAVES, int QW, int D = 2, int NBUF = 3, bool STAMPS = false, int TPI = 32, int OCC = 2,
           bool SPREAD = false, int FK = 0, bool SPLITLOAD = false, bool ARRIVE = false, int PROBE = 0, int LD = kLd,
           int MORDER = 0, int AUX = 0, bool BMK = false>
@@ -946,6 +964,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   if constexpr (STAMPS) {
     t_start = __builtin_amdgcn_s_memtime();
     r_start = __builtin_amdgcn_s_memrealtime();
+  } else {
+    if (stamps != nullptr && threadIdx.x == 0) clock_probe(stamps, false);   // product: the clock probe
   }
 
   bf16x8 qf[QW][2][4];
@@ -1220,6 +1240,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       if (qi >= B) continue;
       topk_flush(cand + q * FK, tk_state + q * kFusedStateBytes, topk_k,
                  part + ((size_t)qi * nslots + (size_t)chunk) * topk_k, lane);
+    }
+  }
+  if constexpr (!STAMPS) {
+    if (stamps != nullptr) {   // block-uniform
+      __syncthreads();
+      if (threadIdx.x == 0) clock_probe(stamps, true);
     }
   }
   if constexpr (STAMPS) {
@@ -2031,7 +2057,9 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
     const uint8_t* __restrict__ tokens, const uint8_t* __restrict__ tscales, const int32_t* __restrict__ doclens,
     int64_t n, const uint8_t* __restrict__ Qb, const uint8_t* __restrict__ Qs, int B, int lq,
     float* __restrict__ out, int64_t ld_out, int64_t chunk_docs, int64_t static_docs, int* __restrict__ task_ctr,
-    int task_docs, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0, int tail_slices = 1) {
+    int task_docs, int topk_k = 0, uint64_t* __restrict__ part = nullptr, int nslots = 0, int tail_slices = 1,
+    uint64_t* __restrict__ clk = nullptr) {
+  if (clk != nullptr && threadIdx.x == 0) clock_probe(clk, false);   // the bench's clock probe (null otherwise)
   constexpr int QPB = WAVES * QW;
   constexpr int kIterBytes = 4 * TPI * kDim;                 // e4m3 bytes per iteration
   constexpr int kIterStage = kIterBytes + 4 * TPI * 2;        // + 2 scale bytes per row
@@ -2268,6 +2296,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan_f8x4_kernel(
       topk_flush(cand + q * FK, tk_state + q * kFusedStateBytes, topk_k,
                  part + ((size_t)qi * nslots + (size_t)chunk) * topk_k, lane);
     }
+  }
+  if (clk != nullptr) {   // block-uniform
+    __syncthreads();
+    if (threadIdx.x == 0) clock_probe(clk, true);
   }
 }
 
@@ -2729,13 +2761,27 @@ struct Mirror {
 // written by the host after the launch.  Thread 0 of a workgroup polls its
 // candidate's word (system-scope loads, s_sleep between polls) until the tag
 // is the call's seq -- so the host's fusion -> rerank hop costs a PCIe read,
-// not a kernel launch.  It never waits forever: after kCandWaitTicks of
-// s_memrealtime (100 MHz) the candidate reads as -1 (scores -inf), and the
+// not a kernel launch.  It never waits forever: after `ticks` of
+// s_memrealtime (100 MHz; kCandWaitTicks = 1 s) it gives up through the
+// call's wait gate (below) and the candidate reads as -1 (scores -inf); the
 // host, which writes the words whatever happens (-1 words on its own
-// failure), reports an error then.
+// failure), then fails the call.
+//
+// The wait gate: two tagged words of the call's mapped buffer, gate[0]
+// written by a kernel that is about to give up, gate[1] by the host just
+// before it publishes the words the kernel waits for.  Each side stores its
+// own word, fences (seq_cst, system scope), then loads the other's (Dekker):
+// of a kernel that gave up (read no host word) and a host that then
+// published, at least one read the other's -- so a host whose load misses
+// the kernel's word knows no kernel gave up, and a kernel that reads the
+// host's word withdraws and waits on (kBackstopTicks: the host is past its
+// last wait and writing).  A host that reads the kernel's word fails the call
+// (CBV2_EHIP): no call returns after a timed-out device wait.
 struct TaggedCand {
   const uint64_t* w = nullptr;
   uint32_t seq = 0;
+  uint64_t* gate = nullptr;   // [0] kernel's word, [1] host's word (nullable: a timeout gives up at once)
+  uint64_t ticks = 0;         // the wait's bound (s_memrealtime ticks)
 };
 
 // The FINAL top-k of a retrieve call, also written to host memory by the
@@ -2755,15 +2801,43 @@ struct FinalMirror {
     __hip_atomic_store(row + 2 * k + r, t | (uint32_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 };
-constexpr uint64_t kCandWaitTicks = 100000000ull;   // 1 s
-__device__ __forceinline__ int32_t wait_tagged(const uint64_t* w, uint32_t seq) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+constexpr uint64_t kCandWaitTicks = 100000000ull;    // 1 s
+constexpr uint64_t kBackstopTicks = 3000000000ull;   // 30 s: the host committed to publish (gate) yet nothing came
+// Added to a row's band count by a collect workgroup whose wait for phase 1
+// gave up: above any real count (<= k + n < 2^28), so the row overflows.
+constexpr int32_t kWaitTimedOut = 1 << 28;
+// The kernel's side of the wait gate: true = give up (the host had not
+// committed to publish), false = the host is publishing: wait on.
+__device__ __forceinline__ bool gate_give_up(uint64_t* gate, uint32_t seq) {
+  if (gate == nullptr) return true;
+  const uint64_t t = ((uint64_t)seq << 32) | 1u;
+  __hip_atomic_store(gate, t, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  return __hip_atomic_load(gate + 1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM) != t;
+}
+// Polls one tagged word until it carries seq; -1 once the gate says give up.
+__device__ __forceinline__ bool poll_tagged(const uint64_t* w, uint32_t seq, uint64_t* gate, uint64_t ticks,
+                                            uint64_t* out) {
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool committed = false;
   for (;;) {
     const uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if ((uint32_t)(v >> 32) == seq) return (int32_t)(uint32_t)v;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > kCandWaitTicks) return -1;
+    if ((uint32_t)(v >> 32) == seq) {
+      *out = v;
+      return true;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      if (committed || gate_give_up(gate, seq)) return false;
+      committed = true;   // the host is writing: a generous bound of its own
+      ticks = kBackstopTicks;
+      t0 = __builtin_amdgcn_s_memrealtime();
+    }
     __builtin_amdgcn_s_sleep(2);
   }
+}
+__device__ __forceinline__ int32_t wait_tagged(const uint64_t* w, const TaggedCand& tc) {
+  uint64_t v;
+  return poll_tagged(w, tc.seq, tc.gate, tc.ticks, &v) ? (int32_t)(uint32_t)v : -1;
 }
 // The latency path's final top-k picked by the HOST (retrieve.cpp's host
 // rerank: every fused candidate's score is already known -- stage 2's own, or
@@ -2771,21 +2845,17 @@ __device__ __forceinline__ int32_t wait_tagged(const uint64_t* w, uint32_t seq) 
 // launched before the host has the result, polls its tagged words in the
 // call's mapped buffer (FinalMirror's layout: per row [k] score, [k] id, [k]
 // position words) and writes the device outputs.  A word that never comes
-// (kCandWaitTicks) is written -inf / -1.
+// (ticks, then the wait gate) is written -inf / -1 and the host fails the call.
 __global__ __launch_bounds__(256) void host_result_kernel(const uint64_t* __restrict__ w, uint32_t seq, int B, int k,
                                                           float* __restrict__ out_s, int32_t* __restrict__ out_i,
-                                                          int32_t* __restrict__ out_p) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                                                          int32_t* __restrict__ out_p, uint64_t* gate,
+                                                          uint64_t ticks) {
+  bool gave_up = false;   // (one give-up per thread: its later words are not waited for)
   for (int i = threadIdx.x; i < 3 * B * k; i += blockDim.x) {
     const int b = i / (3 * k), r = i - b * 3 * k;
-    uint64_t v;
-    bool ok;
-    for (;;) {
-      v = __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      ok = (uint32_t)(v >> 32) == seq;
-      if (ok || __builtin_amdgcn_s_memrealtime() - t0 > kCandWaitTicks) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
+    uint64_t v = 0;
+    const bool ok = !gave_up && poll_tagged(w + i, seq, gate, ticks, &v);
+    gave_up = !ok;
     const uint32_t x = (uint32_t)v;
     if (r < k)
       out_s[(size_t)b * k + r] = ok ? __uint_as_float(x) : neg_inf();
@@ -3584,6 +3654,94 @@ __global__ __launch_bounds__(256) void select_small_kernel(const float* __restri
                   out_p ? out_p + b * k : nullptr, fin, b);
 }
 
+// The sharded stage 3 without a collective (sharded.cpp,
+// cbv2_rerank_sharded_prescored): every fused candidate's rerank score is
+// already in the stage-2 all-gather -- its owner's local top-k list (the
+// scan's / band's score of the doc: the rerank's bits, test_gpu_fp8 /
+// DESIGN §3.7) or its owner's stage-1 prescore (the rerank of the rank's own
+// BM25 top-kb, run before the all-gather).  Row b of the gathered blocks
+// (rank g's block at recv + g * blk words: [B][k] scores | [B][k] ids | [B][kb]
+// BM25 scores | [B][kb] BM25 ids | [B][kb] prescores): the row's candidates go
+// into an LDS id table (open addressing), every gathered (id, score) entry
+// probes it, and the row's top-k is selected as select_small_kernel does
+// (score desc, position asc).  A candidate found nowhere (not from these
+// lists) scores -inf and is counted in *misses; a negative id scores -inf,
+// as the rerank scores it.  C <= kSmallMax.
+constexpr int kPreTab = 2 * kSmallMax;   // id table slots (a power of two >= 2 C)
+__global__ __launch_bounds__(256) void prescored_select_kernel(
+    const int32_t* __restrict__ recv, int G, int64_t blk, int B, int k, int kb, const int32_t* __restrict__ cand,
+    int C, int fk, float* __restrict__ out_s, int32_t* __restrict__ out_i, int32_t* __restrict__ out_p,
+    int32_t* __restrict__ misses) {
+  __shared__ float sc[kSmallMax];
+  __shared__ uint64_t keys[kSmallMax];
+  __shared__ int32_t tab_id[kPreTab];
+  __shared__ uint32_t tab_sc[kPreTab];
+  __shared__ int32_t tab_hit[kPreTab];
+  const int b = blockIdx.x;
+  const int32_t* crow = cand + (size_t)b * C;
+  int bits = 4;
+  while ((1 << bits) < 2 * C) ++bits;
+  const uint32_t mask = (1u << bits) - 1;
+  auto slot0 = [&](int32_t id) { return ((uint32_t)id * 2654435761u) >> (32 - bits); };
+  for (int t = threadIdx.x; t <= (int)mask; t += blockDim.x) {
+    tab_id[t] = -1;
+    tab_hit[t] = 0;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < C; t += blockDim.x) {   // the row's candidates (duplicates share a slot)
+    const int32_t id = crow[t];
+    if (id < 0) continue;
+    for (uint32_t h = slot0(id);; h = (h + 1) & mask) {
+      const int32_t prev = atomicCAS(&tab_id[h], -1, id);
+      if (prev == -1 || prev == id) break;
+    }
+  }
+  __syncthreads();
+  const int per = k + kb;
+  for (int e = threadIdx.x; e < G * per; e += blockDim.x) {   // every gathered (id, score) of row b
+    const int g = e / per, j = e - g * per;
+    const int32_t* base = recv + (size_t)g * blk;
+    int32_t id;
+    uint32_t sb;
+    if (j < k) {
+      id = base[(size_t)B * k + (size_t)b * k + j];
+      sb = (uint32_t)base[(size_t)b * k + j];
+    } else {
+      const size_t jj = (size_t)b * kb + (j - k);
+      id = base[2 * (size_t)B * k + (size_t)B * kb + jj];
+      sb = (uint32_t)base[2 * (size_t)B * k + 2 * (size_t)B * kb + jj];
+    }
+    if (id < 0) continue;
+    for (uint32_t h = slot0(id);; h = (h + 1) & mask) {
+      const int32_t t = tab_id[h];
+      if (t == -1) break;
+      if (t == id) {   // (an id in both of its owner's lists carries the same bits in each)
+        tab_sc[h] = sb;
+        tab_hit[h] = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  int miss = 0;
+  for (int t = threadIdx.x; t < C; t += blockDim.x) {
+    const int32_t id = crow[t];
+    float v = neg_inf();
+    if (id >= 0) {
+      uint32_t h = slot0(id);
+      while (tab_id[h] != id) h = (h + 1) & mask;
+      if (tab_hit[h]) v = __uint_as_float(tab_sc[h]);
+      else ++miss;
+    }
+    sc[t] = v;
+    keys[t] = rank_key(v, (uint32_t)t);
+  }
+  if (miss != 0 && misses != nullptr) atomicAdd(misses, miss);
+  __syncthreads();
+  select_from_lds(sc, keys, C, fk, crow, out_s + (size_t)b * fk, out_i + (size_t)b * fk,
+                  out_p ? out_p + (size_t)b * fk : nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Rerank: one workgroup per query; each wave gathers whole candidate docs
 // (32 KiB, contiguous) straight into VGPRs and scores them with the same MFMA
@@ -3772,7 +3930,7 @@ __global__ __launch_bounds__(256, 2) void rerank_split_kernel(
   const int b = blockIdx.y, c = blockIdx.x;
   int32_t id;
   if (tc.w != nullptr) {   // pre-armed: the host writes the candidate after this launch
-    if (threadIdx.x == 0) s_cid = wait_tagged(tc.w + (size_t)b * C + c, tc.seq);
+    if (threadIdx.x == 0) s_cid = wait_tagged(tc.w + (size_t)b * C + c, tc);
     __syncthreads();
     id = s_cid;
   } else {
@@ -4337,7 +4495,7 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
       topk_exact_row(row, n, kk, sel, hist, &s_bin, &s_above, &s_bincount, &s_cnt);
       sort_and_write(sel, kk, fb_k, id_base, fb_s + (size_t)b * fb_k, fb_i + (size_t)b * fb_k,
                      rs.ids_mirror.row(b, fb_k));
-      if (rs.mode == kSelBand && threadIdx.x == 0) rs.status[b] = -1;
+      if (rs.mode == kSelBand && threadIdx.x == 0) rs.status[b] = cb >= kWaitTimedOut ? -2 : -1;
       return;
     }
   }
@@ -4351,7 +4509,7 @@ __global__ __launch_bounds__(NW * 64, 2) void rescore_split_kernel(
       int64_t id;
       if (tc.w != nullptr) {   // pre-armed (the latency path's rerank): the host writes the candidate after the launch
         if (threadIdx.x == 0) {
-          s_cid = wait_tagged(tc.w + (size_t)b * ld_c + c, tc.seq);
+          s_cid = wait_tagged(tc.w + (size_t)b * ld_c + c, tc);
           // handed to the row select through device memory (cand: the
           // caller's device array, unread on this path), not re-read from host
           if (rs.mode != kSelNone)
@@ -4940,10 +5098,11 @@ __global__ __launch_bounds__(256, 2) void phase1_collect_kernel(
     const int32_t* __restrict__ topk_i, const float* __restrict__ topk_s, int k, float* __restrict__ F,
     int64_t ld_F, uint32_t* __restrict__ lbu, int32_t* __restrict__ done1, int64_t done_ld,
     const float* __restrict__ T, const float* __restrict__ beta, const uint32_t* __restrict__ bm, int cap,
-    int32_t* __restrict__ cand, int32_t* __restrict__ count, uint64_t* __restrict__ stamps = nullptr) {
+    int32_t* __restrict__ cand, int32_t* __restrict__ count, uint64_t wait_ticks,
+    uint64_t* __restrict__ stamps = nullptr) {
   __shared__ float s_m[4][32];
   __shared__ int32_t s_ids[kBandLds];
-  __shared__ int s_n, s_base;
+  __shared__ int s_n, s_base, s_timed_out;
   __shared__ uint32_t s_lb;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -5017,15 +5176,25 @@ __global__ __launch_bounds__(256, 2) void phase1_collect_kernel(
       for (int e = 0; e < 4; ++e) v[s4][e] = i0[s4] + e < n ? row[i0[s4] + e] : 0.0f;
     }
   }
-  // phase 1 of row b done: thread 0 polls (sc1), the barrier releases the rest
+  // phase 1 of row b done: thread 0 polls (sc1), the barrier releases the rest.
+  // The poll is bounded (wait_ticks; 0 = give up at once, the tests' knob): a
+  // workgroup that gives up knows no lb, so it marks its row overflowed with
+  // kWaitTimedOut -- the row then takes the full faithful scan in the
+  // rescoring launch (exact whatever phase 1 did) and reports status -2.
   if (threadIdx.x == 0) {
     const int32_t* d = done1 + (size_t)b * done_ld + 32 * ((x - k) % kP1Replicas);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int)__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k &&
-           __builtin_amdgcn_s_memrealtime() - t0 < kCandWaitTicks)
+    bool done = false;
+    for (;;) {
+      done = (int)__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k;
+      if (done || wait_ticks == 0 || __builtin_amdgcn_s_memrealtime() - t0 >= wait_ticks) break;
       __builtin_amdgcn_s_sleep(4);
+    }
+    s_timed_out = done ? 0 : 1;
+    if (!done) atomicAdd(count + b, kWaitTimedOut);
   }
   __syncthreads();
+  if (s_timed_out) return;   // block-uniform
   {   // lb = min over the k faithful scores (sc1 loads), as the atomic min has it
     uint32_t mn = ~0u;
     for (int j = threadIdx.x; j < k; j += blockDim.x) mn = min(mn, f2u(ld_sc1(F + (size_t)b * ld_F + j)));
@@ -5477,6 +5646,8 @@ struct cbv2_index {
   // launch is bracketed by a pair of HIP events recorded on its own stream;
   // the pairs are reused across enable cycles and destroyed with the handle.
   bool time_scans = false;
+  uint64_t* clk = nullptr;   // the scans' clock probe sums (cbv2_index_time_scans(ix, 2)), device [4]
+  bool clock_on = false;
   size_t scan_ev_used = 0;
   std::vector<hipEvent_t> scan_ev;  // [2 * i] start, [2 * i + 1] stop
   // Band timing (same switch): a faithful search's work after the bf16 top-k
@@ -5710,6 +5881,7 @@ thread_local Mirror g_ids_mirror;
 thread_local bool g_ids_mirror_used = false;
 // ... and its pre-armed rerank's candidates (cbv2_retrieve_finish sets them
 // around its rerank call): a rerank that can take them sets g_cand_tagged_used.
+thread_local uint64_t g_wait_ticks = kCandWaitTicks;   // cbv2_set_wait_ticks (lab knob)
 thread_local TaggedCand g_cand_tagged;
 thread_local bool g_cand_tagged_used = false;
 // The final result's host words (cbv2_set_final_mirror, set by retrieve.cpp
@@ -5745,6 +5917,9 @@ thread_local uint64_t* g_lab_stamps = nullptr;
 #else
 #define LAB_STAMPS(kind) ((uint64_t*)nullptr)
 #endif
+// The clock probe the scan launched next passes its workgroups (set by
+// scan_maxsim_timed while the handle's probe is on; nullptr otherwise).
+thread_local uint64_t* g_clock_probe = nullptr;
 thread_local int g_ctr_policy = kCtrDefault;
 thread_local bool g_ctr_zeroed = false;
 struct CtrPolicy {
@@ -5876,7 +6051,8 @@ int launch_scan16x4(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out
   hipLaunchKernelGGL((maxsim_scan16x4_kernel<WAVES, QW, D, NBUF, STAMPS, TPI, OCC, SPREAD, FK, SPLITLOAD, ARRIVE, PROBE, LD, MORDER,
                                              AUX, BMK>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->doclens,
-                     ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs, stamps,
+                     ix->n, Q, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr, sp.task_docs,
+                     STAMPS ? stamps : g_clock_probe,
                      ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices, bm,
                      bm_blocks(ix->n), bm != nullptr ? bm_super_keys(bm, B, ix->n) : nullptr, bm_supers(ix->n));
   if ((rc = launch_check("maxsim_scan16x4_kernel"))) return rc;
@@ -6016,6 +6192,31 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     variant = pick_shape(kBf16Shapes, B);
   }
   switch (variant) {
+    case kScan16x4W4Q1:     // 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
+      if (B <= 4 && bm != nullptr)   // the block keys folded in (zeroed by the caller: scan_folds_bmax_zeroed)
+        return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2, true>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws, nullptr, bm);
+      if (B <= 4)           // one query group: every doc byte is read once (non-temporal)
+        return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
+      return launch_scan16x4<4, 1, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
+    case kScan16x4W8:   // SPLITLOAD: lab, same box, 1M / 125k / B=64: 145.25 -> 144.10, 18.14 -> 17.97, 37.98 -> 37.53 ms
+      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac,
+                                                                          kScanTaskDocs, nullptr, ctr_ws);
+    case kScan16x4W4:
+      if (B <= 16)          // one query group: non-temporal doc stream
+        return launch_scan16x4<4, 4, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs, nullptr, ctr_ws);
+      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
+    case kScan16x4W4Q2:   // 8 queries per workgroup (2 per wave)
+      if (B <= 8)         // one query group: non-temporal doc stream
+        return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
+      return launch_scan16x4<4, 2, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
+                                                   nullptr, ctr_ws);
+#ifdef CBV2_LAB   // variants tools/scan_lab.hip A/Bs (the product never dispatches them: its library leaves them out)
     case kScanDirectQ1:
       return launch_direct<1>(ix, Q, B, lq, out, ld_out, st);
     case kScanDirectQ2:
@@ -6068,16 +6269,6 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
     case kScan16x4W8Q1x2:   // lab: the same, two workgroups per CU
       return launch_scan16x4<8, 1, 2, 2, 2, false, 32, 4>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB,
                                                           kScanTaskDocs, nullptr, ctr_ws);
-    case kScan16x4W4Q1:     // 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
-      if (B <= 4 && bm != nullptr)   // the block keys folded in (zeroed by the caller: scan_folds_bmax_zeroed)
-        return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2, true>(
-            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws, nullptr, bm);
-      if (B <= 4)           // one query group: every doc byte is read once (non-temporal)
-        return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
-            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
-      return launch_scan16x4<4, 1, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
-                                                   nullptr, ctr_ws);
-
     case kScan32Shfl:
       return launch_scan<4, 4, 2>(maxsim_scan_kernel<4, 4, false>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan_kernel");
     case kScan32Dpp:
@@ -6096,21 +6287,7 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
       return launch_scan<8, 3, 1>(maxsim_scan16_kernel<8, 3>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
     case kScan16W4Q2:
       return launch_scan<4, 2, 2>(maxsim_scan16_kernel<4, 2>, ix, Q, B, lq, out, ld_out, st, "maxsim_scan16_kernel");
-    case kScan16x4W8:   // SPLITLOAD: lab, same box, 1M / 125k / B=64: 145.25 -> 144.10, 18.14 -> 17.97, 37.98 -> 37.53 ms
-      return launch_scan16x4<8, 4, 1, 2, 2, false, 64, 2, false, 0, true>(ix, Q, B, lq, out, ld_out, st, kScanDynFrac,
-                                                                          kScanTaskDocs, nullptr, ctr_ws);
-    case kScan16x4W4:
-      if (B <= 16)          // one query group: non-temporal doc stream
-        return launch_scan16x4<4, 4, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
-            ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs, nullptr, ctr_ws);
-      return launch_scan16x4<4, 4, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracB16, kScanTaskDocs,
-                                                   nullptr, ctr_ws);
-    case kScan16x4W4Q2:   // 8 queries per workgroup (2 per wave)
-      if (B <= 8)         // one query group: non-temporal doc stream
-        return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
-            ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws);
-      return launch_scan16x4<4, 2, 2, 2, 2, false>(ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs,
-                                                   nullptr, ctr_ws);
+#endif
     default:
       return fail(CBV2_EINVAL, "unknown scan variant %d", variant);
   }
@@ -6142,6 +6319,10 @@ constexpr int kF8Waves = 8, kF8QW = 8;
 // -> 70.98 ms, B=64 19.19 -> 18.77, B=32 10.26 -> 10.17, B=16 5.73 -> 5.71,
 // B=8 3.73 -> 3.65.
 constexpr int kF8D = 3;
+// ... except the 4-wave shapes 7 and 8 (4 x 4 at three workgroups per CU, 4
+// x 8 at two): fold distance 1, where 3 spilled 2 VGPRs (12 B of scratch per
+// lane) -- the max is exact, so the bits do not depend on the distance
+constexpr int kF8D47 = CBV2_F8_D47;
 // Dynamic share of the MXFP8 scans (dyn_frac = kF8DynAuto picks it per shape):
 // the 4-wave shapes hand more of the corpus to the ticket tail.  Lab, same
 // process, 1M docs (profiles/r02s3_lab_dynfrac_f8.log): B=16 (4 x 4, three
@@ -6173,7 +6354,8 @@ int launch_f8x4(cbv2_index* ix, const uint8_t* Qb, const uint8_t* Qs, int B, int
                                               AUX>),
                      dim3((unsigned)(nq_groups * sp.n_chunks)), dim3(WAVES * 64), 0, st, ix->tokens, ix->scales,
                      ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, sp.chunk_docs, sp.static_docs, sp.ctr,
-                     sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices);
+                     sp.task_docs, ft ? ft->k : 0, ft ? ft->part : nullptr, ft ? (int)ft->max_slots : 0, sp.slices,
+                     g_clock_probe);
   if ((rc = launch_check("maxsim_scan_f8x4_kernel"))) return rc;
   return finish_split(ix, sp, st);
 }
@@ -6235,12 +6417,17 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     if (ft != nullptr || shape != 0) return fail(CBV2_EUNSUPPORTED, "long-doc index: automatic scan only");
     return scan_f8_long(ix, Qb, Qs, B, lq, out, ld_out, st, ctr_ws);
   }
-  if (ft != nullptr)   // fused top-k: the production B > 8 doc-interleaved shape only (fused_eligible)
+#ifdef CBV2_LAB   // fused top-k on MXFP8 (A/B only: its build spills; fused_slots never picks it in the product)
+  if (ft != nullptr)
     return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, kFusedCap>(ix, Qb, Qs, B, lq, nullptr, 0, st,
                                                                       frac(kScanDynFrac), task_docs, ctr_ws, ft);
+#else
+  if (ft != nullptr) return fail(CBV2_EUNSUPPORTED, "fused top-k: not built for MXFP8 indexes");
+#endif
   // dense docs (CBV2_OPT_DENSE_DOCS): B <= 2 too on the 4 x 1 shape (every slot streamed)
   if ((B > kF8DirectMaxB || ix->dense_docs) && shape == 0) shape = pick_shape(kF8Shapes, B);
   if (B <= kF8DirectMaxB && shape == 0) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);
+#ifdef CBV2_LAB   // shapes tools/scan_lab.hip A/Bs (the product's library leaves them out)
   if (B <= kF8DirectMaxB && shape == 25) return launch_f8_stream(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 19) return launch_f8_stream<4, 16, false>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
   if (B <= kF8DirectMaxB && shape == 21) return launch_f8_stream<16, 4, false>(ix, Qb, Qs, B, lq, out, ld_out, st);  // lab
@@ -6261,6 +6448,7 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
                        ix->scales, ix->doclens, ix->n, Qb, Qs, B, lq, out, ld_out, chunk_docs, kLd);
     return launch_check("maxsim_scan_f8_direct_kernel");
   }
+#endif
   // shape: 0 = auto (above); 5 = 8 waves x 8 queries, 32-token iterations,
   // two per barrier (PAIR, round 3: lab, same process, bit-identical, 1M docs
   // B=256 73.95 -> 73.28 ms, 1.25M 92.39 -> 91.75, B=64 19.28 -> 19.20;
@@ -6270,25 +6458,20 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
   // 2-deep (2-4 spill at 8 queries per wave), 6 = 2 with PF, 10 = 9 with
   // three workgroups per CU.
   switch (shape) {
-    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
-    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
-    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
-    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     case 5: return launch_f8x4<32, 4, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true, true>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
-    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 4-wave workgroups (32-token / 3-deep, PF): 7 = 4 queries per wave, three
     // workgroups per CU (3 waves per SIMD); 8 = 8 queries per wave, two per CU
     // (2 waves per SIMD from independent barrier domains); 9 = 2 queries per
     // wave, two per CU
     case 7:
       if (B <= 16)   // one query group: non-temporal doc stream
-        return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true, false, false, false, false, 0, 2>(
+        return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D47, true, false, false, false, false, 0, 2>(
             ix, Qb, Qs, B, lq, out, ld_out, st, frac(kF8DynSmall), task_docs, ctr_ws);
-      return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
-                                                                     frac(kF8DynSmall), task_docs, ctr_ws);
-    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4, 0, kLd, kF8D, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
-                                                                            frac(kF8DynSmall), task_docs, ctr_ws);
+      return launch_f8x4<32, 3, true, 4, 3, 3, 4, 0, kLd, kF8D47, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                       frac(kF8DynSmall), task_docs, ctr_ws);
+    case 8: return launch_f8x4<32, 3, true, 8, 2, 2, 4, 0, kLd, kF8D47, true>(ix, Qb, Qs, B, lq, out, ld_out, st,
+                                                                              frac(kF8DynSmall), task_docs, ctr_ws);
     case 9:
       if (B <= 8)    // one query group: non-temporal doc stream
         return launch_f8x4<32, 3, true, 2, 2, 2, 4, 0, kLd, kF8D, true, false, false, false, false, 0, 2>(
@@ -6298,10 +6481,15 @@ int scan_f8(cbv2_index* ix, const uint8_t* Qb, int B, int lq, float* out, int64_
     // 24 = 1 query per wave, two per CU (B = 3-4 without padded slots), non-temporal
     case 24: return launch_f8x4<32, 3, true, 1, 2, 2, 4, 0, kLd, 1, true, false, false, false, false, 0, 2>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kF8DynB8), task_docs, ctr_ws);
+#ifdef CBV2_LAB
+    case 1: return launch_f8x4<32, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 2: return launch_f8x4<64, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 3: return launch_f8x4<64, 3>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 4: return launch_f8x4<128, 2>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
+    case 6: return launch_f8x4<64, 2, true>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 12 = shape 5 before PAIR: one 32-token iteration per barrier, 3-deep ring
     case 12: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, kF8D, true>(
         ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
-#ifdef CBV2_LAB
     case 10: return launch_f8x4<32, 3, true, 2, 3, 3, 4>(ix, Qb, Qs, B, lq, out, ld_out, st, frac(kScanDynFrac), task_docs, ctr_ws);
     // 11 = shape 5 as it was before the packed scales and D = 3 (round 2)
     case 11: return launch_f8x4<32, 3, true, kF8QW, 1, 2, kF8Waves, 0, kLd, 1, false>(ix, Qb, Qs, B, lq, out, ld_out,
@@ -6338,6 +6526,9 @@ int64_t fused_slots(const cbv2_index* ix, int32_t scorer, int32_t B, int32_t k) 
   // VGPR file): 78.1 vs 74.1 ms at 1M, B=256 (profiles/r02b_fused_ab.jsonl),
   // so MXFP8 searches stay unfused; CBV2_OPT_FUSED_TOPK = 2 forces it (A/B).
   if (ix->dtype == CBV2_DTYPE_MXFP8) {
+#ifndef CBV2_LAB
+    return 0;   // (lab builds: CBV2_OPT_FUSED_TOPK = 2 forces it)
+#endif
     if (B <= kF8SmallMaxB || ix->fused_topk_mode < 2) return 0;
     return scan_chunks(ix, (B + kF8Waves * kF8QW - 1) / (kF8Waves * kF8QW), cu_count(ix->device));
   }
@@ -6447,9 +6638,11 @@ int scan_maxsim_timed(cbv2_index* ix, const void* Q, int32_t B, int32_t lq, floa
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timed = scan_event_pair(ix, &e0, &e1);
   if (timed && hipEventRecord(e0, st) != hipSuccess) return fail(CBV2_EHIP, "hipEventRecord failed");
+  g_clock_probe = timed && ix->clock_on ? ix->clk : nullptr;
   const int rc = ix->dtype == CBV2_DTYPE_MXFP8
                      ? scan_f8(ix, (const uint8_t*)Q, B, lq, out, ld_out, st, kF8DynAuto, kScanTaskDocs, 0, ctr_ws, ft)
                      : scan_maxsim(ix, (const uint16_t*)Q, B, lq, out, ld_out, st, kDefaultScan, ctr_ws, ft, bm);
+  g_clock_probe = nullptr;
   // the stop event is recorded even after a failed launch, so the reserved pair stays readable
   if (timed && hipEventRecord(e1, st) != hipSuccess && rc == CBV2_OK) return fail(CBV2_EHIP, "hipEventRecord failed");
   return rc;
@@ -6709,8 +6902,10 @@ int launch_rescore(cbv2_index* ix, const F32Ws* w, int B, int lq, const int32_t*
     const int64_t grid_auto = std::min<int64_t>(kRsSplitGrid, std::max<int64_t>(256, 4096 / std::max(B, 1)));
     const int64_t grid_max = ix->rescore_grid > 0 ? ix->rescore_grid : grid_auto;
     const unsigned gx = (unsigned)(span < grid_max ? span : grid_max);
-    const bool two = (int64_t)gx * B > 3LL * cu_count(ix->device);
-    auto kern = ix->ld != kLd ? (two ? rescore_split_kernel<true, 2> : rescore_split_kernel<true, 4>)
+    // (long documents keep 4 waves: the 2-wave build of the long-doc pair
+    // carries its row maxima across blocks and spills; same bits either way)
+    const bool two = ix->ld == kLd && (int64_t)gx * B > 3LL * cu_count(ix->device);
+    auto kern = ix->ld != kLd ? rescore_split_kernel<true, 4>
                               : (two ? rescore_split_kernel<false, 2> : rescore_split_kernel<false, 4>);
     hipLaunchKernelGGL(kern, dim3(gx, (unsigned)B), dim3(two ? 128 : 256), 0, st, ix->tokens, ix->resid, ix->doclens,
                        ix->n, ix->id_base, w->qhi, w->qlo, lq, cand, count, limit, ld_c, out, ld_out, only_neg,
@@ -6842,10 +7037,11 @@ int cbv2_hbm_free(int device, void* p) {
 }
 
 int cbv2_index_destroy(cbv2_index* index) {
-  if (index != nullptr && (index->task_ring != nullptr || !index->scan_ev.empty())) {
+  if (index != nullptr && (index->task_ring != nullptr || !index->scan_ev.empty() || index->clk != nullptr)) {
     int prev = 0;
     if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(index->device) == hipSuccess) {
       if (index->task_ring != nullptr) (void)hipFree(index->task_ring);
+      if (index->clk != nullptr) (void)hipFree(index->clk);
       for (hipEvent_t e : index->ring_ev)
         if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : index->scan_ev) (void)hipEventDestroy(e);
@@ -6859,9 +7055,31 @@ int cbv2_index_destroy(cbv2_index* index) {
 
 int cbv2_index_time_scans(cbv2_index* ix, int32_t enable) {
   CBV2_REQUIRE(ix != nullptr, "null index");
+  CBV2_REQUIRE(enable >= 0 && enable <= 2, "enable must be 0, 1 or 2 (got %d)", enable);
   std::lock_guard<std::mutex> lk(ix->mu);
   if (enable) ix->scan_ev_used = ix->band_ev_used = 0, ix->band_open = false;
+  if (enable == 2) {
+    DeviceGuard dg(ix->device);
+    if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+    if (ix->clk == nullptr) CBV2_HIP(hipMalloc(&ix->clk, 4 * sizeof(uint64_t)));
+    CBV2_HIP(hipMemset(ix->clk, 0, 4 * sizeof(uint64_t)));
+  }
   ix->time_scans = enable != 0;
+  ix->clock_on = enable == 2;
+  return CBV2_OK;
+}
+int cbv2_index_scan_clock(cbv2_index* ix, int64_t* out4, int32_t reset) {
+  CBV2_REQUIRE(ix != nullptr && out4 != nullptr, "null index or output");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  for (int i = 0; i < 4; ++i) out4[i] = 0;
+  if (ix->clk == nullptr) return CBV2_OK;
+  DeviceGuard dg(ix->device);
+  if (!dg.ok) return fail(CBV2_EHIP, "cannot select device %d", ix->device);
+  CBV2_HIP(hipDeviceSynchronize());
+  uint64_t v[4];
+  CBV2_HIP(hipMemcpy(v, ix->clk, sizeof(v), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 4; ++i) out4[i] = (int64_t)v[i];
+  if (reset) CBV2_HIP(hipMemset(ix->clk, 0, 4 * sizeof(uint64_t)));
   return CBV2_OK;
 }
 
@@ -7165,6 +7383,20 @@ int cbv2_select_topk(const float* scores, const int32_t* ids, int32_t B, int32_t
   return launch_check("select_small_kernel");
 }
 
+// Internal (sharded.cpp): the prescored select of the sharded stage 3
+// (prescored_select_kernel; C <= kSmallMax, misses nullable).
+int cbv2_prescored_select(const int32_t* recv, int32_t G, int64_t blk, int32_t B, int32_t k, int32_t kb,
+                          const int32_t* cand, int32_t C, int32_t fk, float* out_s, int32_t* out_i, int32_t* out_p,
+                          int32_t* misses, void* stream) {
+  CBV2_REQUIRE(recv && cand && out_s && out_i, "null blocks / candidates / outputs");
+  CBV2_REQUIRE(G >= 1 && B >= 1 && k >= 1 && kb >= 0 && fk >= 1, "bad sizes (G %d, B %d, k %d, kb %d, k %d)", G, B,
+               k, kb, fk);
+  CBV2_REQUIRE(C >= 1 && C <= kSmallMax, "prescored select: C must be in [1, %d] (got %d)", kSmallMax, C);
+  hipLaunchKernelGGL(prescored_select_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, recv, G, blk, B,
+                     k, kb, cand, C, fk, out_s, out_i, out_p, misses);
+  return launch_check("prescored_select_kernel");
+}
+
 int cbv2_split_f32(const float* x, int64_t rows, int32_t ld, const int32_t* doclens, void* hi, void* lo,
                    float* bounds, void* stream) {
   CBV2_REQUIRE(rows >= 0, "rows must be >= 0");
@@ -7316,7 +7548,7 @@ int search_f32_phase2_impl(cbv2_index* ix, int32_t B, int32_t lq, int32_t k, int
                        ix->tokens, ix->resid, ix->doclens, ix->n, ix->id_base, w.qhi, w.qlo, lq, out_ids, out_scores,
                        k, w.F, (int64_t)cap, const_cast<uint32_t*>(lbu), arrive_row0(w, kArrPhase1, B),
                        (int64_t)kArriveInts, w.T, w.beta, reinterpret_cast<const uint32_t*>(w.tk), cap, w.cand,
-                       w.count, LAB_STAMPS(1));
+                       w.count, g_wait_ticks, LAB_STAMPS(1));
     if ((rc = launch_check("phase1_collect_kernel"))) return rc;
   } else if (B <= kBandPairMaxB && ix->ld == kLd && ix->band_fused) {
     // the latency path: collect + rescore in one launch, one band doc per wave
@@ -7609,10 +7841,14 @@ void cbv2_set_ids_mirror(void* p, uint32_t seq, int64_t score_off) {
   g_ids_mirror_used = false;
 }
 int cbv2_ids_mirror_used(void) { return g_ids_mirror_used ? 1 : 0; }
-void cbv2_set_cand_tagged(const void* p, uint32_t seq) {
-  g_cand_tagged = TaggedCand{(const uint64_t*)p, seq};
+void cbv2_set_cand_tagged(const void* p, uint32_t seq, void* gate) {
+  g_cand_tagged = TaggedCand{(const uint64_t*)p, seq, (uint64_t*)gate, g_wait_ticks};
   g_cand_tagged_used = false;
 }
+// Lab knob (retrieve.cpp's cbv2_set_wait_lab, this thread): the bound of the
+// in-kernel waits on host words and on phase 1 (s_memrealtime ticks; < 0:
+// the default 1 s, 0: give up at once).
+void cbv2_set_wait_ticks(int64_t ticks) { g_wait_ticks = ticks < 0 ? kCandWaitTicks : (uint64_t)ticks; }
 int cbv2_cand_tagged_used(void) { return g_cand_tagged_used ? 1 : 0; }
 void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k) {
   g_final_mirror = p != nullptr ? FinalMirror{(uint64_t*)p, seq, (int)k} : FinalMirror();
@@ -7620,9 +7856,9 @@ void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k) {
 }
 int cbv2_final_mirror_used(void) { return g_final_mirror_used ? 1 : 0; }
 int cbv2_host_result_copy(const void* words, uint32_t seq, int32_t B, int32_t k, float* out_s, int32_t* out_i,
-                          int32_t* out_p, void* stream) {
+                          int32_t* out_p, void* gate, void* stream) {
   hipLaunchKernelGGL(host_result_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (const uint64_t*)words, seq, B, k,
-                     out_s, out_i, out_p);
+                     out_s, out_i, out_p, (uint64_t*)gate, g_wait_ticks);
   return launch_check("host_result_kernel");
 }
 void cbv2_set_split_ready(uint32_t seq) {

@@ -37,7 +37,8 @@ extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_w
 extern "C" int cbv2_index_device(const cbv2_index* ix);
 extern "C" void cbv2_set_ids_mirror(void* p, uint32_t seq, int64_t score_off);
 extern "C" int cbv2_ids_mirror_used(void);
-extern "C" void cbv2_set_cand_tagged(const void* p, uint32_t seq);
+extern "C" void cbv2_set_cand_tagged(const void* p, uint32_t seq, void* gate);
+extern "C" void cbv2_set_wait_ticks(int64_t ticks);
 extern "C" int cbv2_cand_tagged_used(void);
 extern "C" void cbv2_set_final_mirror(void* p, uint32_t seq, int32_t k);
 extern "C" int cbv2_final_mirror_used(void);
@@ -48,7 +49,7 @@ extern "C" const void* cbv2_last_ready_flag(int64_t* ld);
 extern "C" void cbv2_set_prescore_ready(uint32_t seq);
 extern "C" int cbv2_raw_mirror_used(void);
 extern "C" int cbv2_host_result_copy(const void* words, uint32_t seq, int32_t B, int32_t k, float* out_s, int32_t* out_i,
-                                     int32_t* out_p, void* stream);
+                                     int32_t* out_p, void* gate, void* stream);
 
 namespace {
 int err(int code, const char* fmt, ...) {
@@ -363,13 +364,18 @@ HostLayout host_layout(void* h, int32_t B, int32_t k, int32_t kb, int32_t C) {
   return H;
 }
 
-// Stage 3 of one call: the sharded rerank (all-reduce MAX), the faithful
+// Stage 3 of one call: the sharded one (the fused candidates' scores looked
+// up in the exchange's gathered blocks: no collective; kb = this call's
+// stage-1 width, as the exchange laid out the workspace), the faithful
 // rerank on begin's query split, or the bf16 / MXFP8 one.
 int rerank_call(cbv2_index* ix, cbv2_comm* c, Kind kd, const void* Q, int32_t B, int32_t lq, int32_t k,
-                const Layout& L, const int32_t* cand, int32_t C, int32_t final_k, float* out_scores,
+                int32_t kb, const Layout& L, const int32_t* cand, int32_t C, int32_t final_k, float* out_scores,
                 int32_t* out_ids, int32_t* out_pos, hipStream_t st) {
   if (c)
-    return cbv2_rerank_sharded(ix, c, Q, B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos, st);
+    return C <= 1024 ? cbv2_rerank_sharded_prescored(ix, c, B, k, kb, cand, C, final_k, L.base, L.stage2, out_scores,
+                                                     out_ids, out_pos, nullptr, st)
+                     : cbv2_rerank_sharded(ix, c, Q, B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids,
+                                           out_pos, st);
   if (kd.faithful)   // the search's query split (begin, same stream) serves the rerank when it is still there
     return cbv2_rerank_f32_after_search(ix, L.base, L.stage2, k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP,
                                         B, lq, cand, C, final_k, L.rr, L.rerank, out_scores, out_ids, out_pos,
@@ -387,33 +393,68 @@ std::atomic<int64_t> g_host_rerank_calls{0};
 // fusion (no tagged candidates), 1 = pre-armed (default).
 int g_prearm = 1;
 
-// Polls the call's tagged stage-2 id words until every one carries seq (the
-// search's last kernel writes them; written whole, in any order).  Never
-// waits forever: a GPU that never writes them (a fault) fails the call after
-// 2 s.
-int wait_words(const uint64_t* w, size_t n, uint32_t seq, const char* what = "stage-2 results") {
+// Polls the call's tagged words until every one carries seq (a kernel on
+// stream st writes them; written whole, in any order).  No wall-clock
+// deadline (a call queued behind other work, or on a shared GPU, is slow,
+// not failed): flat out for kSpinNs, then sleeping between polls (1/32 of the
+// time waited, 20-500 us) and asking the stream -- an error on it fails the
+// call, and a stream that completed without writing every word too.
+int wait_words(const uint64_t* w, size_t n, uint32_t seq, hipStream_t st, const char* what = "stage-2 results") {
   const volatile uint64_t* vw = w;
   const auto t0 = std::chrono::steady_clock::now();
+  bool drained = false;   // the stream had completed at the last query
   for (size_t i = 0; i < n;) {
     if ((uint32_t)(vw[i] >> 32) == seq) {
       ++i;
       continue;
     }
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
-      return err(CBV2_EHIP, "%s did not arrive (2 s)", what);
+    if (drained) return err(CBV2_EHIP, "%s: the stream completed without writing them", what);
+    const long long waited =
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (waited <= kSpinNs) continue;
+    std::this_thread::sleep_for(std::chrono::nanoseconds(std::min(500000LL, std::max(20000LL, waited / 32))));
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      drained = true;   // every word must be there now: one more pass decides
+    } else if (q != hipErrorNotReady) {
+      return err(CBV2_EHIP, "%s: stream error while waiting (%d)", what, (int)q);
+    }
   }
   return CBV2_OK;
+}
+
+// The host's side of the wait gate of the in-kernel waits on host words
+// (colbert_mi355x.hip, TaggedCand): the host's word, a seq_cst fence, the
+// kernels' word.  true = no kernel gave up before this commit, so every
+// waiting kernel takes the words the host publishes next; false = one gave
+// up (its outputs are -inf / -1): the call must fail.
+bool gate_commit(uint64_t* gate, uint32_t seq) {
+  const uint64_t t = ((uint64_t)seq << 32) | 1u;
+  __atomic_store_n(gate + 1, t, __ATOMIC_SEQ_CST);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  return __atomic_load_n(gate, __ATOMIC_SEQ_CST) != t;
+}
+
+// Lab knob (cbv2_set_wait_lab, this thread): the host sleeps this long before
+// it commits and publishes the words a kernel waits for (with a short
+// in-kernel bound, the tests force each device-side timeout once).
+thread_local int32_t t_lab_publish_delay_us = 0;
+void lab_publish_delay() {
+  if (t_lab_publish_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(t_lab_publish_delay_us));
 }
 
 // A one-shard call's mapped buffer, in 8-byte words: [B][k] stage-2 id words
 // | [B][k] their score words | [B][C] fused candidate words | [B][3 fk] final
 // words | [B][kb] stage-1 prescore words | [B][kb] stage-1 ids (int32) +
-// [B][kb] raw prescores (float), one word per pair | ... | the search's ready
-// flags (int32, row b's at the last B words' first int) at the buffer's end.
+// [B][kb] raw prescores (float), one word per pair | ... | the wait gate (2
+// words) | the search's ready flags (int32, row b's at the last B words'
+// first int) at the buffer's end.
 size_t mapped_words(int32_t B, int32_t k, int32_t C, int32_t fk, int32_t kb) {
-  return (size_t)B * (2 * (size_t)k + (size_t)C + 3 * (size_t)fk + 2 * (size_t)kb + 1);
+  return (size_t)B * (2 * (size_t)k + (size_t)C + 3 * (size_t)fk + 2 * (size_t)kb + 1) + 2;
 }
 size_t ready_word_off(const MappedBuf& b, int32_t B) { return b.bytes / 8 - (size_t)B; }   // in 8-byte words
+size_t gate_word_off(const MappedBuf& b, int32_t B) { return ready_word_off(b, B) - 2; }
 
 // Whether the search has published its ready flags (every one reads seq),
 // polled for at most bound: the stage-1 prescore may then run on the second
@@ -478,6 +519,13 @@ int cbv2_retrieve_host_marks(int64_t* out, int32_t max) {
 }
 
 void cbv2_set_wait_mode(int32_t mode) { g_wait_mode = mode; }
+// Lab knob (tests): this thread's in-kernel wait bound (ticks of 10 ns; < 0
+// the default 1 s, 0 give up at once) and the host's delay before it
+// publishes what those kernels wait for.
+void cbv2_set_wait_lab(int64_t ticks, int32_t publish_delay_us) {
+  cbv2_set_wait_ticks(ticks);
+  t_lab_publish_delay_us = publish_delay_us;
+}
 void cbv2_set_host_rerank(int32_t on) { g_host_rerank = on; }
 void cbv2_set_prearm(int32_t on) { g_prearm = on; }
 
@@ -538,6 +586,11 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   // first launch publishes ready flags to the buffer's end (once the host has
   // seen them, the stage-1 prescore can read the queries from another stream)
   const bool host_rr = mapped && B <= kSpinMaxB && (kd.faithful || kd.dtype == CBV2_DTYPE_BF16);
+  if (host_rr) {   // a pooled buffer's flag slots may hold any earlier call's words: cleared before the search
+    volatile uint64_t* fl = (uint64_t*)pd.mb.h + ready_word_off(pd.mb, B);
+    for (int32_t b = 0; b < B; ++b) fl[b] = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+  }
   cbv2_set_ids_mirror(mapped ? pd.mb.d : nullptr, pd.seq, host_rr ? (int64_t)B * k : 0);
   pd.ready_seq = host_rr ? next_ready_seq() : 0;
   cbv2_set_split_ready_begin(pd.ready_seq, host_rr ? (uint64_t*)pd.mb.d + ready_word_off(pd.mb, B) : nullptr);
@@ -585,7 +638,9 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
   uint64_t* const lxw = fw + (size_t)3 * B * fk;
   int32_t* const lxi = (int32_t*)(lxw + Bkb);
   auto dev = [&](const void* h) { return (uint8_t*)pd.mb.d + ((const uint8_t*)h - (const uint8_t*)pd.mb.h); };
+  uint64_t* const gate = (uint64_t*)pd.mb.h + gate_word_off(pd.mb, B);
   int rc = CBV2_OK;
+  hipStream_t pre = st;   // the stream the stage-1 prescore went to
   // 1. stage 1's prescore: the rerank's raw scores of the whole stage-1 list
   if (kb > 0) {
     std::memcpy(lxi, lex_ids, Bkb * 4);
@@ -605,6 +660,7 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
         g_host_rerank != 2 && flags_seen(pd.ready, pd.ready_n, pd.ready_seq, std::chrono::microseconds(2000));
     cbv2_set_prescore_ready(pd.ready_seq);
     hipStream_t side = seen ? side_stream(cbv2_index_device(ix)) : st;
+    pre = side;
     rc = kd.faithful ? cbv2_rerank_f32_after_search(ix, L.base, L.stage2,
                                                     k > CBV2_RETRIEVE_BAND_CAP ? k : CBV2_RETRIEVE_BAND_CAP, B, lq,
                                                     lxi_d, kb, 0, L.rr, L.rerank, lxf_d, nullptr, nullptr,
@@ -620,13 +676,13 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
     if (!rc && !used) rc = err(CBV2_ESTATE, "stage-1 prescore without host words");
   }
   // 2. the device outputs: a copy launched now, polling the final words
-  if (!rc) rc = cbv2_host_result_copy(dev(fw), pd.seq, B, fk, out_scores, out_ids, out_pos, st);
+  if (!rc) rc = cbv2_host_result_copy(dev(fw), pd.seq, B, fk, out_scores, out_ids, out_pos, dev(gate), st);
   const bool copy_armed = rc == CBV2_OK;
   mark_mapped(pd.mb, st);   // every reader of the buffer is enqueued
   mark(1);
   // 3. the round trip: stage 2's ids and scores, stage 1's prescores
-  if (!rc) rc = wait_words(idw, 2 * Bk, pd.seq);
-  if (!rc && kb > 0) rc = wait_words(lxw, Bkb, pd.seq, "stage-1 prescores");
+  if (!rc) rc = wait_words(idw, 2 * Bk, pd.seq, st);
+  if (!rc && kb > 0) rc = wait_words(lxw, Bkb, pd.seq, pre, "stage-1 prescores");
   mark(2);
   thread_local std::vector<int32_t> ids_s, cand_s;
   ids_s.resize(Bk);
@@ -643,12 +699,29 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
   const float ninf = -std::numeric_limits<float>::infinity();
   uint32_t ninf_bits;
   std::memcpy(&ninf_bits, &ninf, 4);
+  // a failed call: the prescore on the second stream may still read the
+  // buffer (and Q): the call's stream waits for it before the buffer is
+  // marked free again
+  auto fence_side = [&]() {
+    if (kb <= 0 || pre == st) return;
+    thread_local hipEvent_t ev[kMaxDev] = {};
+    const int d = cbv2_index_device(ix);
+    if (d < 0 || d >= kMaxDev) return;
+    if ((ev[d] == nullptr && hipEventCreateWithFlags(&ev[d], hipEventDisableTiming) != hipSuccess) ||
+        hipEventRecord(ev[d], pre) != hipSuccess || hipStreamWaitEvent(st, ev[d], 0) != hipSuccess)
+      (void)hipStreamSynchronize(pre);
+    mark_mapped(pd.mb, st);
+  };
   if (rc) {   // the armed copy must not wait for its timeout: publish -inf / -1
     if (copy_armed)
       for (size_t i = 0; i < (size_t)3 * B * fk; ++i)
         vf[i] = tag | ((i / fk) % 3 == 0 ? ninf_bits : 0xffffffffu);
+    fence_side();
     return rc;
   }
+  lab_publish_delay();
+  // the copy kernel's wait gate: committed before the first final word (below)
+  const bool gate_ok = gate_commit(gate, pd.seq);
   int bits = 4;
   while ((1 << bits) < 2 * (k + kb)) ++bits;
   const uint32_t hmask = (1u << bits) - 1;
@@ -712,6 +785,9 @@ int host_rerank(cbv2_index* ix, Kind kd, const void* Q, int32_t B, int32_t lq, i
   }
   if (rc)   // (a row failed: every word still gets published)
     for (size_t i = 0; i < (size_t)3 * B * fk; ++i) vf[i] = tag | ((i / fk) % 3 == 0 ? ninf_bits : 0xffffffffu);
+  else if (!gate_ok)
+    rc = err(CBV2_EHIP, "the device copy of the results gave up its wait before the host published them "
+                        "(device outputs are -inf / -1)");
   else
     g_host_rerank_calls.fetch_add(1, std::memory_order_relaxed);
   mark(4);   // (the GPU rerank's "rerank enqueued" slot: the host select published)
@@ -751,7 +827,9 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
       std::memcpy(H.lex_ids, lex_ids, (size_t)B * kb * 4);
       std::memcpy(H.lex_scores, lex_scores, (size_t)B * kb * 4);
     }
-    rc = cbv2_search_sharded_exchange(ix, c, B, k, kb > 0 ? H.lex_ids : nullptr,
+    // (with Q: this rank's BM25 top-kb prescored before the all-gather, so
+    // stage 3 needs no collective -- cbv2_rerank_sharded_prescored)
+    rc = cbv2_search_sharded_exchange(ix, c, Q, q_dtype, lq, B, k, kb > 0 ? H.lex_ids : nullptr,
                                       kb > 0 ? (const float*)H.lex_scores : nullptr, kb, L.base, L.stage2, L.s,
                                       L.ids, kb > 0 ? L.lex_ids : nullptr, st);
     if (rc) return rc;
@@ -806,17 +884,18 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
     rc = err(CBV2_EHIP, "stage-2 ids copy failed");
   mark(1);
   bool armed = false;
+  uint64_t* const gate = mapped ? (uint64_t*)pd.mb.h + gate_word_off(pd.mb, B) : nullptr;
   if (!rc && prearm) {
-    cbv2_set_cand_tagged(cwd, pd.seq);
+    cbv2_set_cand_tagged(cwd, pd.seq, (uint64_t*)pd.mb.d + gate_word_off(pd.mb, B));
     if (fwd) cbv2_set_final_mirror(fwd, pd.seq, final_k);
-    rc = rerank_call(ix, c, kd, Q, B, lq, k, L, L.cand, C, final_k, out_scores, out_ids, out_pos, st);
+    rc = rerank_call(ix, c, kd, Q, B, lq, k, kb, L, L.cand, C, final_k, out_scores, out_ids, out_pos, st);
     armed = cbv2_cand_tagged_used() != 0;   // else it read L.cand (any ids are range-checked): rerun below
     fin_used = armed && fwd && cbv2_final_mirror_used() != 0;
-    cbv2_set_cand_tagged(nullptr, 0);
+    cbv2_set_cand_tagged(nullptr, 0, nullptr);
     cbv2_set_final_mirror(nullptr, 0, 0);
   }
   // the one host round trip: the ColBERT (and merged BM25) top-k are here
-  if (!rc) rc = mirrored && B <= kSpinMaxB ? wait_words(idw, (size_t)B * k, pd.seq) : wait_copy(st, B);
+  if (!rc) rc = mirrored && B <= kSpinMaxB ? wait_words(idw, (size_t)B * k, pd.seq, st) : wait_copy(st, B);
   mark(2);
   thread_local std::vector<int32_t> ids_s, cand_s;
   const int32_t* ids_h = H.ids;
@@ -833,6 +912,12 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
   if (!rc) rc = cbv2_rrf_fuse(bm, kb, ids_h, k, B, rrf_k, C, cand_h, nullptr, nullptr);
   mark(3);
   if (armed) {   // always publish, failed or not: the armed rerank must not wait for its timeout
+    if (!rc) {
+      lab_publish_delay();
+      if (!gate_commit(gate, pd.seq))
+        rc = err(CBV2_EHIP, "the pre-armed rerank gave up its wait before the host published the candidates "
+                            "(device outputs are invalid)");
+    }
     const uint64_t tag = (uint64_t)pd.seq << 32;
     volatile uint64_t* vw = cw;
     for (size_t i = 0; i < (size_t)B * C; ++i) vw[i] = tag | (uint32_t)(rc ? -1 : cand_h[i]);
@@ -847,7 +932,7 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
     }
     if (!rc) {
       if (fwd) cbv2_set_final_mirror(fwd, pd.seq, final_k);
-      rc = rerank_call(ix, c, kd, Q, B, lq, k, L, cand_d, C, final_k, out_scores, out_ids, out_pos, st);
+      rc = rerank_call(ix, c, kd, Q, B, lq, k, kb, L, cand_d, C, final_k, out_scores, out_ids, out_pos, st);
       fin_used = fwd && cbv2_final_mirror_used() != 0;
       cbv2_set_final_mirror(nullptr, 0, 0);
     }
@@ -857,7 +942,7 @@ int finish_impl(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, in
   if (!rc && host_s) {
     const size_t n = (size_t)B * final_k;
     if (fin_used) {   // the final select's words, row by row: [k] scores | [k] ids | [k] positions
-      rc = wait_words(fw, fin_words, pd.seq, "final results");
+      rc = wait_words(fw, fin_words, pd.seq, st, "final results");
       if (!rc) g_final_words_calls.fetch_add(1, std::memory_order_relaxed);
       for (size_t i = 0; !rc && i < n; ++i) {
         const uint64_t* row = fw + (i / final_k) * 3 * final_k;

@@ -1,15 +1,22 @@
 // sharded.cpp — the multi-GPU exchange behind the C ABI (SURVEY.md §8(b),(e)):
 // cbv2_comm_init borrows an initialised RCCL communicator (e.g. the one
 // torch.distributed's "nccl" backend created: ProcessGroupNCCL._comm_ptr()),
-// and cbv2_search_sharded / cbv2_rerank_sharded run one stage each with ONE
-// collective, everything enqueued on the caller's stream:
+// and the stages run with ONE collective in all, everything enqueued on the
+// caller's stream:
 //
 //   search:  local scan + top-k written straight into this rank's send block
-//            [scores B*k | ids B*k | bm25 scores B*kb | bm25 ids B*kb]
+//            [scores B*k | ids B*k | bm25 scores B*kb | bm25 ids B*kb |
+//             bm25 prescores B*kb]  (the prescores: the rerank's raw scores
+//            of the rank's own BM25 top-kb, scored before the all-gather)
 //            -> ncclAllGather of the blocks -> HIP merge (score desc, id asc)
 //            of the G stage-2 lists and of the G stage-1 lists.
-//   rerank:  raw candidate scores (-inf for ids this shard does not own)
-//            -> ncclAllReduce(MAX) -> HIP top-k select.
+//   rerank:  cbv2_rerank_sharded_prescored (no collective): every fused
+//            candidate is in a stage-2 list or a stage-1 list, so its rerank
+//            score is in the gathered blocks already (the owner's top-k score
+//            -- the rerank's bits -- or its prescore); a HIP lookup + select.
+//            cbv2_rerank_sharded keeps the collective form for candidates
+//            from anywhere: raw candidate scores (-inf for ids this shard
+//            does not own) -> ncclAllReduce(MAX) -> HIP top-k select.
 //
 // An fp32-faithful shard bounds its band by the GLOBAL k-th
 // faithful score: the local call runs the bf16 scan + top-k and the exact
@@ -43,6 +50,13 @@ extern "C" int cbv2_merge_topk_strided(const float* in_scores, const int32_t* in
                                        size_t g_stride, float* out_scores, int32_t* out_ids, void* stream);
 extern "C" int cbv2_union_kth(const float* fk, int32_t G, int32_t B, int32_t k, size_t g_stride, float* lb,
                               void* stream);
+extern "C" int cbv2_prescored_select(const int32_t* recv, int32_t G, int64_t blk, int32_t B, int32_t k, int32_t kb,
+                                     const int32_t* cand, int32_t C, int32_t fk, float* out_s, int32_t* out_i,
+                                     int32_t* out_p, int32_t* misses, void* stream);
+extern "C" int cbv2_rerank_f32_after_search(cbv2_index* ix, const void* search_ws, size_t search_wsb, int32_t cap,
+                                            int32_t B, int32_t lq, const int32_t* cand, int32_t C, int32_t k, void* ws,
+                                            size_t wsb, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                                            const float* Q, void* stream);
 
 namespace {
 // The RCCL entry points used here (rccl.h: ncclResult_t is an int enum,
@@ -79,6 +93,7 @@ struct cbv2_comm {
   ErrStrFn err_str = nullptr;
   int nranks = 0, rank = 0;
   bool loopback = false;
+  int64_t gathers = 0, reduces = 0;   // collectives issued on this handle (cbv2_comm_stats)
 };
 
 namespace {
@@ -325,6 +340,7 @@ size_t rerank_bytes(const cbv2_index* ix, int32_t B, int32_t C, int32_t lq = 32)
 }
 
 // [local search part | send block | recv blocks | merged BM25 scores | rerank part]
+// (send block, words: [scores B*k | ids B*k | bm25 scores B*kb | bm25 ids B*kb | bm25 prescores B*kb])
 // local search part: bf16 / MXFP8: the cbv2_search workspace; fp32-faithful:
 // [f32 search workspace | fk B*k | fk of every rank G*B*k | lb B | status B].
 struct Layout {
@@ -333,6 +349,7 @@ struct Layout {
   float* lex_s_out;
   float *fk, *fk_all, *lb;
   int32_t* status;
+  uint8_t* rr;   // the rerank part (the exchange's stage-1 prescore: a faithful shard's rerank workspace)
 };
 Layout layout(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, int32_t kb, void* ws) {
   Layout L{};
@@ -351,12 +368,13 @@ Layout layout(const cbv2_index* ix, const cbv2_comm* c, int32_t B, int32_t k, in
   } else {
     L.search_ws = align256(cbv2_search_workspace_size(ix, B, k, CBV2_SCORER_MAXSIM));
   }
-  L.blk = (size_t)2 * B * (k + kb);
+  L.blk = (size_t)B * (2 * (size_t)k + 3 * (size_t)kb);
   if (base) {
     uint8_t* p = base + L.search_ws;
     L.send = (int32_t*)p;
     L.recv = (int32_t*)(p + align256(L.blk * 4));
     L.lex_s_out = (float*)(p + align256(L.blk * 4) + align256(L.blk * 4 * c->nranks));
+    L.rr = (uint8_t*)L.lex_s_out + align256((size_t)B * (kb > 0 ? kb : 1) * 4);
   }
   return L;
 }
@@ -369,8 +387,9 @@ size_t cbv2_sharded_workspace_bytes(const cbv2_index* ix, const cbv2_comm* c, in
   const size_t gather = align256(L.blk * 4) + align256(L.blk * 4 * c->nranks);
   const size_t lex_out = align256((size_t)B * (kb > 0 ? kb : 1) * 4);
   // the local search's part is sized for MaxSim (the sharded exchange's scorer;
-  // cbv2_search rejects another scorer's larger need with CBV2_EINVAL)
-  return L.search_ws + gather + lex_out + rerank_bytes(ix, B, C);
+  // cbv2_search rejects another scorer's larger need with CBV2_EINVAL); the
+  // rerank part serves the exchange's stage-1 prescore (kb candidates) too
+  return L.search_ws + gather + lex_out + rerank_bytes(ix, B, C > kb ? C : kb);
 }
 
 namespace {
@@ -402,26 +421,44 @@ int cbv2_search_sharded_local(cbv2_index* ix, cbv2_comm* c, int32_t scorer, cons
   // the global bound: every rank's fk, the k-th largest of their union
   rc = nccl_check(c, c->all_gather(L.fk, L.fk_all, (size_t)B * k, kNcclFloat32, c->nccl, st), "ncclAllGather");
   if (rc) return rc;
+  ++c->gathers;
   if ((rc = cbv2_union_kth(L.fk_all, c->nranks, B, k, (size_t)B * k, L.lb, st))) return rc;
   return cbv2_search_f32_finish(ix, B, lq, k, cap, workspace, L.f32_ws, L.lb, send_s, send_i, L.status, st);
 }
 
-int cbv2_search_sharded_exchange(cbv2_index* ix, cbv2_comm* c, int32_t B, int32_t k, const int32_t* lex_ids,
-                                 const float* lex_scores, int32_t kb, void* workspace, size_t workspace_bytes,
-                                 float* out_scores, int32_t* out_ids, int32_t* out_lex_ids, void* stream) {
+int cbv2_search_sharded_exchange(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t lq,
+                                 int32_t B, int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb,
+                                 void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids,
+                                 int32_t* out_lex_ids, void* stream) {
   if (int rc = check_sizes(ix, c, B, k, kb, workspace, workspace_bytes)) return rc;
   if (kb > 0 && (!lex_ids || !lex_scores || !out_lex_ids)) return err(CBV2_EINVAL, "null bm25 lists/output");
   if (!out_scores || !out_ids) return err(CBV2_EINVAL, "null outputs");
+  if (Q && (lq < 1 || lq > 32)) return err(CBV2_EINVAL, "lq must be in [1, 32] (got %d)", lq);
   hipStream_t st = (hipStream_t)stream;
   const Layout L = layout(ix, c, B, k, kb, workspace);
+  int rc;
   if (kb > 0) {
     int32_t* ls = L.send + (size_t)2 * B * k;
     SH_HIP(hipMemcpyAsync(ls, lex_scores, (size_t)B * kb * 4, hipMemcpyDefault, st));
     SH_HIP(hipMemcpyAsync(ls + (size_t)B * kb, lex_ids, (size_t)B * kb * 4, hipMemcpyDefault, st));
+    if (Q) {   // the stage-1 prescore: the rerank's raw scores of this rank's own BM25 top-kb
+      const int32_t* ids_d = ls + (size_t)B * kb;
+      float* pre = (float*)(ls + (size_t)2 * B * kb);
+      const size_t rrb = workspace_bytes - (size_t)(L.rr - (uint8_t*)workspace);
+      if (is_faithful(ix)) {   // on the local search's query split (re-split from Q if it is gone)
+        if (q_dtype != CBV2_DTYPE_F32) return err(CBV2_EINVAL, "an fp32-faithful shard takes f32 queries");
+        rc = cbv2_rerank_f32_after_search(ix, workspace, L.f32_ws, band_cap(k), B, lq, ids_d, kb, 0, L.rr, rrb, pre,
+                                          nullptr, nullptr, (const float*)Q, st);
+      } else {
+        rc = cbv2_rerank_ws(ix, Q, B, lq, ids_d, kb, 0, L.rr, rrb, pre, nullptr, nullptr, st);
+      }
+      if (rc) return rc;
+    }
   }
   // one all-gather of the blocks, then the merges (shard g's block at g * blk words)
-  int rc = nccl_check(c, c->all_gather(L.send, L.recv, L.blk, kNcclInt32, c->nccl, st), "ncclAllGather");
+  rc = nccl_check(c, c->all_gather(L.send, L.recv, L.blk, kNcclInt32, c->nccl, st), "ncclAllGather");
   if (rc) return rc;
+  ++c->gathers;
   rc = cbv2_merge_topk_strided((const float*)L.recv, L.recv + (size_t)B * k, c->nranks, B, k, L.blk, out_scores,
                                out_ids, st);
   if (rc || kb == 0) return rc;
@@ -436,8 +473,8 @@ int cbv2_search_sharded(cbv2_index* ix, cbv2_comm* c, int32_t scorer, const void
                         int32_t* out_lex_ids, void* stream) {
   int rc = cbv2_search_sharded_local(ix, c, scorer, Q, q_dtype, B, lq, k, kb, workspace, workspace_bytes, stream);
   if (rc) return rc;
-  return cbv2_search_sharded_exchange(ix, c, B, k, lex_ids, lex_scores, kb, workspace, workspace_bytes, out_scores,
-                                      out_ids, out_lex_ids, stream);
+  return cbv2_search_sharded_exchange(ix, c, Q, q_dtype, lq, B, k, lex_ids, lex_scores, kb, workspace,
+                                      workspace_bytes, out_scores, out_ids, out_lex_ids, stream);
 }
 
 int cbv2_rerank_sharded(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t B, int32_t lq, const int32_t* cand,
@@ -460,7 +497,28 @@ int cbv2_rerank_sharded(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t B, 
   if (rc) return rc;
   rc = nccl_check(c, c->all_reduce(raw, raw, (size_t)B * C, kNcclFloat32, kNcclMax, c->nccl, st), "ncclAllReduce");
   if (rc) return rc;
+  ++c->reduces;
   return cbv2_select_topk(raw, cand, B, C, k, out_scores, out_ids, out_pos, st);
+}
+
+int cbv2_rerank_sharded_prescored(cbv2_index* ix, cbv2_comm* c, int32_t B, int32_t k, int32_t kb,
+                                  const int32_t* cand, int32_t C, int32_t final_k, void* workspace,
+                                  size_t workspace_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                                  int32_t* misses, void* stream) {
+  if (int rc = check_sizes(ix, c, B, k, kb, workspace, workspace_bytes)) return rc;
+  if (!cand || !out_scores || !out_ids) return err(CBV2_EINVAL, "null candidates/outputs");
+  if (C < 1 || C > 1024 || final_k < 1) return err(CBV2_EINVAL, "C must be in [1, 1024], final_k >= 1 (C %d, k %d)", C,
+                                                   final_k);
+  const Layout L = layout(ix, c, B, k, kb, workspace);
+  return cbv2_prescored_select(L.recv, c->nranks, (int64_t)L.blk, B, k, kb, cand, C, final_k, out_scores, out_ids,
+                               out_pos, misses, stream);
+}
+
+int cbv2_comm_stats(const cbv2_comm* c, int64_t* out2) {
+  if (!c || !out2) return err(CBV2_EINVAL, "null comm/output");
+  out2[0] = c->gathers;
+  out2[1] = c->reduces;
+  return CBV2_OK;
 }
 
 }  // extern "C"

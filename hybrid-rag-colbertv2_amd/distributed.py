@@ -7,17 +7,25 @@ is the §8(e) design:
            global id) -> ONE all-gather over RCCL/xGMI of the packed pairs
            [G, B, k, 2] -> HIP merge with the (score desc, id asc) rule.
            Every rank ends with the identical global top-k.
-  stage 3  every rank scores the candidates it owns (-inf for the rest) ->
-           all-reduce(MAX) over [B, C] -> HIP top-k select.  Each id is owned by
-           exactly one shard, so MAX picks the owner's score.
+  stage 3  NO collective: every fused candidate is in a stage-2 list or a
+           stage-1 list, and both carry the rerank's score of the doc -- a
+           rank's local top-k scores are the rerank's bits (the same MaxSim
+           arithmetic), and each rank prescores its own BM25 top-kb with the
+           rerank before the stage-2 all-gather, where the prescores ride -- so
+           every rank looks the candidates' scores up in the gathered lists
+           and selects the top-k (``rerank(..., pool=...)``).  Candidates from
+           anywhere else take the collective form: every rank scores the
+           candidates it owns (-inf for the rest) -> all-reduce(MAX) over
+           [B, C] -> HIP top-k select (each id has exactly one owner).
 
 Stage 1 (host BM25) is doc-sharded the same way (bm25.sharded: global
 statistics from one build-time all-reduce), and its per-rank top-kb lists
 ride the stage-2 all-gather (search_hybrid), so a query costs each rank only
 its shard's postings and the whole exchange stays ONE collective per stage.
 
-Messages are tiny (B=256, k=100: 200 KiB per rank), so the exchange is
-latency-bound; it is one collective per stage.  torch.distributed's "nccl"
+Messages are tiny (B=256, k=100, kb=100: 400 KiB per rank), so the exchange
+is latency-bound; it is ONE collective per query batch (fp32-faithful shards:
+one more, the global band bound).  torch.distributed's "nccl"
 backend IS RCCL on ROCm.  The same code runs on "gloo" for CPU tests, where
 the caller injects CPU ``local``/``ops`` objects (tests only).
 """
@@ -190,7 +198,11 @@ class NativeExchange:
         self._stage = _PinnedStage(slots=4)               # ids + scores per call
         self.world = int(_lib.lib().cbv2_comm_size(h))
         self.rank = int(_lib.lib().cbv2_comm_rank(h))
-        self._ws = None
+        # two search workspaces, used in turn: a pipelined caller's stage 3 of
+        # batch j reads batch j's gathered blocks (its pool) after batch j+1's
+        # exchange was enqueued; + one for the collective rerank's scratch
+        self._ws = [None, None, None]
+        self._turn = 0
 
     def __del__(self):
         try:
@@ -198,13 +210,23 @@ class NativeExchange:
         except Exception:
             pass
 
-    def _workspace(self, B: int, k: int, kb: int, C: int) -> torch.Tensor:
+    def _workspace(self, B: int, k: int, kb: int, C: int, slot: int = 2) -> torch.Tensor:
         need = int(self._lib.lib().cbv2_sharded_workspace_bytes(self.index._h, self._h, B, k, kb, C))
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty((need,), dtype=torch.uint8, device=self.dev)
-        return self._ws
+        if self._ws[slot] is None or self._ws[slot].numel() < need:
+            self._ws[slot] = torch.empty((need,), dtype=torch.uint8, device=self.dev)
+        return self._ws[slot]
 
-    def search(self, Q: torch.Tensor, k: int, lexical=None):
+    def comm_stats(self):
+        """(all-gathers, all-reduces) issued on this handle so far."""
+        import ctypes
+        out = (ctypes.c_int64 * 2)()
+        self._lib.check(self._lib.lib().cbv2_comm_stats(self._h, out))
+        return int(out[0]), int(out[1])
+
+    def search(self, Q: torch.Tensor, k: int, lexical=None, return_pool: bool = False):
+        """(scores, ids, merged BM25 ids or None)[, pool]: the pool names this
+        call's gathered blocks for ``rerank(..., pool=pool)`` (stage 3 without
+        a collective); it stays valid until the next-but-one search."""
         from .index import _stream_ptr
         L = self._lib.lib()
         _keep, qptr, qdt, B, lq = self.index._prep_query(Q, "maxsim")
@@ -212,7 +234,8 @@ class NativeExchange:
         # the local scan is enqueued BEFORE stage 1 runs on the host, so the
         # workspace is sized for up to ``lexical_k`` stage-1 ids per query
         kb_cap = self.lexical_k if lexical is not None else 0
-        ws = self._workspace(B, k, kb_cap, 0)
+        slot, self._turn = self._turn, self._turn ^ 1
+        ws = self._workspace(B, k, kb_cap, 0, slot)
         self._lib.check(L.cbv2_search_sharded_local(self.index._h, self._h, self._lib.SCORERS["maxsim"], qptr, qdt,
                                                     B, lq, int(k), kb_cap, ws.data_ptr(), ws.numel(), st))
         kb = 0
@@ -227,17 +250,35 @@ class NativeExchange:
             li = self._stage.upload(np.ascontiguousarray(lex_i, np.int32), self.dev)
             ls = self._stage.upload(np.ascontiguousarray(lex_s, np.float32), self.dev)
             out_li = torch.empty((B, kb), dtype=torch.int32, device=self.dev)
+        # (Q: this rank's BM25 top-kb prescored with the rerank before the all-gather)
         self._lib.check(L.cbv2_search_sharded_exchange(
-            self.index._h, self._h, B, int(k), li.data_ptr() if li is not None else None,
+            self.index._h, self._h, qptr, qdt, lq, B, int(k), li.data_ptr() if li is not None else None,
             ls.data_ptr() if ls is not None else None, kb, ws.data_ptr(), ws.numel(), out_s.data_ptr(),
             out_i.data_ptr(), out_li.data_ptr() if out_li is not None else None, st))
+        if return_pool:
+            return out_s, out_i, out_li, _NativePool(ws, B, int(k), kb)
         return out_s, out_i, out_li
 
-    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int, pool=None, misses: torch.Tensor = None):
+        """Stage 3.  pool (from ``search(..., return_pool=True)`` of the batch
+        whose lists the candidates were fused from): the scores are looked up
+        in that exchange's gathered blocks, no collective
+        (cbv2_rerank_sharded_prescored; ``misses``: optional device int32 [1]
+        that counts candidates found in no list).  Otherwise every rank scores
+        its own candidates and one all-reduce(MAX) combines them."""
         from .index import _stream_ptr
-        _keep, qptr, _, B, lq = self.index._prep_query(Q, "maxsim")
         cand = cand.to(device=self.dev, dtype=torch.int32).contiguous()
-        C = int(cand.shape[1])
+        B, C = int(cand.shape[0]), int(cand.shape[1])
+        if pool is not None and pool.B == B and C <= 1024:
+            out_s = torch.empty((B, k), dtype=torch.float32, device=self.dev)
+            out_i = torch.empty((B, k), dtype=torch.int32, device=self.dev)
+            out_p = torch.empty((B, k), dtype=torch.int32, device=self.dev)
+            self._lib.check(self._lib.lib().cbv2_rerank_sharded_prescored(
+                self.index._h, self._h, B, pool.k, pool.kb, cand.data_ptr(), C, int(k), pool.ws.data_ptr(),
+                pool.ws.numel(), out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(),
+                misses.data_ptr() if misses is not None else None, _stream_ptr(self.dev)))
+            return out_s, out_i, out_p
+        _keep, qptr, _, B, lq = self.index._prep_query(Q, "maxsim")
         ws = self._workspace(B, 1, 0, C)
         out_s = torch.empty((B, k), dtype=torch.float32, device=self.dev)
         out_i = torch.empty((B, k), dtype=torch.int32, device=self.dev)
@@ -246,6 +287,33 @@ class NativeExchange:
             self.index._h, self._h, qptr, B, lq, cand.data_ptr(), C, int(k), ws.data_ptr(), ws.numel(),
             out_s.data_ptr(), out_i.data_ptr(), out_p.data_ptr(), _stream_ptr(self.dev)))
         return out_s, out_i, out_p
+
+
+class _NativePool:
+    """The gathered blocks of one NativeExchange search (its workspace)."""
+
+    def __init__(self, ws, B, k, kb):
+        self.ws, self.B, self.k, self.kb = ws, B, k, kb
+
+
+class _TorchPool:
+    """Every rank's stage-2 top-k and prescored stage-1 list of one
+    ShardedSearcher.search_hybrid call: [B, M] (id, rerank score) pairs."""
+
+    def __init__(self, ids, scores):
+        self.ids, self.scores = ids, scores
+
+
+def pool_scores(cand: torch.Tensor, ids: torch.Tensor, scores: torch.Tensor):
+    """raw [B, C]: each candidate's score in its row of (ids, scores) [B, M]
+    (-inf for a negative id, as the rerank scores one; -inf for an id found
+    nowhere, counted in misses).  Returns (raw, misses: a 0-d tensor on the
+    candidates' device -- read it only where a sync is harmless)."""
+    eq = (cand[:, :, None] == ids[:, None, :]) & (cand[:, :, None] >= 0)
+    hit = eq.any(-1)
+    idx = eq.to(torch.int8).argmax(-1)
+    raw = torch.where(hit, scores.gather(1, idx), torch.full_like(cand, float("-inf"), dtype=torch.float32))
+    return raw, ((cand >= 0) & ~hit).sum()
 
 
 class ShardedSearcher:
@@ -267,6 +335,7 @@ class ShardedSearcher:
         # native=True: the whole exchange runs inside the C ABI (NativeExchange)
         self._nx = NativeExchange(local, group, lexical_k) if native else None
         self._coll = None          # collective timing record (time_collectives)
+        self.last_pool_misses = None   # the last pooled rerank's count of candidates in no list (tensor)
 
     # ------------------------------------------------------------ measurement
     def time_collectives(self, enable: bool) -> None:
@@ -281,7 +350,8 @@ class ShardedSearcher:
         rec, self._coll = self._coll or [], None
         out = {}
         for name, e0, e1, host_ms in rec:
-            e1.synchronize()
+            if e1 is not None:
+                e1.synchronize()
             d = out.setdefault(name, {"calls": 0, "device_ms": 0.0, "host_ms": 0.0})
             d["calls"] += 1
             d["device_ms"] += e0.elapsed_time(e1) if e0 is not None else 0.0
@@ -342,7 +412,7 @@ class ShardedSearcher:
             return s, i
         return self.search_exchange(s, i, k)
 
-    def search_hybrid(self, Q: torch.Tensor, k: int, lexical=None):
+    def search_hybrid(self, Q: torch.Tensor, k: int, lexical=None, return_pool: bool = False):
         """Stage 2 plus this rank's stage-1 lists in the SAME collective.
 
         ``lexical()`` runs on the host AFTER the scan is enqueued (so it
@@ -352,26 +422,49 @@ class ShardedSearcher:
         array; otherwise both lists ride one all-gather and are merged with the
         same (score desc, id asc) rule, which reproduces the unsharded stage 1
         exactly because the shards were built with global statistics.
+        With several ranks the rank's BM25 ids are first prescored with the
+        rerank (raw MaxSim of its own docs) and the prescores ride the same
+        all-gather: ``return_pool=True`` appends the pool that lets
+        ``rerank(..., pool=pool)`` run stage 3 with no collective (None with
+        one rank).
         """
         if self._nx is not None:
-            return self._nx.search(Q, k, lexical)
+            return self._nx.search(Q, k, lexical, return_pool=return_pool)
         s, i = self._local_search(Q, k)
         if lexical is None:
             if self.world == 1:
-                return s, i, None
-            S, I = self.search_exchange(s, i, k)
-            return S, I, None
+                return (s, i, None, None) if return_pool else (s, i, None)
+            allp = self._all_gather(torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1))
+            S, I = self.ops.merge(allp[..., 0].contiguous().view(torch.float32), allp[..., 1].contiguous(), k)
+            pool = self._pool(allp, k, 0)
+            return (S, I, None, pool) if return_pool else (S, I, None)
         lex_i, lex_s = lexical()
         if self.world == 1:
-            return s, i, np.ascontiguousarray(lex_i, np.int32)
+            bm = np.ascontiguousarray(lex_i, np.int32)
+            return (s, i, bm, None) if return_pool else (s, i, bm)
         kb = lex_i.shape[1]
-        lex = self._stage.upload(np.stack([np.ascontiguousarray(lex_s, np.float32).view(np.int32),
-                                           np.ascontiguousarray(lex_i, np.int32)], axis=-1), i.device)
-        packed = torch.cat([torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1), lex], dim=1)
-        allp = self._all_gather(packed)                                                    # [G, B, k+kb, 2]
+        lex_i = np.ascontiguousarray(lex_i, np.int32)
+        lex_d = self._stage.upload(lex_i, i.device)
+        pre = self.local.rerank(Q, lex_d, 0)                     # this rank's own BM25 docs, rerank arithmetic
+        lex = self._stage.upload(np.stack([np.ascontiguousarray(lex_s, np.float32).view(np.int32), lex_i],
+                                          axis=-1), i.device)
+        packed = torch.cat([torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1), lex,
+                            torch.stack([pre.contiguous().view(torch.int32), lex_d], dim=-1)], dim=1)
+        allp = self._all_gather(packed)                                                    # [G, B, k+2kb, 2]
         S, I = self.ops.merge(allp[:, :, :k, 0].contiguous().view(torch.float32), allp[:, :, :k, 1].contiguous(), k)
-        _, LI = self.ops.merge(allp[:, :, k:, 0].contiguous().view(torch.float32), allp[:, :, k:, 1].contiguous(), kb)
-        return S, I, LI
+        _, LI = self.ops.merge(allp[:, :, k:k + kb, 0].contiguous().view(torch.float32),
+                               allp[:, :, k:k + kb, 1].contiguous(), kb)
+        pool = self._pool(allp, k, kb)
+        return (S, I, LI, pool) if return_pool else (S, I, LI)
+
+    @staticmethod
+    def _pool(allp: torch.Tensor, k: int, kb: int) -> _TorchPool:
+        """[B, G*(k+kb)] (id, score) pairs: every rank's local top-k and its
+        prescored stage-1 list (allp [G, B, k + 2kb, 2])."""
+        parts = allp[:, :, :k] if kb == 0 else torch.cat([allp[:, :, :k], allp[:, :, k + kb:]], dim=2)
+        G, B = parts.shape[0], parts.shape[1]
+        flat = parts.permute(1, 0, 2, 3).reshape(B, -1, 2)
+        return _TorchPool(flat[..., 1].contiguous(), flat[..., 0].contiguous().view(torch.float32))
 
     def search_exchange(self, s: torch.Tensor, i: torch.Tensor, k: int):
         packed = torch.stack([s.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1)  # [B, k, 2]
@@ -380,11 +473,21 @@ class ShardedSearcher:
         I = allp[..., 1].contiguous()
         return self.ops.merge(S, I, k)
 
-    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int):
+    def rerank(self, Q: torch.Tensor, cand: torch.Tensor, k: int, pool=None):
+        """Stage 3.  pool: from ``search_hybrid(..., return_pool=True)`` of the
+        batch whose lists ``cand`` was fused from -- the candidates' scores are
+        looked up in it (no collective; ``last_pool_misses`` counts
+        candidates found in none of its lists, which score -inf: fused from
+        other lists, pass no pool).  Without a pool: every rank scores its own
+        candidates, one all-reduce(MAX)."""
         if self._nx is not None:
-            return self._nx.rerank(Q, cand, k)
+            return self._nx.rerank(Q, cand, k, pool=pool)
         if self.world == 1:
             return self.local.rerank(Q, cand, k)                                           # fused select
+        if pool is not None:
+            cand_d = cand.to(device=pool.ids.device, dtype=torch.int32)
+            raw, self.last_pool_misses = pool_scores(cand_d, pool.ids, pool.scores)
+            return self.ops.select(raw, k, ids=cand_d)
         raw = self.local.rerank(Q, cand, 0)                                                # [B, C]
         self._collective("all_reduce_max", lambda: dist.all_reduce(raw, op=dist.ReduceOp.MAX, group=self.group),
                          raw.device)

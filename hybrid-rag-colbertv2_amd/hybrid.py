@@ -309,8 +309,9 @@ class PipelinedRetriever:
         """Enqueue stage 2 (+ the D2H of its ids, on the same stream, so the
         copy runs right after the scan and not starved behind the next one);
         run (or take) stage 1 on the host meanwhile."""
+        pool = None   # sharded: the gathered lists stage 3 looks its scores up in (no collective)
         if callable(lex):
-            _, ids, bm = self.searcher.search_hybrid(Q, self.k, lex)
+            _, ids, bm, pool = self.searcher.search_hybrid(Q, self.k, lex, return_pool=True)
         else:
             _, ids = self.searcher.search(Q, self.k)
             bm = np.ascontiguousarray(lex, np.int32)
@@ -325,7 +326,7 @@ class PipelinedRetriever:
             bm = lex_h
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        return ids_h, bm, ev
+        return ids_h, bm, ev, pool
 
     def run(self, batches):
         """batches: sequence of (Q [B, lq, D] device, lexical), where lexical is
@@ -341,14 +342,14 @@ class PipelinedRetriever:
             B = Q.shape[0]
             # the GPU scans batch j+1 while the host runs its BM25 and fuses batch j
             nxt = self._stage12(*batches[j + 1], slot=(j + 1) & 1) if j + 1 < len(batches) else None
-            ids_h, bm, ev = cur
+            ids_h, bm, ev, pool = cur
             ev.synchronize()
             bm_h = bm.numpy() if isinstance(bm, torch.Tensor) else bm
             self._cand_h[j & 1] = self._pinned(self._cand_h[j & 1], B, self.fused)
             cand = self._cand_h[j & 1][:B]
             cand.numpy()[:] = rrf_fuse(bm_h, ids_h.numpy(), rrf_k=self.rrf_k, C=self.fused)
             cand_d = cand.to(self.device, non_blocking=True)
-            s, i, _ = self.searcher.rerank(Q, cand_d, self.final_k)
+            s, i, _ = self.searcher.rerank(Q, cand_d, self.final_k, pool=pool)
             out.append((s, i))
             cur = nxt
         return out

@@ -404,11 +404,24 @@ class ColbertIndex:
         return {"workgroups": int(buf[0]), "chunk_docs": int(buf[1]), "static_docs": int(buf[2]),
                 "dynamic_tail": bool(buf[3])}
 
-    def time_scans(self, enable: bool) -> None:
+    def time_scans(self, enable: bool, clock: bool = False) -> None:
         """Bracket every following MaxSim scan launch of this index with HIP
         events on its own stream (cbv2_index_time_scans); enable clears the
-        previous record."""
-        _lib.check(_lib.lib().cbv2_index_time_scans(self._h, 1 if enable else 0))
+        previous record.  clock: also the doc-interleaved scans' clock probe
+        (``scan_clock``)."""
+        _lib.check(_lib.lib().cbv2_index_time_scans(self._h, (2 if clock else 1) if enable else 0))
+
+    def scan_clock(self, reset: bool = False):
+        """The clock probe's sums since ``time_scans(True, clock=True)`` or the
+        last reset (cbv2_index_scan_clock; synchronizes the device): dict with
+        the held clock in GHz (run-time weighted over the probed scans'
+        workgroups; None when no probed scan ran) and the raw sums."""
+        out = (ctypes.c_int64 * 4)()
+        _lib.check(_lib.lib().cbv2_index_scan_clock(self._h, out, 1 if reset else 0))
+        cyc, ticks, started, ended = (int(x) for x in out)
+        ghz = cyc / ticks * 0.1 if ticks > 0 and started == ended and started > 0 else None
+        return {"clock_ghz": ghz, "cycles": cyc, "ticks": ticks, "workgroups": ended,
+                "complete": started == ended}
 
     def scan_times(self, max_launches: int = 4096) -> List[float]:
         """Durations (ms) of the scans recorded since ``time_scans(True)``;

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define CBV2_ABI_VERSION 1
+#define CBV2_ABI_VERSION 2
 
 /* dtypes */
 #define CBV2_DTYPE_BF16 1
@@ -109,16 +109,26 @@ int cbv2_hbm_free(int device, void* p);
  * (cbv2_search_f32 / _begin + _finish), each bracketed from the end of the
  * bf16 top-k of its scan to the end of its band select and full-scan fallback:
  * the time the faithful arithmetic adds to a bf16 search (the query split
- * before the scan, one small kernel, is outside the bracket).  */
+ * before the scan, one small kernel, is outside the bracket).
+ * enable=2: the events, plus the clock probe of the doc-interleaved scans
+ * (bf16 maxsim_scan16x4_kernel, MXFP8 maxsim_scan_f8x4_kernel): each of their
+ * workgroups adds its run time in shader cycles (s_memtime) and in 10-ns ticks
+ * (s_memrealtime) to the handle's sums.  cbv2_index_scan_clock (after the
+ * launches completed) writes out4 = {sum of cycles, sum of ticks, workgroups
+ * started, workgroups ended} since enable=2 or the last reset (reset != 0
+ * zeroes them after the read): the clock the scans held in THIS run is
+ * out4[0] / out4[1] x 0.1 GHz.  */
 int cbv2_index_time_scans(cbv2_index* index, int32_t enable);
 int cbv2_index_scan_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
 int cbv2_index_band_times(cbv2_index* index, float* ms, int32_t max, int32_t* count);
+int cbv2_index_scan_clock(cbv2_index* index, int64_t* out4, int32_t reset);
 
 /* Handle options (A/B and tests; defaults = production):
  *  CBV2_OPT_FUSED_TOPK   1: cbv2_search fuses the top-k into eligible scans
- *                        (the bf16 doc-interleaved scan; 2 also fuses the
- *                        MXFP8 scan).  Default 0: on MI355X the fused scan
- *                        runs ~1 % longer than the scan + radix top-k.
+ *                        (the bf16 doc-interleaved scan; 2 the same -- the
+ *                        fused MXFP8 scan spills and is built in lab builds
+ *                        only).  Default 0: on MI355X the fused scan runs
+ *                        ~1 % longer than the scan + radix top-k.
  *  CBV2_OPT_DYNAMIC_TAIL 1: large scans hand the last part of the corpus out
  *                        as dynamic tasks, in 8 XCD-local slices (2: one
  *                        shared tail; 0: static chunks only).
@@ -493,10 +503,26 @@ int cbv2_index_writer_close(cbv2_index_writer* w);
  *   cbv2_search_sharded_exchange (lists in, all-gather, merges) with the SAME
  *   workspace, sized for the exchange's kb (the local call writes only the
  *   head of the send block; its kb just sizes its workspace check).
+ *   Q (nullable; the local call's queries, q_dtype, lq): with kb > 0 the
+ *   exchange first scores this rank's own BM25 top-kb with the rerank's
+ *   arithmetic (raw MaxSim; faithful shards on the local call's query split)
+ *   and those prescores ride the same all-gather.
+ * cbv2_rerank_sharded_prescored — stage 3 with NO collective, after an
+ *   exchange with Q (or kb = 0) on the same workspace with the same B, k, kb:
+ *   the fused candidates (RRF of the exchange's merged lists, as
+ *   cbv2_retrieve_finish builds them) all sit in the gathered blocks -- in
+ *   their owner's stage-2 top-k (whose scores are the rerank's bits) or its
+ *   BM25 top-kb (prescored) -- so every rank looks their scores up and selects
+ *   the top final_k (score desc, position asc), as cbv2_rerank_sharded would.
+ *   cand [B][C] device, C <= 1024.  A candidate found in no list scores -inf
+ *   and is counted into *misses (device int32, nullable; the caller zeroes
+ *   it): candidates from elsewhere take cbv2_rerank_sharded.
  * cbv2_rerank_sharded — every rank scores the candidates it owns (-inf
  *   otherwise) -> ncclAllReduce(MAX) -> top-k select; cand [B][C] global ids
  *   (device).  Workspace: the size above with C (a bf16 / MXFP8 shard needs
  *   only B*C*4 bytes).
+ * cbv2_comm_stats (diagnostic): out2 = {all-gathers, all-reduces} issued on
+ *   the handle so far.
  * fp32-faithful shards (cbv2_index_attach_residual; Q f32, q_dtype
  *   CBV2_DTYPE_F32): the local call runs the faithful search against the
  *   GLOBAL k-th bound -- bf16 scan + top-k + the exact faithful scores of that
@@ -522,12 +548,18 @@ int cbv2_search_sharded(cbv2_index* index, cbv2_comm* comm, int32_t scorer, cons
 int cbv2_search_sharded_local(cbv2_index* index, cbv2_comm* comm, int32_t scorer, const void* Q, int32_t q_dtype,
                               int32_t B, int32_t lq, int32_t k, int32_t kb, void* workspace, size_t workspace_bytes,
                               void* stream);
-int cbv2_search_sharded_exchange(cbv2_index* index, cbv2_comm* comm, int32_t B, int32_t k, const int32_t* lex_ids,
-                                 const float* lex_scores, int32_t kb, void* workspace, size_t workspace_bytes,
-                                 float* out_scores, int32_t* out_ids, int32_t* out_lex_ids, void* stream);
+int cbv2_search_sharded_exchange(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t q_dtype, int32_t lq,
+                                 int32_t B, int32_t k, const int32_t* lex_ids, const float* lex_scores, int32_t kb,
+                                 void* workspace, size_t workspace_bytes, float* out_scores, int32_t* out_ids,
+                                 int32_t* out_lex_ids, void* stream);
+int cbv2_rerank_sharded_prescored(cbv2_index* index, cbv2_comm* comm, int32_t B, int32_t k, int32_t kb,
+                                  const int32_t* cand, int32_t C, int32_t final_k, void* workspace,
+                                  size_t workspace_bytes, float* out_scores, int32_t* out_ids, int32_t* out_pos,
+                                  int32_t* misses, void* stream);
 int cbv2_rerank_sharded(cbv2_index* index, cbv2_comm* comm, const void* Q, int32_t B, int32_t lq,
                         const int32_t* cand, int32_t C, int32_t k, void* workspace, size_t workspace_bytes,
                         float* out_scores, int32_t* out_ids, int32_t* out_pos, void* stream);
+int cbv2_comm_stats(const cbv2_comm* comm, int64_t* out2);
 
 /* TEST-ONLY -- not for production use.  cbv2_comm_loopback_init writes
  * `nranks` (1..64) communicator handles out[0..nranks) that form ONE group

@@ -102,3 +102,19 @@ def test_main_line_takes_native_numbers_once_validated():
         assert torch_leg is None
     line, torch_leg = bench.main_line(*own, good, True)     # --native-exchange: the main legs ran native
     assert line["value"] == 1000.0 and torch_leg is None and line["exchange"].startswith("native")
+
+
+def test_clock_view_reproduces_avg_ms():
+    """bench.clock_view: the line's roofline frac split into THIS run's held
+    clock (the scans' in-kernel probe) and the MFMA-busy fraction at that
+    clock -- frac = clock / 2.4 GHz x busy, and FLOP / (busy x peak x clock /
+    2.4) gives back the measured avg_ms.  No probe -> no split."""
+    import bench
+    flop = 256 * 1_000_000 * bench.FLOP_PER_PAIR
+    for avg_ms, ghz in ((144.677, 2.022), (138.12, 1.95), (4.6, 1.59)):
+        v = bench.clock_view(flop, avg_ms, bench.PEAK_BF16_TFLOPS, ghz)
+        frac = flop / (avg_ms * 1e-3) / 1e12 / bench.PEAK_BF16_TFLOPS
+        assert v["clock_ghz_this_run"] == round(ghz, 4)
+        assert abs(v["avg_ms_from_clock_and_busy"] - avg_ms) <= 1e-3
+        assert abs(v["mfma_busy_this_run"] * ghz / bench.NOMINAL_GHZ - frac) < 1e-4
+    assert bench.clock_view(flop, 140.0, bench.PEAK_BF16_TFLOPS, None)["mfma_busy_this_run"] is None

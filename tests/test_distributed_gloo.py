@@ -132,20 +132,36 @@ def _hybrid_worker(rank, world, port, q):
     try:
         from hybrid_rag_colbertv2_amd import bm25
         from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range
+        from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
         Q, docs, doclens, _ = _data()
         terms, off, qt, qo, V = _bm25_data()
         a, b = shard_range(len(docs), rank, world)
         lex = bm25.sharded(terms[off[a]:off[b]], off[a:b + 1] - off[a], V, id_base=a)   # all-reduced stats
         ss = ShardedSearcher(OracleShard(Q, docs[a:b], doclens[a:b], a), ops=OracleOps())
         s, i, li = ss.search_hybrid(Q, 40, lambda: lex.search(qt, qo, 50))
-        q.put((rank, s.numpy(), i.numpy(), li.numpy()))
+        # stage 3 without a collective: the fused candidates' scores from the
+        # pool (stage-2 lists + the ranks' prescored BM25 lists), for a full
+        # and a narrower stage-1 width (kb 50 / 30)
+        pooled = []
+        for kb in (50, 30):
+            ss.time_collectives(True)
+            s3, i3, li3, pool = ss.search_hybrid(Q, 40, lambda: lex.search(qt, qo, kb), return_pool=True)
+            cand = rrf_fuse(li3.numpy(), i3.numpy(), rrf_k=60, C=20)
+            rs, ri, rp = ss.rerank(Q, torch.from_numpy(cand), 7, pool=pool)
+            coll = ss.collective_times()
+            pooled.append((cand, rs.numpy(), ri.numpy(), rp.numpy(), int(ss.last_pool_misses),
+                           {n: d["calls"] for n, d in coll.items()}))
+        q.put((rank, s.numpy(), i.numpy(), li.numpy(), pooled))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_hybrid_exchange_equals_unsharded(world):
-    """Doc-sharded BM25 (global stats by all-reduce) + stage 2 in one all-gather."""
+    """Doc-sharded BM25 (global stats by all-reduce) + stage 2 in one all-gather;
+    stage 3 of the fused lists with NO collective (every candidate's rerank
+    score rides that all-gather) equals the unsharded rerank, at kb 50 and 30."""
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -160,9 +176,16 @@ def test_hybrid_exchange_equals_unsharded(world):
     es, ei = orc.topk(orc.maxsim(Q.numpy(), docs, doclens), 40)
     terms, off, qt, qo, V = _bm25_data()
     bi, _ = orc.bm25_topk(terms, off, qt, qo, V, 50)
-    for _, s, i, li in res:
+    for _, s, i, li, pooled in res:
         assert np.array_equal(i, ei) and np.array_equal(li, bi)
         np.testing.assert_allclose(s, es, atol=1e-5)
+        for kb, (cand, rs, ri, rp, misses, calls) in zip((50, 30), pooled):
+            bk, _ = orc.bm25_topk(terms, off, qt, qo, V, kb)
+            assert np.array_equal(cand, rrf_fuse(bk, ei, rrf_k=60, C=20))
+            ws, wi, wp = orc.rerank(Q.numpy(), docs, doclens, cand, 7)
+            assert np.array_equal(ri, wi) and np.array_equal(rp, wp), f"kb {kb}: pooled stage 3 differs"
+            np.testing.assert_allclose(rs, ws, atol=1e-5)
+            assert misses == 0 and calls == {"all_gather": 1}, (kb, misses, calls)
 
 
 _QUERIES = ["what is late interaction", "colbert maxsim on mi355x", "bm25 and rrf fusion",

@@ -95,7 +95,9 @@ def test_fused_equals_unfused_fp8(dev, N, B, k):
     ix = ColbertIndex.mxfp8(docs, doclens)
     assert ix.fused_topk_slots(B, k) == 0            # off by default: the fused f8 build spills
     ix.set_option(_lib.OPT_FUSED_TOPK, 2)
-    assert ix.fused_topk_slots(B, k) > 0
+    # the product library leaves the spilling fused MXFP8 scan out (lab builds
+    # only): mode 2 searches an MXFP8 index unfused, with the same results
+    assert ix.fused_topk_slots(B, k) == 0
     fs, fi, us, ui = _both(ix, Q, k, mode=2)
     assert torch.equal(fi, ui) and torch.equal(fs.view(torch.int32), us.view(torch.int32))
 

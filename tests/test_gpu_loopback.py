@@ -20,6 +20,7 @@ import torch
 from hybrid_rag_colbertv2_amd import synth
 from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
 from hybrid_rag_colbertv2_amd.distributed import NativeExchange, loopback_comms
+from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
 from hybrid_rag_colbertv2_amd.index import ColbertIndex
 
 pytestmark = pytest.mark.gpu
@@ -87,22 +88,33 @@ def test_native_exchange_loopback_equals_unsharded(dev, G, B, fp8):
     cand = cand.contiguous()
 
     def rank(r):
-        s, i, li = nxs[r].search(Q, k, lexical=lambda: lex[r].search(qt, qo, kb))
+        s, i, li, pool = nxs[r].search(Q, k, lexical=lambda: lex[r].search(qt, qo, kb), return_pool=True)
         s2, i2, _ = nxs[r].search(Q, 7)                # a second exchange without stage-1 lists
-        rr = nxs[r].rerank(Q, cand, kf)
-        return [x.cpu() for x in (s, i, li, s2, i2, *rr)]
+        rr = nxs[r].rerank(Q, cand, kf)                # candidates from elsewhere: the all-reduce form
+        # stage 3 of the fused lists: scores from the first exchange's pool, no collective
+        fused = torch.from_numpy(rrf_fuse(li.cpu().numpy(), i.cpu().numpy(), rrf_k=60, C=C)).to(dev)
+        miss = torch.zeros(1, dtype=torch.int32, device=dev)
+        c0 = nxs[r].comm_stats()
+        pr = nxs[r].rerank(Q, fused, kf, pool=pool, misses=miss)
+        c1 = nxs[r].comm_stats()
+        return [x.cpu() for x in (s, i, li, s2, i2, *rr, *pr, miss)] + [(c1[0] - c0[0], c1[1] - c0[1])]
 
     outs = _run_ranks(G, rank)
     torch.cuda.synchronize()
     bi, _ = lex_full.search(qt, qo, kb)
     ers, eri, erp = full.rerank(Q, cand, kf)
     e7s, e7i = full.search(Q, 7)
-    for r, (s, i, li, s2, i2, rs, ri, rp) in enumerate(outs):
+    pws, pwi, pwp = (x.cpu() for x in full.rerank(Q, torch.from_numpy(rrf_fuse(bi, ei.cpu().numpy(), rrf_k=60,
+                                                                                  C=C)).to(dev), kf))
+    for r, (s, i, li, s2, i2, rs, ri, rp, ps, pi, pp, miss, dc) in enumerate(outs):
         assert torch.equal(i, ei.cpu()), f"rank {r}: ids differ from the unsharded search"
         assert torch.equal(s, es.cpu()), f"rank {r}: scores differ from the unsharded search"
         assert np.array_equal(li.numpy(), bi), f"rank {r}: merged BM25 lists differ from the unsharded BM25"
         assert torch.equal(i2, e7i.cpu()) and torch.equal(s2, e7s.cpu())
         assert torch.equal(ri, eri.cpu()) and torch.equal(rp, erp.cpu()) and torch.equal(rs, ers.cpu())
+        assert torch.equal(pi, pwi) and torch.equal(pp, pwp) and torch.equal(ps, pws), \
+            f"rank {r}: the prescored stage 3 differs from the unsharded rerank"
+        assert int(miss) == 0 and dc == (0, 0), f"rank {r}: misses {int(miss)}, collectives {dc}"
     # the planted docs are the global top-10 whatever shard holds them
     for b in range(B):
         assert set(outs[0][1][b, :10].tolist()) == set(planted[b].tolist())
@@ -173,19 +185,27 @@ def test_native_exchange_loopback_faithful_equals_unsharded(dev, G, B):
     cand = cand.contiguous()
 
     def rank(r):
-        s, i, li = nxs[r].search(Q, k, lexical=lambda: lex[r].search(qt, qo, kb))
+        s, i, li, pool = nxs[r].search(Q, k, lexical=lambda: lex[r].search(qt, qo, kb), return_pool=True)
         rr = nxs[r].rerank(Q, cand, kf)
-        return [x.cpu() for x in (s, i, li, *rr)]
+        fused = torch.from_numpy(rrf_fuse(li.cpu().numpy(), i.cpu().numpy(), rrf_k=60, C=C)).to(dev)
+        miss = torch.zeros(1, dtype=torch.int32, device=dev)
+        pr = nxs[r].rerank(Q, fused, kf, pool=pool, misses=miss)   # faithful prescores, no collective
+        return [x.cpu() for x in (s, i, li, *rr, *pr, miss)]
 
     outs = _run_ranks(G, rank)
     torch.cuda.synchronize()
     bi, _ = lex_full.search(qt, qo, kb)
     ers, eri, erp = full.rerank(Q, cand, kf)
-    for r, (s, i, li, rs, ri, rp) in enumerate(outs):
+    pws, pwi, pwp = (x.cpu() for x in full.rerank(Q, torch.from_numpy(rrf_fuse(bi, ei.cpu().numpy(), rrf_k=60,
+                                                                                  C=C)).to(dev), kf))
+    for r, (s, i, li, rs, ri, rp, ps, pi, pp, miss) in enumerate(outs):
         assert torch.equal(i, ei.cpu()), f"rank {r}: ids differ from the unsharded faithful search"
         assert torch.equal(s, es.cpu()), f"rank {r}: scores differ from the unsharded faithful search"
         assert np.array_equal(li.numpy(), bi)
         assert torch.equal(ri, eri.cpu()) and torch.equal(rp, erp.cpu()) and torch.equal(rs, ers.cpu())
+        assert torch.equal(pi, pwi) and torch.equal(pp, pwp) and torch.equal(ps, pws), \
+            f"rank {r}: the faithful prescored stage 3 differs from the unsharded rerank"
+        assert int(miss) == 0
     tied = 0
     for b in range(B):
         row = outs[0][0][b]

@@ -156,9 +156,16 @@ def test_one_trip_sharded_loopback_equals_unsharded(dev, G, B, kind, kb_ret):
     comms = loopback_comms(G)
     ones = [OneTripRetriever(NativeExchange(shards[r], comm=comms[r]), colbert_k=K, fused=C, final_k=KF)
             for r in range(G)]
+    c0 = [o._owner.comm_stats() for o in ones]
     outs = _run_ranks(G, lambda r: [x.cpu() for x in ones[r](Q, lambda: lex[r].search(qt, qo, kb_ret))])
     hosts = _run_ranks(G, lambda r: ones[r](Q, lambda: lex[r].search(qt, qo, kb_ret), host=True))
     torch.cuda.synchronize()
+    # collectives per call: the stage-2 all-gather (+ the faithful band bound's),
+    # and NO stage-3 all-reduce (the fused candidates' scores ride the all-gather)
+    for r, o in enumerate(ones):
+        g1, a1 = o._owner.comm_stats()
+        assert (g1 - c0[r][0], a1 - c0[r][1]) == (2 * (2 if kind == "fp32" else 1), 0), \
+            f"rank {r}: {(g1 - c0[r][0], a1 - c0[r][1])} collectives (all-gather, all-reduce) for two calls"
     bi, _ = lex_full.search(qt, qo, kb_ret)
     want = [x.cpu() for x in _composed(full, Q, bi)]
     for r, got in enumerate(outs):

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(L):
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib._SIGS), "ctypes signatures out of sync with the header"
-    assert L.cbv2_abi_version() == 1
+    assert L.cbv2_abi_version() == 2
 
 
 def test_library_stamp_is_the_sources_content_hash(L, tmp_path):

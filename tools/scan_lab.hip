@@ -417,6 +417,14 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   if (kind == 31) LAB_MID(4, 2, 2, 0);
   if (kind == 32) LAB_MID(4, 2, 1, 3);
 #undef LAB_MID
+  // kind 33 (round 6): the B <= 4 dense-doc production shape, 4 waves x 1
+  // query, two per CU, non-temporal (kScan16x4W4Q1 without the folded keys);
+  // stamps != null: its STAMPS build (per-workgroup clock, start skew, tail)
+  if (kind == 33)
+    return stamps ? launch_scan16x4<4, 1, 2, 2, 2, true, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
+                  : launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
