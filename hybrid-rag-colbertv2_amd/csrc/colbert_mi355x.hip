@@ -874,6 +874,9 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // A wave waits only for what it reads or overwrites, so the partner waves
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
+#ifndef CBV2_SCAN_LINMAP
+#define CBV2_SCAN_LINMAP 0   // lab A/B builds set 1: a one-group scan's chunk = blockIdx
+#endif
 #ifndef CBV2_F8_D47
 #define CBV2_F8_D47 1   // lab A/B builds set 3
 #endif
@@ -957,7 +960,8 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   const int nq_groups = (B + QPB - 1) / QPB;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
-  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int lin = CBV2_SCAN_LINMAP && nq_groups == 1 ? bid   // (lab A/B: chunks interleaved over the XCDs)
+                  : (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
   const int qg = lin % nq_groups;
   const int64_t chunk = lin / nq_groups;
   uint64_t t_start = 0, r_start = 0;

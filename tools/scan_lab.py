@@ -30,6 +30,8 @@ ALT_DEFS = os.environ.get("SCANLAB_ALT_DEFS", "-DCBV2_TAIL_CAS=1").split()
 
 
 def build():
+    if os.environ.get("SCANLAB_NO_BUILD") == "1" and os.path.exists(LAB) and os.path.exists(LAB_NT):
+        return   # (the GPU box: the libraries built in the container travel with the tree)
     src = os.path.join(ROOT, "tools", "scan_lab.hip")
     stamp = LAB_NT + ".defs"
     if not os.path.exists(stamp) or open(stamp).read() != " ".join(ALT_DEFS):
