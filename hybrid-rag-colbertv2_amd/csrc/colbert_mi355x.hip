@@ -874,6 +874,9 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // A wave waits only for what it reads or overwrites, so the partner waves
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
+#ifndef CBV2_SCAN_HANDOFF
+#define CBV2_SCAN_HANDOFF 1   // lab A/B builds set 0: drained task switches (before round 6)
+#endif
 #ifndef CBV2_SCAN_LINMAP
 #define CBV2_SCAN_LINMAP 0   // lab A/B builds set 1: a one-group scan's chunk = blockIdx
 #endif
@@ -931,7 +934,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   constexpr int kPiecesPerWave = kPieces / kLoadWaves;   // per loading wave
   static_assert(TPI == 32 || TPI == 64, "32 or 64 tokens per iteration");
   static_assert(kPieces % kLoadWaves == 0, "pieces must split evenly over the loading waves");
-  static_assert(NBUF == 2 || NBUF == 3 || (ARRIVE && NBUF == 4), "2- or 3-deep ring (4 with ARRIVE)");
+  static_assert(NBUF >= 2 && NBUF <= 4, "2- to 4-deep ring");
   static_assert(!(SPREAD && SPLITLOAD), "SPREAD spreads every wave's pieces; SPLITLOAD moves them");
   static_assert(!ARRIVE || (SPLITLOAD && !SPREAD && kLoadWaves + WAVES <= 16), "ARRIVE needs SPLITLOAD");
   // one LDS object only: with a second __shared__ array hipcc starts putting
@@ -1010,24 +1013,43 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   // (tiles + epilogue, to the next iteration's top) -- and the iteration count
   uint64_t ph_wait = 0, ph_issue = 0, ph_comp = 0, ph_n = 0, ph_t = 0;
 
+  // Seamless task hand-off (2-deep ring, round 6): a range's next range is
+  // grabbed by thread 0 at the end of its second-last iteration (its atomic
+  // returns with that iteration's wait), published by the last iteration's
+  // barrier, and the next range's first iteration is issued into the ring
+  // slot the last iteration frees -- so a task switch costs no ring drain, no
+  // extra barrier and no exposed atomic.  At a 125k-doc shard, B = 1, the
+  // drained switches held the scan at 0.632 ms against 0.610 for a static
+  // split whose odd XCDs run 17 % behind the even ones (profiles/r06).
+  // (the 4-wave shapes, B <= 16: the 8-wave B > 16 shape keeps drained
+  // switches -- its fragments fill the VGPR file and the hand-off's state
+  // spills there -- and hands the tail out in tasks the MFMAs amortize)
+  constexpr bool kHandoff = CBV2_SCAN_HANDOFF && NBUF == 2 && !ARRIVE && !SPREAD && WAVES == 4;
+  // one range's first iteration into ring slot buf (its G = 0, j = 0 pieces)
+  auto issue_piece_at = [&](int64_t rb, int rnd, int it, int buf, int jj) {
+    const int G = it / IPG, j = it % IPG;
+    const int piece = lwave * kPiecesPerWave + jj;
+    int pdoc;
+    const uint32_t poff = piece_src(jj, pdoc);
+    int d = 4 * G + pdoc;
+    d = d < rnd ? d : rnd - 1;  // the last group's missing docs: any valid doc (rows masked)
+    const uint8_t* src = tokens + (size_t)(rb + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16, 0,
+                                     AUX);
+  };
+
   // the first range: this workgroup's static chunk (may be empty)
   int64_t d_begin = chunk * chunk_docs;
   int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
+  int cur = 0;               // ring slot of iteration it
+  bool pre_issued = false;   // kHandoff: this range's first iteration is in slot cur already
   for (int k = 0;; ++k) {
+    bool handed = false;                       // kHandoff: the next range was grabbed inside this one
+    int64_t nx_begin = 0, nx_end = 0;          // ... and it is [nx_begin, nx_end) (empty: none)
     if (d_begin < d_end) {
       const int nd = (int)(d_end - d_begin);
       const int ngr = (nd + 3) >> 2;
-      auto issue_piece = [&](int it, int buf, int jj) {
-        const int G = it / IPG, j = it % IPG;
-        const int piece = lwave * kPiecesPerWave + jj;
-        int pdoc;
-        const uint32_t poff = piece_src(jj, pdoc);
-        int d = 4 * G + pdoc;
-        d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
-                                         0, AUX);
-      };
+      auto issue_piece = [&](int it, int buf, int jj) { issue_piece_at(d_begin, nd, it, buf, jj); };
       auto issue = [&](int it, int buf) {
         if (!loader || (PROBE == 2 && it >= NBUF)) return;   // PROBE 2 (INVALID): no streaming after the first fill
 #pragma unroll
@@ -1040,14 +1062,17 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
       int dl_g = 0, dl_min = 0, dl_max = 0;
 
-      const int nit = IPG * ngr;
+      const int nit = IPG * ngr;   // (>= IPG >= 2)
       if constexpr (ARRIVE) {   // the first NBUF-1 iterations (every earlier iteration is done: range barrier)
         for (int j0 = 0; j0 < NBUF - 1 && j0 < nit; ++j0) issue(j0, (int)((gbase + (uint32_t)j0) % NBUF));
-      } else {
+      } else if (!pre_issued) {
+        cur = 0;
         issue(0, 0);
-        if (NBUF == 3 && nit > 1) issue(1, 1);
+        if (NBUF >= 3 && nit > 1) issue(1, 1);
+        if (NBUF >= 4 && nit > 2) issue(2, 2);
       }
-      int cur = 0;           // ring slot of iteration it
+      pre_issued = false;
+      const bool grab = kHandoff && task_ctr != nullptr;   // block-uniform
       bool stored = false;   // global stores issued last iteration (they count in vmcnt)
       for (int it = 0; it < nit; ++it) {
         uint64_t ph_a = 0;
@@ -1077,8 +1102,11 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           }
           buf = smem + (gi % NBUF) * kIterBytes;
         } else {
-          if (NBUF == 3 && it + 1 < nit && !stored)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");  // it landed; it+1 in flight
+          // it landed; the younger iterations issued (NBUF - 2 at most) stay in flight
+          if (NBUF == 4 && it + 2 < nit && !stored)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPiecesPerWave) : "memory");
+          else if (NBUF >= 3 && it + 1 < nit && !stored)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
@@ -1092,10 +1120,22 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
         stored = false;
         if constexpr (!ARRIVE) {
           nslot = cur ^ 1;  // 2-deep ring: iteration it+1's slot
+          if (grab && it + 1 == nit) {   // the next range (grabbed at the end of it - 1): its first tiles
+            const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1)]);
+            const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1) + 1]);
+            handed = true;
+            nx_begin = static_docs + (int64_t)o;
+            nx_end = sz > 0 && nx_begin < n ? (nx_begin + sz < n ? nx_begin + sz : n) : nx_begin;
+            if (nx_begin < nx_end && loader) {
+#pragma unroll
+              for (int jj = 0; jj < kPiecesPerWave; ++jj) issue_piece_at(nx_begin, (int)(nx_end - nx_begin), 0, nslot, jj);
+            }
+          }
           if (NBUF == 2 && !SPREAD && it + 1 < nit) issue(it + 1, nslot);
           if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+          if (NBUF == 4 && it + 3 < nit) issue(it + 3, (cur + 3) & 3);
           buf = smem + cur * kIterBytes;
-          cur = NBUF == 2 ? (cur ^ 1) : (cur == 2 ? 0 : cur + 1);
+          cur = NBUF == 2 ? (cur ^ 1) : NBUF == 3 ? (cur == 2 ? 0 : cur + 1) : ((cur + 1) & 3);
         }
 
         const int G = it / IPG, j = it % IPG;
@@ -1220,10 +1260,22 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           asm volatile("" ::: "memory");
           if (lane == 0) __hip_atomic_store(sync_done + wave, (int)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        if (grab && it + 2 == nit && threadIdx.x == 0) {   // the hand-off's grab (its return waits with it + 1's data)
+          next_task_sliced(task_ctr + tail_slices * qg, tail_slices, bid & 7, task_docs, (int)(n - static_docs),
+                           nwg / nq_groups, task_slot + 2 * (k & 1));
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // in LDS before this wave reaches the next barrier
+        }
       }
       if constexpr (ARRIVE) gbase += (uint32_t)nit;
     }
     if (task_ctr == nullptr) break;
+    if (kHandoff && handed) {   // the next range was grabbed and its first iteration issued above
+      if (nx_begin >= nx_end) break;
+      d_begin = nx_begin;
+      d_end = nx_end;
+      pre_issued = true;   // (cur is its slot)
+      continue;
+    }
     // next dynamic task; the barrier also retires every wave's reads of the
     // ring before the next range refills it (two slots: a slow wave may still
     // read slot k&1 while thread 0 fills slot (k+1)&1).

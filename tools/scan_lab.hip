@@ -425,6 +425,48 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
                         ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
                   : launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
                         ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  // kinds 34-36 (round 6): the B <= 4 shape with more doc bytes in flight per
+  // CU -- 34: one workgroup per CU, 3-deep 32-token ring (96 KiB of LDS);
+  // 35: one per CU, 64-token iterations, 2-deep (128 KiB); 36: one per CU,
+  // ARRIVE (no per-iteration barrier, waves 0-1 load), 4-deep 32-token ring
+  if (kind == 34)
+    return stamps ? launch_scan16x4<4, 1, 1, 2, 3, true, 32, 1, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
+                  : launch_scan16x4<4, 1, 1, 2, 3, false, 32, 1, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  if (kind == 35)
+    return stamps ? launch_scan16x4<4, 1, 1, 2, 2, true, 64, 1, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
+                  : launch_scan16x4<4, 1, 1, 2, 2, false, 64, 1, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  if (kind == 36)
+    return stamps ? launch_scan16x4<4, 1, 1, 2, 4, true, 32, 1, false, 0, true, true, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
+                  : launch_scan16x4<4, 1, 1, 2, 4, false, 32, 1, false, 0, true, true, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  // kinds 37 / 38: kind 34 with SPLITLOAD (waves 0-1 issue every DMA piece) /
+  // with a 4-deep ring (128 KiB of LDS, three iterations in flight)
+  if (kind == 37)
+    return stamps ? launch_scan16x4<4, 1, 1, 2, 3, true, 32, 1, false, 0, true, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
+                  : launch_scan16x4<4, 1, 1, 2, 3, false, 32, 1, false, 0, true, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  if (kind == 38)
+    return stamps ? launch_scan16x4<4, 1, 1, 2, 4, true, 32, 1, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, (uint64_t*)stamps, nullptr)
+                  : launch_scan16x4<4, 1, 1, 2, 4, false, 32, 1, false, 0, false, false, 0, kLd, 0, 2>(
+                        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  // kinds 39 / 40: the B = 5-8 shape (4 x 2) at one workgroup per CU, 3- / 4-deep
+  if (kind == 39)
+    return launch_scan16x4<4, 2, 1, 2, 3, false, 32, 1, false, 0, false, false, 0, kLd, 0, 2>(
+        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  if (kind == 40)
+    return launch_scan16x4<4, 2, 1, 2, 4, false, 32, 1, false, 0, false, false, 0, kLd, 0, 2>(
+        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  // kind 41: the production B = 5-8 shape (4 x 2, two per CU, nt)
+  if (kind == 41)
+    return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
+        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,

@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--chain", type=int, default=1,
+                    help="launches back to back between the timing events (reported per launch)")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16", help="fp8: lab_scan_f8 variants 0/1")
     ap.add_argument("--stamps", default="",
                     help="comma list of f<frac>t<docs> splits: after the A/B, run each with per-workgroup "
@@ -123,10 +125,11 @@ def main():
         for v in variants:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            run(v)
+            for _ in range(a.chain):
+                run(v)
             e1.record(st)
             e1.synchronize()
-            times[v].append(e0.elapsed_time(e1))
+            times[v].append(e0.elapsed_time(e1) / a.chain)
     # oracle on a slice (first 64 and last 200 docs, 8 queries)
     sl = torch.cat([torch.arange(64), torch.arange(a.docs - 200, a.docs)]).to(dev)
     nq = min(8, a.batch)
