@@ -874,12 +874,6 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // A wave waits only for what it reads or overwrites, so the partner waves
 // cross iteration boundaries without draining the MFMA pipe at a barrier, and
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
-#ifndef CBV2_SCAN_HANDOFF
-#define CBV2_SCAN_HANDOFF 1   // lab A/B builds set 0: drained task switches (before round 6)
-#endif
-#ifndef CBV2_SCAN_LINMAP
-#define CBV2_SCAN_LINMAP 0   // lab A/B builds set 1: a one-group scan's chunk = blockIdx
-#endif
 #ifndef CBV2_F8_D47
 #define CBV2_F8_D47 1   // lab A/B builds set 3
 #endif
@@ -963,8 +957,7 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   const int nq_groups = (B + QPB - 1) / QPB;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, idx = bid >> 3, qd = nwg >> 3, rm = nwg & 7;
-  const int lin = CBV2_SCAN_LINMAP && nq_groups == 1 ? bid   // (lab A/B: chunks interleaved over the XCDs)
-                  : (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
+  const int lin = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + idx;
   const int qg = lin % nq_groups;
   const int64_t chunk = lin / nq_groups;
   uint64_t t_start = 0, r_start = 0;
@@ -1013,43 +1006,24 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   // (tiles + epilogue, to the next iteration's top) -- and the iteration count
   uint64_t ph_wait = 0, ph_issue = 0, ph_comp = 0, ph_n = 0, ph_t = 0;
 
-  // Seamless task hand-off (2-deep ring, round 6): a range's next range is
-  // grabbed by thread 0 at the end of its second-last iteration (its atomic
-  // returns with that iteration's wait), published by the last iteration's
-  // barrier, and the next range's first iteration is issued into the ring
-  // slot the last iteration frees -- so a task switch costs no ring drain, no
-  // extra barrier and no exposed atomic.  At a 125k-doc shard, B = 1, the
-  // drained switches held the scan at 0.632 ms against 0.610 for a static
-  // split whose odd XCDs run 17 % behind the even ones (profiles/r06).
-  // (the 4-wave shapes, B <= 16: the 8-wave B > 16 shape keeps drained
-  // switches -- its fragments fill the VGPR file and the hand-off's state
-  // spills there -- and hands the tail out in tasks the MFMAs amortize)
-  constexpr bool kHandoff = CBV2_SCAN_HANDOFF && NBUF == 2 && !ARRIVE && !SPREAD && WAVES == 4;
-  // one range's first iteration into ring slot buf (its G = 0, j = 0 pieces)
-  auto issue_piece_at = [&](int64_t rb, int rnd, int it, int buf, int jj) {
-    const int G = it / IPG, j = it % IPG;
-    const int piece = lwave * kPiecesPerWave + jj;
-    int pdoc;
-    const uint32_t poff = piece_src(jj, pdoc);
-    int d = 4 * G + pdoc;
-    d = d < rnd ? d : rnd - 1;  // the last group's missing docs: any valid doc (rows masked)
-    const uint8_t* src = tokens + (size_t)(rb + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16, 0,
-                                     AUX);
-  };
-
   // the first range: this workgroup's static chunk (may be empty)
   int64_t d_begin = chunk * chunk_docs;
   int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
-  int cur = 0;               // ring slot of iteration it
-  bool pre_issued = false;   // kHandoff: this range's first iteration is in slot cur already
   for (int k = 0;; ++k) {
-    bool handed = false;                       // kHandoff: the next range was grabbed inside this one
-    int64_t nx_begin = 0, nx_end = 0;          // ... and it is [nx_begin, nx_end) (empty: none)
     if (d_begin < d_end) {
       const int nd = (int)(d_end - d_begin);
       const int ngr = (nd + 3) >> 2;
-      auto issue_piece = [&](int it, int buf, int jj) { issue_piece_at(d_begin, nd, it, buf, jj); };
+      auto issue_piece = [&](int it, int buf, int jj) {
+        const int G = it / IPG, j = it % IPG;
+        const int piece = lwave * kPiecesPerWave + jj;
+        int pdoc;
+        const uint32_t poff = piece_src(jj, pdoc);
+        int d = 4 * G + pdoc;
+        d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
+        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
+                                         0, AUX);
+      };
       auto issue = [&](int it, int buf) {
         if (!loader || (PROBE == 2 && it >= NBUF)) return;   // PROBE 2 (INVALID): no streaming after the first fill
 #pragma unroll
@@ -1062,17 +1036,15 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
       int dl_g = 0, dl_min = 0, dl_max = 0;
 
-      const int nit = IPG * ngr;   // (>= IPG >= 2)
+      const int nit = IPG * ngr;
       if constexpr (ARRIVE) {   // the first NBUF-1 iterations (every earlier iteration is done: range barrier)
         for (int j0 = 0; j0 < NBUF - 1 && j0 < nit; ++j0) issue(j0, (int)((gbase + (uint32_t)j0) % NBUF));
-      } else if (!pre_issued) {
-        cur = 0;
+      } else {
         issue(0, 0);
         if (NBUF >= 3 && nit > 1) issue(1, 1);
         if (NBUF >= 4 && nit > 2) issue(2, 2);
       }
-      pre_issued = false;
-      const bool grab = kHandoff && task_ctr != nullptr;   // block-uniform
+      int cur = 0;           // ring slot of iteration it
       bool stored = false;   // global stores issued last iteration (they count in vmcnt)
       for (int it = 0; it < nit; ++it) {
         uint64_t ph_a = 0;
@@ -1120,17 +1092,6 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
         stored = false;
         if constexpr (!ARRIVE) {
           nslot = cur ^ 1;  // 2-deep ring: iteration it+1's slot
-          if (grab && it + 1 == nit) {   // the next range (grabbed at the end of it - 1): its first tiles
-            const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1)]);
-            const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1) + 1]);
-            handed = true;
-            nx_begin = static_docs + (int64_t)o;
-            nx_end = sz > 0 && nx_begin < n ? (nx_begin + sz < n ? nx_begin + sz : n) : nx_begin;
-            if (nx_begin < nx_end && loader) {
-#pragma unroll
-              for (int jj = 0; jj < kPiecesPerWave; ++jj) issue_piece_at(nx_begin, (int)(nx_end - nx_begin), 0, nslot, jj);
-            }
-          }
           if (NBUF == 2 && !SPREAD && it + 1 < nit) issue(it + 1, nslot);
           if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
           if (NBUF == 4 && it + 3 < nit) issue(it + 3, (cur + 3) & 3);
@@ -1260,22 +1221,10 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           asm volatile("" ::: "memory");
           if (lane == 0) __hip_atomic_store(sync_done + wave, (int)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (grab && it + 2 == nit && threadIdx.x == 0) {   // the hand-off's grab (its return waits with it + 1's data)
-          next_task_sliced(task_ctr + tail_slices * qg, tail_slices, bid & 7, task_docs, (int)(n - static_docs),
-                           nwg / nq_groups, task_slot + 2 * (k & 1));
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // in LDS before this wave reaches the next barrier
-        }
       }
       if constexpr (ARRIVE) gbase += (uint32_t)nit;
     }
     if (task_ctr == nullptr) break;
-    if (kHandoff && handed) {   // the next range was grabbed and its first iteration issued above
-      if (nx_begin >= nx_end) break;
-      d_begin = nx_begin;
-      d_end = nx_end;
-      pre_issued = true;   // (cur is its slot)
-      continue;
-    }
     // next dynamic task; the barrier also retires every wave's reads of the
     // ring before the next range refills it (two slots: a slow wave may still
     // read slot k&1 while thread 0 fills slot (k+1)&1).
@@ -5821,6 +5770,7 @@ constexpr int kDefaultScan = kScanAuto;
 // same with 4 queries per wave; larger B the 8-wave scan.  Long documents
 // keep the direct scan up to B=8 (kLongDirectMaxB).
 constexpr int kDirectMaxB = 2;
+constexpr int kOneWgMaxB = 2;   // the dense B <= 2 scan: one 4-wave workgroup per CU (scan_maxsim)
 constexpr int kSmallLdsMaxB = 16;
 constexpr int kLongDirectMaxB = 8;
 
@@ -5900,6 +5850,12 @@ constexpr float kScanDynFracSmallB = 0.30f;
 // 1.064 / 1.069 / 1.129 ms.  The 4 x 2 shape (B = 3-8) stays at 0.3 (0.45 and
 // 0.6 are flat or slower at B = 4 / 8, profiles/r02s3_lab_dynfrac_b8.log).
 constexpr float kScanDynFracB16 = 0.60f;
+// The dense B <= 2 one-workgroup-per-CU scan (round 6): a 10 % tail.  Lab,
+// same box (profiles/r06/onewg_*): 125k docs 0.597 (0.3) -> 0.591 ms (0.1),
+// 100k 0.487 -> 0.484, 1M B=2 4.541 -> 4.538.  (Its static split alone is
+// not enough: the odd XCDs stream 17 % behind the even ones at B = 1, and a
+// static split waits for them -- profiles/r06/scan_lab_b1_*_split.log.)
+constexpr float kScanDynFracOneWg = 0.10f;
 constexpr int64_t kMinChunkDocs = 64;
 
 // Fused top-k output of one scan launch: part [B][max_slots][k] keys; the
@@ -6249,6 +6205,19 @@ int scan_maxsim(cbv2_index* ix, const uint16_t* Q, int B, int lq, float* out, in
   }
   switch (variant) {
     case kScan16x4W4Q1:     // 4 queries per workgroup (1 per wave): B = 3-4 without padded query slots
+      // B <= 2 (dense docs: the latency path): ONE workgroup per CU, a 3-deep
+      // ring, waves 0-1 issue the LDS-DMA (SPLITLOAD) -- the waves of padded
+      // query slots idle, so HBM decides: lab, same box, interleaved
+      // (profiles/r06/ringdepth_*): 125k docs B=1 0.634 -> 0.595 ms (6.46 ->
+      // 6.88 TB/s), 100k 0.517 -> 0.494 (3-deep, no SPLITLOAD), 1M 4.594 ->
+      // 4.522; at B = 4 (every slot live) the two-per-CU form stays (4.70 vs
+      // 5.54 ms: one wave per SIMD cannot hide the MFMA latency)
+      if (B <= kOneWgMaxB && bm != nullptr)
+        return launch_scan16x4<4, 1, 1, 2, 3, false, 32, 1, false, 0, true, false, 0, kLd, 0, 2, true>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracOneWg, kScanTaskDocs, nullptr, ctr_ws, nullptr, bm);
+      if (B <= kOneWgMaxB)
+        return launch_scan16x4<4, 1, 1, 2, 3, false, 32, 1, false, 0, true, false, 0, kLd, 0, 2>(
+            ix, Q, B, lq, out, ld_out, st, kScanDynFracOneWg, kScanTaskDocs, nullptr, ctr_ws);
       if (B <= 4 && bm != nullptr)   // the block keys folded in (zeroed by the caller: scan_folds_bmax_zeroed)
         return launch_scan16x4<4, 1, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2, true>(
             ix, Q, B, lq, out, ld_out, st, kScanDynFracSmallB, kScanTaskDocs, nullptr, ctr_ws, nullptr, bm);

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--root", default=ROOT)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--ab-opt", default="",
+                    help="OPT:v0,v1 -- the host-results one-trip leg once per value of that handle option "
+                         "(cbv2_index_set_option, e.g. BAND_LOWER_BOUND:1,0), interleaved")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for n in (int(x) for x in a.docs.split(",")):
@@ -73,13 +76,26 @@ def main():
             legs["one_trip_host"] = onetrip_host
         except TypeError:     # a tree without host results
             pass
+        ab_out = {}
+        if a.ab_opt:
+            from hybrid_rag_colbertv2_amd import _lib
+            oname, vals = a.ab_opt.split(":")
+            oid = getattr(_lib, "OPT_" + oname)
+            for v in (int(x) for x in vals.split(",")):
+                def leg(v=v):
+                    ix.set_option(oid, v)
+                    r = one(Q1, bm_one, host=True)
+                    ix.set_option(oid, int(vals.split(",")[0]))
+                    return r
+                legs[f"one_trip_host[{oname}={v}]"] = leg
+                ab_out[v] = leg()
         lat = {k: [] for k in legs}
         for it in range(a.iters + 5):
             for name, fn in legs.items():
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 out = fn()
-                if name != "one_trip_host":
+                if not name.startswith("one_trip_host"):
                     torch.cuda.synchronize()
                 if it >= 5:
                     lat[name].append((time.perf_counter() - t) * 1e3)
@@ -87,6 +103,8 @@ def main():
         same = all(torch.equal(x, y) for x, y in zip(a_out, b_out))
         if "one_trip_host" in legs:
             same = same and all(np.array_equal(x.cpu().numpy(), y) for x, y in zip(a_out, onetrip_host()))
+        for r in ab_out.values():   # every option value: the same results
+            same = same and all(np.array_equal(x.cpu().numpy(), y) for x, y in zip(a_out, r))
         ix.time_scans(True)
         for _ in range(20):
             ix.search(Q1, 100)
@@ -102,8 +120,9 @@ def main():
                          "min_ms": round(min(v), 4)}
         rec["p50_gain_us"] = round((rec["composed"]["p50_ms"] - rec["one_trip"]["p50_ms"]) * 1e3, 1)
         rec["one_trip_minus_scan_us"] = round((rec["one_trip"]["p50_ms"] - scan) * 1e3, 1)
-        if "one_trip_host" in rec:
-            rec["one_trip_host_minus_scan_us"] = round((rec["one_trip_host"]["p50_ms"] - scan) * 1e3, 1)
+        for name in list(rec):
+            if name.startswith("one_trip_host"):
+                rec[name + "_minus_scan_us"] = round((rec[name]["p50_ms"] - scan) * 1e3, 1)
         print(json.dumps(rec), flush=True)
         del ix, one, lex
 
