@@ -105,6 +105,10 @@ def main():
             same = same and all(np.array_equal(x.cpu().numpy(), y) for x, y in zip(a_out, onetrip_host()))
         for r in ab_out.values():   # every option value: the same results
             same = same and all(np.array_equal(x.cpu().numpy(), y) for x, y in zip(a_out, r))
+        band = None
+        if f32:   # the faithful band of the query (docs rescored exactly), as the call sizes it
+            ix.search(Q1, 100)
+            band = int(getattr(ix, "last_band").cpu()[0])
         ix.time_scans(True)
         for _ in range(20):
             ix.search(Q1, 100)
@@ -114,7 +118,7 @@ def main():
         from hybrid_rag_colbertv2_amd import _lib
         rec = {"tag": a.tag, "lib": _lib.lib().cbv2_build_stamp().decode(), "docs": n, "dtype": a.dtype, "B": B,
                "iters": a.iters, "scan_event_ms_p50": round(scan, 4),
-               "identical": same, "top10": [int(x) for x in b_out[1][0][:3]]}
+               "identical": same, "top10": [int(x) for x in b_out[1][0][:3]], "faithful_band_docs": band}
         for name, v in lat.items():
             rec[name] = {"p50_ms": round(statistics.median(v), 4), "p99_ms": round(float(np.percentile(v, 99)), 4),
                          "min_ms": round(min(v), 4)}

@@ -527,6 +527,21 @@ extern "C" int lab_scan_f8(cbv2_index* ix, int variant, const void* Qbuf, int B,
   const uint8_t* Qb = (const uint8_t*)Qbuf;
   const uint8_t* Qs = Qb + (size_t)B * lq * kDim;
   hipStream_t st = (hipStream_t)stream;
+  // 300 / 301 (round 6): the dense B <= 2 shape (24: 4 waves x 1 query, 3-deep
+  // ring, nt) at ONE workgroup per CU, without / with SPLIT (waves 0-1 load);
+  // 302: the production shape 24 (two per CU) at a 10 % tail
+  if (variant == 300)
+    return launch_f8x4<32, 3, true, 1, 1, 1, 4, 0, kLd, 1, true, false, false, false, false, 0, 2>(
+        ix, Qb, Qs, B, lq, out, ld, st, kF8DynB8, kScanTaskDocs, nullptr);
+  if (variant == 301)
+    return launch_f8x4<32, 3, true, 1, 1, 1, 4, 0, kLd, 1, true, false, false, true, false, 0, 2>(
+        ix, Qb, Qs, B, lq, out, ld, st, kF8DynB8, kScanTaskDocs, nullptr);
+  if (variant == 302)
+    return launch_f8x4<32, 3, true, 1, 2, 2, 4, 0, kLd, 1, true, false, false, false, false, 0, 2>(
+        ix, Qb, Qs, B, lq, out, ld, st, 0.1f, kScanTaskDocs, nullptr);
+  if (variant == 303)
+    return launch_f8x4<32, 3, true, 1, 1, 1, 4, 0, kLd, 1, true, false, false, true, false, 0, 2>(
+        ix, Qb, Qs, B, lq, out, ld, st, 0.1f, kScanTaskDocs, nullptr);
   if (variant >= 200 && variant < 300) {   // 200 + mult: the f8 direct scan (QW = 2) with mult x the resident waves
     constexpr int QW = 2;
     const int nq_groups = (B + QW - 1) / QW;
