@@ -17,7 +17,9 @@ One STEP = one batch of B=256 queries through the whole path:
            top-100 -> RCCL all-gather -> HIP merge (the ranks' BM25 lists over
            their doc shards ride the same all-gather),
   fusion   host RRF (native C++, reference semantics) -> top-50 candidates,
-  stage 3  HIP gather-by-id MaxSim rerank -> top-10 (sharded: RCCL all-reduce MAX).
+  stage 3  HIP gather-by-id MaxSim rerank -> top-10 (sharded: no collective -- the
+           fused candidates' rerank scores ride the stage-2 all-gather: each
+           rank's top-k scores and its prescored BM25 list).
 Inputs (the query batch and term ids, both indexes) are resident before the
 timed region; every stage runs in full inside every timed step.
 
@@ -736,8 +738,8 @@ def main():
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
                        "index_dtype": args.dtype,
                        "parallelism": f"corpus sharded x{world}" + (
-                           ((" (RCCL all-gather + all-reduce, " + ("native in-ABI" if args.native_exchange
-                                                                   else "torch.distributed") + " exchange)")
+                           ((" (RCCL all-gather, stage 3 without a collective, " + (
+                               "native in-ABI" if args.native_exchange else "torch.distributed") + " exchange)")
                             if nccl else f" ({backend} rehearsal: ranks share one GPU)")
                            if world > 1 else "")},
             "p50_ms_b1": round(p50, 3) if p50 is not None else None,
