@@ -386,6 +386,10 @@ def main():
                     help="BASELINE configs 4 / 5 (10M docs sharded over the ranks, stage 2, bf16 and MXFP8) as "
                          "extra legs of the line; auto = at 8 ranks (the configs' node)")
     ap.add_argument("--c45-docs", type=int, default=10_000_000, help="corpus of the config-4/5 legs")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N>1: query-level data-parallel replicas (SURVEY §8(e), the alternative for config 3): "
+                         "every rank holds the WHOLE corpus and runs its own query batches, no collective; "
+                         "value = N x the per-rank rate (weak scaling).  Default: the corpus sharded (strong).")
     ap.add_argument("--dtype", choices=["fp32", "bf16", "fp8"], default="fp32",
                     help="index: fp32-faithful (default: the reference's fp32 arithmetic, LRC:735-746 / 802-831, "
                          "within 1e-4 -- bf16 hi scanned + residual-certified band, DESIGN §3.7), bf16 tokens, "
@@ -414,14 +418,18 @@ def main():
             dist.init_process_group(backend)
 
     B, n_total = args.batch, args.docs
-    begin, end = shard_range(n_total, rank, world)
+    replicas = args.replicas and world > 1
+    begin, end = (0, n_total) if replicas else shard_range(n_total, rank, world)
     n_local = end - begin
     t_setup = time.time()
     Qf = synth.make_queries(B, LQ, seed=1)
     planted = synth.planted_ids(B, n_total, 10, seed=2)
     t_bm = time.time()
     bm_terms, bm_off, vocab = synth.bm25_shard(begin, end, planted)
-    lex = bm25_mod.sharded(bm_terms, bm_off, vocab, id_base=begin, device=dev)   # global stats: 1 all-reduce
+    if replicas:   # the whole BM25 index on every rank (its own statistics: no all-reduce)
+        lex = bm25_mod.NativeBM25(bm_terms, bm_off, vocab)
+    else:
+        lex = bm25_mod.sharded(bm_terms, bm_off, vocab, id_base=begin, device=dev)   # global stats: 1 all-reduce
     del bm_terms, bm_off
     qt, qo = synth.bm25_queries(B)
     log(f"host BM25 shard built in {time.time() - t_bm:.1f}s ({lex.n_docs} docs, {len(lex.doc_terms)} terms)")
@@ -441,8 +449,9 @@ def main():
     if args.fused_topk:
         from hybrid_rag_colbertv2_amd import _lib
         ix.set_option(_lib.OPT_FUSED_TOPK, 1)
-    nccl = world > 1 and backend == "nccl"
-    searcher = ShardedSearcher(ix, native=args.native_exchange and nccl, lexical_k=args.k)
+    nccl = world > 1 and backend == "nccl" and not replicas
+    searcher = (ShardedSearcher(ix, world=1, lexical_k=args.k) if replicas else   # a replica: the one-shard path
+                ShardedSearcher(ix, native=args.native_exchange and nccl, lexical_k=args.k))
     Q = Qf.to(dev, torch.float32 if faithful else torch.bfloat16)
     Q1 = Q[:1].contiguous()
     torch.cuda.synchronize()
@@ -507,7 +516,7 @@ def main():
     scan_clk = ix.scan_clock()
     scan_ms = scan_ms[-args.steps:] if len(scan_ms) >= args.steps else scan_ms
     band_ms = ix.band_times()[-args.steps:] if faithful else []
-    qps = B * args.steps / elapsed
+    qps = B * args.steps / elapsed * (world if replicas else 1)   # replicas: every rank ran its own K batches
     band = None
     if faithful:                         # the band each query of the last timed batch rescored
         bs = ix.last_band.float()
@@ -652,12 +661,13 @@ def main():
         def side_prepare():
             if faithful:
                 six = ColbertIndex(ix.tokens, ix.doclens, id_base=begin)
-                ssrch = ShardedSearcher(six, native=nccl and native is not None and "error" not in native,
+                ssrch = ShardedSearcher(six, world=1, lexical_k=args.k) if replicas else ShardedSearcher(
+                    six, native=nccl and native is not None and "error" not in native,
                                         lexical_k=args.k)
                 return six, ssrch, Q.to(torch.bfloat16), None
             f32, dl32 = synth.make_shard(begin, end, Qf, planted, dev, seed=0, dtype=torch.float32)
             six = ColbertIndex.faithful_f32(f32, dl32, id_base=begin)
-            return six, ShardedSearcher(six, lexical_k=args.k), Qf.to(dev), f32
+            return six, ShardedSearcher(six, world=1 if replicas else None, lexical_k=args.k), Qf.to(dev), f32
 
         def side_run(st):
             six, ssrch, Qs, f32 = st
@@ -675,7 +685,8 @@ def main():
             else:
                 sbad = spot_check(sfs, sfi_h, Qs.float().cpu().numpy(), lambda sel: six.tokens[sel].float().cpu().numpy(),
                                   begin, end, check_rows, 1e-3, world, dev)
-            res = {"value": round(B * args.steps / sel, 2), "ms_per_step": round(sel / args.steps * 1e3, 3),
+            res = {"value": round(B * args.steps / sel * (world if replicas else 1), 2),
+                   "ms_per_step": round(sel / args.steps * 1e3, 3),
                    "scan_avg_ms": round(sum(sscan) / len(sscan), 3) if sscan else None,
                    "p50_ms_b1": round(sp50, 3) if sp50 is not None else None,
                    "p99_ms_b1": round(sp99, 3) if sp99 is not None else None,
@@ -701,7 +712,7 @@ def main():
     # ---- BASELINE configs 4 and 5 on the node (8 ranks): the 10M-doc corpus
     # sharded over the ranks, stage 2 (scan + top-100 + ONE all-gather + merge)
     c45 = None
-    if args.c45 == "on" or (args.c45 == "auto" and world == 8 and args.dtype in ("fp32", "bf16")):
+    if args.c45 == "on" or (args.c45 == "auto" and world == 8 and args.dtype in ("fp32", "bf16") and not replicas):
         one = searcher = ix = tokens = None   # noqa: F841  free HBM for the 10M-doc shards
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
@@ -729,7 +740,7 @@ def main():
             "metric": "queries/sec + p50 retrieval latency, 1M-chunk corpus, top-10 rerank",
             "value": mine["value"], "unit": "queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": mine["ms_per_step"],
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak" if replicas else "strong", "vs_baseline": None,
             "dtype": "fp32 (faithful: bf16 hi/lo split, fp32 accumulate)" if faithful else args.dtype,
             "data": "synthetic (unit-norm N(0,I) tokens, Zipf term-id corpus for BM25, 10 planted positives/query)",
             "config": {"workload": workload + f": {n_total} chunks x 128 tokens x 128-d, host BM25 top-100 + "
@@ -737,7 +748,8 @@ def main():
                        "corpus_docs": n_total, "docs_per_gpu": n_local, "global_batch": B, "lq": LQ, "ld": LD,
                        "dim": DIM, "colbert_k": args.k, "fused": args.fused, "final_k": args.final_k,
                        "index_dtype": args.dtype,
-                       "parallelism": f"corpus sharded x{world}" + (
+                       "parallelism": f"query replicas x{world} (the whole corpus on every GPU, no collective)"
+                       if replicas else f"corpus sharded x{world}" + (
                            ((" (RCCL all-gather, stage 3 without a collective, " + (
                                "native in-ABI" if args.native_exchange else "torch.distributed") + " exchange)")
                             if nccl else f" ({backend} rehearsal: ranks share one GPU)")
