@@ -848,6 +848,26 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
   slot[0] = 0;
   slot[1] = 0;
 }
+// The task of ticket t of the first slice next_task_sliced would try (the
+// scan's task hand-off draws it an iteration before it needs the task); size
+// -1: that slice is drained -- the caller takes the drained path, whose
+// next_task_sliced goes on to the other slices (no atomic with a return in
+// the scan's loop but the one ticket: the waitcnt pass would otherwise keep
+// its pending return against the VGPRs the loop's LDS reads reuse).
+__device__ __forceinline__ void task_from_ticket(int t, int nsl, int xcd, int task_docs, int dyn, int P, int* slot) {
+  const int sl = xcd % nsl;
+  const int lo = tail_slice_lo(sl, nsl, dyn);
+  const int sdyn = tail_slice_lo(sl + 1, nsl, dyn) - lo;
+  int o, sz;
+  if (task_docs > 0) {
+    o = t * task_docs;
+    sz = o < sdyn ? (sdyn - o < task_docs ? sdyn - o : task_docs) : 0;
+  } else {
+    ticket_task(t, sdyn, P, -task_docs, o, sz);
+  }
+  slot[0] = o + lo;
+  slot[1] = sz > 0 ? sz : -1;
+}
 
 // Work split (per query group of QPB queries): docs [0, static_docs) in equal
 // chunks, one per workgroup, XCD-aware as above; then, if task_ctr is given,
@@ -876,6 +896,9 @@ __device__ __forceinline__ void next_task_sliced(int* ctr, int nsl, int xcd, int
 // an NBUF-deep ring lets the loaders run up to NBUF-2 iterations ahead.
 #ifndef CBV2_F8_D47
 #define CBV2_F8_D47 1   // lab A/B builds set 3
+#endif
+#ifndef CBV2_SCAN_HANDOFF
+#define CBV2_SCAN_HANDOFF 1   // lab A/B builds set 0: drained task switches (before round 6)
 #endif
 #ifndef CBV2_SCAN_QSKIP
 #define CBV2_SCAN_QSKIP 1   // lab A/B builds set 0
@@ -971,6 +994,12 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   bf16x8 qf[QW][2][4];
 #pragma unroll
   for (int q = 0; q < QW; ++q) load_qfrag16(Q, qg * QPB + wave * QW + q, B, lq, lane, qf[q]);
+  // (kHandoff: the fragments are in VGPRs before any range starts, as the
+  // waitcnt pass sees it -- a range entered with its ring pre-issued issues
+  // no load of its own, and the pass would otherwise wait vmcnt(0) before
+  // every iteration's first MFMA)
+  if constexpr (CBV2_SCAN_HANDOFF && NBUF == 3 && TPI == 32 && SPLITLOAD && !ARRIVE && !SPREAD)
+    __builtin_amdgcn_s_waitcnt(0);
 
   // LDS-DMA piece p = rows 4p..4p+3 of the image [4 docs][TPI tokens] = doc
   // 4p / TPI, tokens TPI*j + 4p % TPI + 0..3; slot XOR (doc << 2 | R & 3)
@@ -1006,24 +1035,42 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
   // (tiles + epilogue, to the next iteration's top) -- and the iteration count
   uint64_t ph_wait = 0, ph_issue = 0, ph_comp = 0, ph_n = 0, ph_t = 0;
 
+  // Task hand-off (3-deep ring, loading waves 0 .. WAVES/2-1: the dense B <= 2
+  // one-per-CU scan): the next range is grabbed by the last (never loading)
+  // wave four iterations before the current range ends, read after the
+  // barrier of the second-last iteration, and its first two iterations go
+  // into the ring where the current range's would have gone -- a task switch
+  // drains nothing.  Lab, same box, interleaved (profiles/r06/handoff3_*):
+  // B = 1 125k docs 0.594 -> 0.591 ms, 100k 0.486 -> 0.481, 1M 4.454 ->
+  // 4.445; bit-identical scores.
+  constexpr bool kHandoff =
+      CBV2_SCAN_HANDOFF && !CBV2_TAIL_CAS && NBUF == 3 && TPI == 32 && SPLITLOAD && !ARRIVE && !SPREAD;
+  // iteration it of the range [rb, rb + rnd) into ring slot buf
+  auto issue_piece_at = [&](int64_t rb, int rnd, int it, int buf, int jj) {
+    const int G = it / IPG, j = it % IPG;
+    const int piece = lwave * kPiecesPerWave + jj;
+    int pdoc;
+    const uint32_t poff = piece_src(jj, pdoc);
+    int d = 4 * G + pdoc;
+    d = d < rnd ? d : rnd - 1;  // the last group's missing docs: any valid doc (rows masked)
+    const uint8_t* src = tokens + (size_t)(rb + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16, 0,
+                                     AUX);
+  };
+
   // the first range: this workgroup's static chunk (may be empty)
   int64_t d_begin = chunk * chunk_docs;
   int64_t d_end = d_begin + chunk_docs < static_docs ? d_begin + chunk_docs : static_docs;
+  int cur = 0;               // ring slot of iteration it
+  bool pre_issued = false;   // kHandoff: this range's first two iterations are in the ring already
+  int grab_t = 0;            // kHandoff: the ticket drawn (last wave, lane 0)
   for (int k = 0;; ++k) {
+    bool handed = false;                  // kHandoff: the next range was grabbed inside this one
+    int64_t nx_begin = 0, nx_end = 0;     // ... and it is [nx_begin, nx_end) (empty: none)
     if (d_begin < d_end) {
       const int nd = (int)(d_end - d_begin);
       const int ngr = (nd + 3) >> 2;
-      auto issue_piece = [&](int it, int buf, int jj) {
-        const int G = it / IPG, j = it % IPG;
-        const int piece = lwave * kPiecesPerWave + jj;
-        int pdoc;
-        const uint32_t poff = piece_src(jj, pdoc);
-        int d = 4 * G + pdoc;
-        d = d < nd ? d : nd - 1;  // the last group's missing docs: any valid doc (rows masked)
-        const uint8_t* src = tokens + (size_t)(d_begin + d) * kDocStride + (size_t)j * TPI * kRowBytes + poff;
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + buf * kIterBytes + piece * 1024), 16,
-                                         0, AUX);
-      };
+      auto issue_piece = [&](int it, int buf, int jj) { issue_piece_at(d_begin, nd, it, buf, jj); };
       auto issue = [&](int it, int buf) {
         if (!loader || (PROBE == 2 && it >= NBUF)) return;   // PROBE 2 (INVALID): no streaming after the first fill
 #pragma unroll
@@ -1036,15 +1083,18 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
       for (int q = 0; q < QW; ++q) sc[q] = 0.0f, m[q][0] = m[q][1] = neg_inf();
       int dl_g = 0, dl_min = 0, dl_max = 0;
 
-      const int nit = IPG * ngr;
+      const int nit = IPG * ngr;   // (kHandoff: >= 4)
       if constexpr (ARRIVE) {   // the first NBUF-1 iterations (every earlier iteration is done: range barrier)
         for (int j0 = 0; j0 < NBUF - 1 && j0 < nit; ++j0) issue(j0, (int)((gbase + (uint32_t)j0) % NBUF));
-      } else {
+      } else if (!pre_issued) {
+        cur = 0;
         issue(0, 0);
         if (NBUF >= 3 && nit > 1) issue(1, 1);
         if (NBUF >= 4 && nit > 2) issue(2, 2);
       }
-      int cur = 0;           // ring slot of iteration it
+      pre_issued = false;
+      const bool grab = kHandoff && task_ctr != nullptr;   // block-uniform
+      const int grab_it = nit - 4;                         // (>= 0)
       bool stored = false;   // global stores issued last iteration (they count in vmcnt)
       for (int it = 0; it < nit; ++it) {
         uint64_t ph_a = 0;
@@ -1075,9 +1125,13 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           buf = smem + (gi % NBUF) * kIterBytes;
         } else {
           // it landed; the younger iterations issued (NBUF - 2 at most) stay in flight
-          if (NBUF == 4 && it + 2 < nit && !stored)
+          // (a hand-off: the next range's first iteration is the younger one
+          // at it = nit - 1; a wait behind stores drains the ring: round 6
+          // lab, not draining there measured neutral)
+          const bool drain = stored;
+          if (NBUF == 4 && it + 2 < nit && !drain)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPiecesPerWave) : "memory");
-          else if (NBUF >= 3 && it + 1 < nit && !stored)
+          else if (NBUF >= 3 && (it + 1 < nit || nx_begin < nx_end) && !drain)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiecesPerWave) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1094,6 +1148,20 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           nslot = cur ^ 1;  // 2-deep ring: iteration it+1's slot
           if (NBUF == 2 && !SPREAD && it + 1 < nit) issue(it + 1, nslot);
           if (NBUF == 3 && it + 2 < nit) issue(it + 2, cur == 0 ? 2 : cur - 1);
+          if (grab && it + 2 >= nit) {   // the next range's iteration it + 2 - nit (its own issue site:
+            if (it + 2 == nit) {         // the common one keeps its hoisted addresses)
+              const int o = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1)]);
+              const int sz = __builtin_amdgcn_readfirstlane(task_slot[2 * (k & 1) + 1]);
+              handed = sz >= 0;   // (-1: the own tail slice is drained -- the drained switch)
+              nx_begin = static_docs + (int64_t)o;
+              nx_end = sz > 0 && nx_begin < n ? (nx_begin + sz < n ? nx_begin + sz : n) : nx_begin;
+            }
+            if (nx_begin < nx_end && loader) {
+#pragma unroll
+              for (int jj = 0; jj < kPiecesPerWave; ++jj)
+                issue_piece_at(nx_begin, (int)(nx_end - nx_begin), it + 2 - nit, cur == 0 ? 2 : cur - 1, jj);
+            }
+          }
           if (NBUF == 4 && it + 3 < nit) issue(it + 3, (cur + 3) & 3);
           buf = smem + cur * kIterBytes;
           cur = NBUF == 2 ? (cur ^ 1) : NBUF == 3 ? (cur == 2 ? 0 : cur + 1) : ((cur + 1) & 3);
@@ -1221,10 +1289,31 @@ __global__ __launch_bounds__(WAVES * 64, OCC) void maxsim_scan16x4_kernel(
           asm volatile("" ::: "memory");
           if (lane == 0) __hip_atomic_store(sync_done + wave, (int)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        // the hand-off's grab by the last wave (never a loader: waiting for
+        // its atomic drains no ring; a wave-uniform branch, so no other wave
+        // executes that wait): the ticket at grab_it, the task in LDS before
+        // that wave's barrier of iteration nit - 2
+        if (grab && wave == WAVES - 1 && (it == grab_it || it == grab_it + 1)) {
+          if (it == grab_it) {
+            if (lane == 0) grab_t = atomicAdd(task_ctr + tail_slices * qg + (bid & 7) % tail_slices, 1);
+          } else {
+            if (lane == 0)
+              task_from_ticket(grab_t, tail_slices, bid & 7, task_docs, (int)(n - static_docs), nwg / nq_groups,
+                               task_slot + 2 * (k & 1));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+        }
       }
       if constexpr (ARRIVE) gbase += (uint32_t)nit;
     }
     if (task_ctr == nullptr) break;
+    if (kHandoff && handed) {   // the next range was grabbed and its first two iterations issued above
+      if (nx_begin >= nx_end) break;
+      d_begin = nx_begin;
+      d_end = nx_end;
+      pre_issued = true;   // (cur is its first slot)
+      continue;
+    }
     // next dynamic task; the barrier also retires every wave's reads of the
     // ring before the next range refills it (two slots: a slow wave may still
     // read slot k&1 while thread 0 fills slot (k+1)&1).
@@ -5977,7 +6066,7 @@ int plan_split(cbv2_index* ix, int nq_groups, int64_t target, float dyn_frac, in
   int64_t n_chunks = target / nq_groups;   // never more workgroups than resident slots
   if (n_chunks < 1) n_chunks = 1;
   if (n_chunks > ix->n) n_chunks = ix->n;
-  sp->task_docs = task_docs > 0 ? std::max(64, task_docs & ~63) : -std::max(16, (-task_docs) & ~15);
+  sp->task_docs = task_docs > 0 ? std::max(64, task_docs & ~63) : -std::max(4, (-task_docs) & ~3);
   sp->ctr = nullptr;
   sp->ring_slot = -1;
   const int64_t tail_chunk = ((int64_t)((double)ix->n * (1.0 - (double)dyn_frac)) / n_chunks) & ~(int64_t)63;

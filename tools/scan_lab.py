@@ -25,7 +25,7 @@ from oracle import oracle as orc  # noqa: E402
 LAB = os.path.join(ROOT, "tools", "_build", "libscanlab.so")
 # "n:" variants run in a second build with the -D flags of ALT_DEFS (env
 # SCANLAB_ALT_DEFS; default: the round-1 CAS task grab of the dynamic tail)
-LAB_NT = os.path.join(ROOT, "tools", "_build", "libscanlab_alt.so")
+LAB_NT = os.environ.get("SCANLAB_ALT_LIB") or os.path.join(ROOT, "tools", "_build", "libscanlab_alt.so")
 ALT_DEFS = os.environ.get("SCANLAB_ALT_DEFS", "-DCBV2_TAIL_CAS=1").split()
 
 
