@@ -467,6 +467,23 @@ extern "C" int lab_scan16x4(cbv2_index* ix, const void* Q, int B, int lq, float*
   if (kind == 41)
     return launch_scan16x4<4, 2, 2, 2, 2, false, 32, 2, false, 0, false, false, 0, kLd, 0, 2>(
         ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr);
+  // kind 42: the production dense B <= 2 scan WITH the block-max keys folded
+  // in (the latency path's form; kind 37 is the same without them): the keys
+  // zeroed by a memset inside the timed region (as the query split does in
+  // the product)
+  if (kind == 42) {
+    static uint32_t* bm = nullptr;
+    static size_t bm_bytes = 0;
+    const size_t need = (size_t)B * (bm_blocks(ix->n) + bm_supers(ix->n)) * 4;
+    if (need > bm_bytes) {
+      if (bm) (void)hipFree(bm);
+      if (hipMalloc(&bm, need) != hipSuccess) return -2;
+      bm_bytes = need;
+    }
+    if (hipMemsetAsync(bm, 0, need, st) != hipSuccess) return -3;
+    return launch_scan16x4<4, 1, 1, 2, 3, false, 32, 1, false, 0, true, false, 0, kLd, 0, 2, true>(
+        ix, q, B, lq, out, ld, st, dyn_frac, task_docs, nullptr, nullptr, nullptr, bm);
+  }
   if (kind != 0) return -1;
   if (stamps != nullptr)
     return launch_scan16x4<8, 4, 1, 2, 2, true, 64>(ix, q, B, lq, out, ld, st, dyn_frac, task_docs,
