@@ -529,9 +529,11 @@ def test_dense_docs_scan_equals_stream(dev, B, fp8):
     tiles hold tokens): B <= 2 streams every slot on the 4 x 1 doc-interleaved
     scan (bf16 or MXFP8) instead of the tile-skipping streaming scan, the
     block-max top-k then runs its own block maxima.  Scores and top-k equal the streaming scan's bit
-    for bit; a ragged index keeps the streaming scan."""
+    for bit -- with the dynamic tail in XCD slices (the bf16 scan's task
+    hand-off, round 6), one shared tail and none; a ragged index keeps the
+    streaming scan."""
     from hybrid_rag_colbertv2_amd import _lib, synth
-    n = 70_000                                    # past the block-max select's threshold
+    n = 70_003                                    # past the block-max select's threshold; ragged slices
     Qf = synth.make_queries(B, 32, seed=3)
     planted = synth.planted_ids(B, n, 10, seed=4)
     tok, dl = synth.make_shard(0, n, Qf, planted, dev, seed=5)
@@ -540,12 +542,17 @@ def test_dense_docs_scan_equals_stream(dev, B, fp8):
     assert ix.dense_docs
     Q = Qf.to(dev, torch.bfloat16)
     got = {}
-    for dense in (1, 0):
+    for dense, tail in ((0, 1), (1, 1), (1, 2), (1, 0)):
         ix.set_option(_lib.OPT_DENSE_DOCS, dense)
+        ix.set_option(_lib.OPT_DYNAMIC_TAIL, tail)
         s, i = ix.search(Q, 100)
-        got[dense] = (s.clone(), i.clone(), ix.score(Q).clone())
-    for a, b in zip(got[1], got[0]):
-        assert torch.equal(a, b)
+        got[dense, tail] = (s.clone(), i.clone(), ix.score(Q).clone())
+        if dense and tail and not fp8:
+            assert ix.last_scan_plan()["dynamic_tail"], (tail, ix.last_scan_plan())
+    ix.set_option(_lib.OPT_DYNAMIC_TAIL, 1)
+    for key in ((1, 1), (1, 2), (1, 0)):
+        for a, b in zip(got[key], got[0, 1]):
+            assert torch.equal(a, b), key
     dl2 = dl.clone()
     dl2[::3] = 40
     assert not (ColbertIndex.mxfp8(tok, dl2) if fp8 else ColbertIndex(tok, dl2)).dense_docs
