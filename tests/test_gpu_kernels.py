@@ -558,6 +558,38 @@ def test_dense_docs_scan_equals_stream(dev, B, fp8):
     assert not (ColbertIndex.mxfp8(tok, dl2) if fp8 else ColbertIndex(tok, dl2)).dense_docs
 
 
+@pytest.mark.parametrize("B", [1, 2])
+def test_dense_scan_handoff_covers_every_doc(dev, B):
+    """The dense B <= 2 scan hands its tail tasks off inside the ring (round
+    6): through the C ABI into a NaN-filled buffer, with the tail in XCD
+    slices and shared, every score is written once and equals the streaming
+    scan's bits (a doc skipped by a hand-off would stay NaN)."""
+    from hybrid_rag_colbertv2_amd import _lib, synth
+    from hybrid_rag_colbertv2_amd.index import _stream_ptr
+    n = 90_011
+    Qf = synth.make_queries(B, 32, seed=7)
+    planted = synth.planted_ids(B, n, 10, seed=8)
+    tok, dl = synth.make_shard(0, n, Qf, planted, dev, seed=9)
+    ix = ColbertIndex(tok, dl)
+    assert ix.dense_docs
+    Q = Qf.to(dev, torch.bfloat16).contiguous()
+    ix.set_option(_lib.OPT_DENSE_DOCS, 0)
+    want = ix.score(Q).clone()                     # the streaming scan
+    ix.set_option(_lib.OPT_DENSE_DOCS, 1)
+    _keep, qptr, qdt, _, _ = ix._prep_query(Q, "maxsim")
+    for tail in (1, 2):
+        ix.set_option(_lib.OPT_DYNAMIC_TAIL, tail)
+        out = torch.full((B, n), float("nan"), device=dev)
+        _lib.check(_lib.lib().cbv2_score(ix._h, _lib.SCORERS["maxsim"], qptr, qdt, B, 32, out.data_ptr(), n,
+                                         _stream_ptr(dev)))
+        torch.cuda.synchronize()
+        plan = ix.last_scan_plan()
+        assert plan["dynamic_tail"] and 0 < plan["static_docs"] < n, (tail, plan)
+        assert not torch.isnan(out).any(), tail
+        assert torch.equal(out, want), tail
+    ix.set_option(_lib.OPT_DYNAMIC_TAIL, 1)
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("dense", [False, True])
 @pytest.mark.parametrize("B", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 15, 16])
