@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Soak of the one-round-trip retrieve (cbv2_retrieve_begin / _finish[_host],
+hybrid.OneTripRetriever) against the same stages called one by one, for a
+bounded time: random batch sizes (the host-rerank B <= 8 path, the GPU-rerank
+path beyond), bf16 / fp32-faithful / MXFP8 shards, dense-doc (one-workgroup
+B <= 2 scan with its task hand-off) and ragged indexes, a BM25 callable / a
+host id array / no stage 1, device or host results.  Every call must equal
+the composed stages bit for bit; the first mismatch is printed and counted.
+A lab tool (GPU box), not a test: the tests pin each path once, this looks
+for rare host/device protocol races over thousands of calls.
+usage: stress_onetrip.py [--seconds S] [--docs N]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from hybrid_rag_colbertv2_amd import synth  # noqa: E402
+from hybrid_rag_colbertv2_amd.bm25 import NativeBM25  # noqa: E402
+from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, rrf_fuse  # noqa: E402
+from hybrid_rag_colbertv2_amd.index import ColbertIndex  # noqa: E402
+
+K, KB, C, KF = 100, 100, 50, 10
+BATCHES = (1, 1, 1, 2, 2, 3, 5, 8, 17)
+
+
+def composed(index, Q, lex_ids):
+    _, ids = index.search(Q, K)
+    bm = np.zeros((ids.shape[0], 0), np.int32) if lex_ids is None else lex_ids
+    cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=C)
+    return index.rerank(Q, torch.from_numpy(cand).to(index.device), KF)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=180.0)
+    ap.add_argument("--docs", type=int, default=125_000)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    bmax = max(BATCHES)
+    Qf = synth.make_queries(bmax, seed=11)
+    planted = synth.planted_ids(bmax, a.docs, 10, seed=12)
+    tok32, dl = synth.make_shard(0, a.docs, Qf, planted, dev, dtype=torch.float32)
+    tok16 = tok32.to(torch.bfloat16)
+    dl_ragged = dl.clone()
+    dl_ragged[::3] = torch.randint(0, 129, (len(dl_ragged[::3]),), device=dev, dtype=torch.int32)
+    dl_ragged[torch.from_numpy(planted.reshape(-1)).to(dev)] = 128
+    terms, off, V = synth.bm25_shard(0, a.docs, planted)
+    lex = NativeBM25(terms, off, V)
+    qt, qo = synth.bm25_queries(bmax)
+    shards = {
+        "bf16 dense": (ColbertIndex(tok16, dl), torch.bfloat16),
+        "bf16 ragged": (ColbertIndex(tok16, dl_ragged), torch.bfloat16),
+        "fp32 dense": (ColbertIndex.faithful_f32(tok32, dl), torch.float32),
+        "fp8 dense": (ColbertIndex.mxfp8(tok16, dl), torch.bfloat16),
+    }
+    del tok32
+    rets = {name: OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF) for name, (ix, _) in shards.items()}
+    rng = np.random.default_rng(5)
+    t0 = time.time()
+    t_print = t0
+    calls = mism = 0
+    per = {}
+    while time.time() - t0 < a.seconds:
+        name = list(shards)[rng.integers(len(shards))]
+        ix, qdt = shards[name]
+        B = int(BATCHES[rng.integers(len(BATCHES))])
+        b0 = int(rng.integers(0, bmax - B + 1))
+        Q = Qf[b0:b0 + B].to(dev, qdt).contiguous()
+        bm_i, bm_s = lex.search(qt[qo[b0]:qo[b0 + B]], qo[b0:b0 + B + 1] - qo[b0], KB)
+        mode = int(rng.integers(3))
+        lexical, lex_ids = ((lambda: (bm_i, bm_s)), bm_i) if mode == 0 else ((bm_i, bm_i) if mode == 1 else (None, None))
+        host = bool(rng.integers(2))
+        got = rets[name](Q, lexical, host=host)
+        want = composed(ix, Q, lex_ids)
+        torch.cuda.synchronize()
+        ok = all(np.array_equal(np.asarray(g if host else g.cpu()), w.cpu().numpy()) for g, w in zip(got, want))
+        calls += 1
+        per[name] = per.get(name, 0) + 1
+        if not ok:
+            mism += 1
+            if mism <= 3:
+                print(f"MISMATCH #{mism}: {name} B={B} rows {b0}.. mode {mode} host {host}", flush=True)
+        if time.time() - t_print > 20:
+            t_print = time.time()
+            print(f"{t_print - t0:.0f}s: {calls} calls, {mism} mismatches", flush=True)
+    print({"calls": calls, "mismatches": mism, "per_shard": per, "seconds": round(time.time() - t0, 1),
+           "docs": a.docs}, flush=True)
+    sys.exit(1 if mism else 0)
+
+
+if __name__ == "__main__":
+    main()
