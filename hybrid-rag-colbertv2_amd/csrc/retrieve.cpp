@@ -141,8 +141,24 @@ struct MappedBuf {
   size_t bytes = 0;
   hipEvent_t ev = nullptr;
   bool recorded = false;
-  uint32_t seq = 0;   // the tag of this buffer's last call (words of older calls carry older tags)
+  uint32_t seq = 0;   // this buffer's call counter (next_tag: words of older calls carry older tags)
 };
+
+// A call's tag in its buffer's words (high half): the buffer's call counter
+// with the top bit set.  The calls also leave plain 32-bit data in a pooled
+// buffer -- the GPU rerank's candidate ids and the stage-1 ids (int32 >= -1,
+// two per word), the raw prescores (floats) -- and a later call with another
+// layout may poll words where such data lies: a small counter as the tag
+// could equal a stale doc id in a word's high half and pass the check with
+// the other id as its value (round-6 soak, tools/stress_onetrip.py: 3-5 in
+// 120k calls).  No id, position or MaxSim score has the top bit set with the
+// rest below 2^31 - 1 (-0.0 is counter 0, never used; -inf and -1 sit at
+// counters no process reaches), so a stale word never passes for a call's.
+uint32_t next_tag(MappedBuf& b) {
+  b.seq = (b.seq + 1) & 0x7fffffffu;
+  if (b.seq == 0) b.seq = 1;
+  return 0x80000000u | b.seq;
+}
 struct MappedPool {
   std::mutex mu;
   std::vector<MappedBuf> free_buf[kMaxDev];
@@ -578,8 +594,7 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
   const bool mapped =
       ds.dev >= 0 && ds.dev < kMaxDev && take_mapped(ds.dev, mapped_words(B, k, C, C, kb) * 8, &pd.mb);
   if (mapped) {
-    pd.seq = ++pd.mb.seq;
-    if (pd.seq == 0) pd.seq = ++pd.mb.seq;
+    pd.seq = next_tag(pd.mb);
   }
   // small batches on bf16 / faithful shards (the host rerank's candidates):
   // the stage-2 ids and, B * k words further, their scores; the search's

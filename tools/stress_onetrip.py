@@ -64,6 +64,7 @@ def main():
     t0 = time.time()
     t_print = t0
     calls = mism = 0
+    prev = None
     per = {}
     while time.time() - t0 < a.seconds:
         name = list(shards)[rng.integers(len(shards))]
@@ -83,8 +84,23 @@ def main():
         per[name] = per.get(name, 0) + 1
         if not ok:
             mism += 1
-            if mism <= 3:
-                print(f"MISMATCH #{mism}: {name} B={B} rows {b0}.. mode {mode} host {host}", flush=True)
+            if mism <= 6:
+                print(f"MISMATCH #{mism}: {name} B={B} rows {b0}.. mode {mode} host {host}; previous call {prev}",
+                      flush=True)
+                for nm, g, w in zip(("scores", "ids", "pos"), got, want):
+                    g = np.asarray(g if host else g.cpu())
+                    w = w.cpu().numpy()
+                    bad = np.argwhere(g != w)
+                    if len(bad):
+                        r = int(bad[0][0])
+                        print(f"  {nm}: {len(bad)} entries differ, rows {sorted(set(int(x) for x in bad[:, 0]))}; "
+                              f"row {r} got {g[r].tolist()} want {w[r].tolist()}", flush=True)
+                again = [rets[name](Q, lexical, host=host) for _ in range(3)]
+                torch.cuda.synchronize()
+                reps = [all(np.array_equal(np.asarray(g if host else g.cpu()), w.cpu().numpy())
+                            for g, w in zip(x, want)) for x in again]
+                print(f"  the same call again x3 equals the composed stages: {reps}", flush=True)
+        prev = (name, B, mode, host)
         if time.time() - t_print > 20:
             t_print = time.time()
             print(f"{t_print - t0:.0f}s: {calls} calls, {mism} mismatches", flush=True)
