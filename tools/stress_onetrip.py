@@ -7,8 +7,13 @@ B <= 2 scan with its task hand-off) and ragged indexes, a BM25 callable / a
 host id array / no stage 1, device or host results.  Every call must equal
 the composed stages bit for bit; the first mismatch is printed and counted.
 A lab tool (GPU box), not a test: the tests pin each path once, this looks
-for rare host/device protocol races over thousands of calls.
-usage: stress_onetrip.py [--seconds S] [--docs N]"""
+for rare host/device protocol races over thousands of calls.  --threads T:
+T host threads, each on its own stream with its own retrievers (the mapped
+buffer pool is process-wide); --cancel P: a stage-1 callable raises with
+probability P (the call is cancelled: cbv2_retrieve_cancel) and later calls
+must still be right.
+usage: stress_onetrip.py [--seconds S] [--docs N] [--threads T] [--cancel P]"""
+import threading
 import argparse
 import os
 import sys
@@ -39,6 +44,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=180.0)
     ap.add_argument("--docs", type=int, default=125_000)
+    ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--cancel", type=float, default=0.0)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     bmax = max(BATCHES)
@@ -59,53 +66,83 @@ def main():
         "fp8 dense": (ColbertIndex.mxfp8(tok16, dl), torch.bfloat16),
     }
     del tok32
-    rets = {name: OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF) for name, (ix, _) in shards.items()}
-    rng = np.random.default_rng(5)
+    combos = {(b0, B): lex.search(qt[qo[b0]:qo[b0 + B]], qo[b0:b0 + B + 1] - qo[b0], KB)
+              for B in set(BATCHES) for b0 in range(bmax - B + 1)}   # stage 1 once, off the threads
     t0 = time.time()
-    t_print = t0
-    calls = mism = 0
-    prev = None
-    per = {}
-    while time.time() - t0 < a.seconds:
-        name = list(shards)[rng.integers(len(shards))]
-        ix, qdt = shards[name]
-        B = int(BATCHES[rng.integers(len(BATCHES))])
-        b0 = int(rng.integers(0, bmax - B + 1))
-        Q = Qf[b0:b0 + B].to(dev, qdt).contiguous()
-        bm_i, bm_s = lex.search(qt[qo[b0]:qo[b0 + B]], qo[b0:b0 + B + 1] - qo[b0], KB)
-        mode = int(rng.integers(3))
-        lexical, lex_ids = ((lambda: (bm_i, bm_s)), bm_i) if mode == 0 else ((bm_i, bm_i) if mode == 1 else (None, None))
-        host = bool(rng.integers(2))
-        got = rets[name](Q, lexical, host=host)
-        want = composed(ix, Q, lex_ids)
-        torch.cuda.synchronize()
-        ok = all(np.array_equal(np.asarray(g if host else g.cpu()), w.cpu().numpy()) for g, w in zip(got, want))
-        calls += 1
-        per[name] = per.get(name, 0) + 1
-        if not ok:
-            mism += 1
-            if mism <= 6:
-                print(f"MISMATCH #{mism}: {name} B={B} rows {b0}.. mode {mode} host {host}; previous call {prev}",
-                      flush=True)
-                for nm, g, w in zip(("scores", "ids", "pos"), got, want):
-                    g = np.asarray(g if host else g.cpu())
-                    w = w.cpu().numpy()
-                    bad = np.argwhere(g != w)
-                    if len(bad):
-                        r = int(bad[0][0])
-                        print(f"  {nm}: {len(bad)} entries differ, rows {sorted(set(int(x) for x in bad[:, 0]))}; "
-                              f"row {r} got {g[r].tolist()} want {w[r].tolist()}", flush=True)
-                again = [rets[name](Q, lexical, host=host) for _ in range(3)]
-                torch.cuda.synchronize()
-                reps = [all(np.array_equal(np.asarray(g if host else g.cpu()), w.cpu().numpy())
-                            for g, w in zip(x, want)) for x in again]
-                print(f"  the same call again x3 equals the composed stages: {reps}", flush=True)
-        prev = (name, B, mode, host)
-        if time.time() - t_print > 20:
-            t_print = time.time()
-            print(f"{t_print - t0:.0f}s: {calls} calls, {mism} mismatches", flush=True)
-    print({"calls": calls, "mismatches": mism, "per_shard": per, "seconds": round(time.time() - t0, 1),
-           "docs": a.docs}, flush=True)
+    stats = {"calls": 0, "mismatches": 0, "cancelled": 0, "per": {}}
+    lock = threading.Lock()
+    # the composed reference reuses the index object's own workspace: one
+    # thread at a time per shard (the one-trip calls run unserialized)
+    ref_lock = {name: threading.Lock() for name in shards}
+
+    class Cancelled(RuntimeError):
+        pass
+
+    def worker(wid):
+        rets = {name: OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF) for name, (ix, _) in shards.items()}
+        rng = np.random.default_rng(5 + wid)
+        stream = torch.cuda.Stream() if a.threads > 1 else torch.cuda.current_stream()
+        prev = None
+        t_print = t0
+        with torch.cuda.stream(stream):
+            while time.time() - t0 < a.seconds:
+                name = list(shards)[rng.integers(len(shards))]
+                ix, qdt = shards[name]
+                B = int(BATCHES[rng.integers(len(BATCHES))])
+                b0 = int(rng.integers(0, bmax - B + 1))
+                Q = Qf[b0:b0 + B].to(dev, qdt).contiguous()
+                bm_i, bm_s = combos[b0, B]
+                mode = int(rng.integers(3))
+                if a.cancel > 0 and rng.random() < a.cancel:   # a stage 1 that fails mid-call
+                    def boom():
+                        raise Cancelled()
+                    try:
+                        rets[name](Q, boom, host=bool(rng.integers(2)))
+                    except Cancelled:
+                        pass
+                    with lock:
+                        stats["cancelled"] += 1
+                    prev = (name, B, "cancelled")
+                    continue
+                lexical, lex_ids = (((lambda: (bm_i, bm_s)), bm_i) if mode == 0
+                                    else ((bm_i, bm_i) if mode == 1 else (None, None)))
+                host = bool(rng.integers(2))
+                got = rets[name](Q, lexical, host=host)
+                with ref_lock[name]:
+                    want = composed(ix, Q, lex_ids)
+                    stream.synchronize()
+                ok = all(np.array_equal(np.asarray(g if host else g.cpu()), w.cpu().numpy()) for g, w in zip(got, want))
+                with lock:
+                    stats["calls"] += 1
+                    stats["per"][name] = stats["per"].get(name, 0) + 1
+                    if not ok:
+                        stats["mismatches"] += 1
+                    mism = stats["mismatches"]
+                if not ok and mism <= 6:
+                    print(f"MISMATCH #{mism} (thread {wid}): {name} B={B} rows {b0}.. mode {mode} host {host}; "
+                          f"previous call {prev}", flush=True)
+                    for nm, g, w in zip(("scores", "ids", "pos"), got, want):
+                        g = np.asarray(g if host else g.cpu())
+                        w = w.cpu().numpy()
+                        bad = np.argwhere(g != w)
+                        if len(bad):
+                            r = int(bad[0][0])
+                            print(f"  {nm}: {len(bad)} entries differ, rows {sorted(set(int(x) for x in bad[:, 0]))}; "
+                                  f"row {r} got {g[r].tolist()} want {w[r].tolist()}", flush=True)
+                prev = (name, B, mode, host)
+                if wid == 0 and time.time() - t_print > 20:
+                    t_print = time.time()
+                    print(f"{t_print - t0:.0f}s: {stats['calls']} calls, {stats['mismatches']} mismatches, "
+                          f"{stats['cancelled']} cancelled", flush=True)
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(a.threads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    calls, mism, per = stats["calls"], stats["mismatches"], stats["per"]
+    print({"calls": calls, "mismatches": mism, "cancelled": stats["cancelled"], "per_shard": per,
+           "seconds": round(time.time() - t0, 1), "docs": a.docs, "threads": a.threads}, flush=True)
     sys.exit(1 if mism else 0)
 
 
