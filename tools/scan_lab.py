@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B the scan-kernel variants in ONE process, interleaved rounds (guide §5.4
 rule 24), on the bench's synthetic corpus; check every variant's scores
-against variant 0 and the oracle.  usage: scan_lab.py [--docs N] [--batch B] [--rounds R] [--variants 0,1,2]
+against variant 0 and a float64 torch MaxSim of a slice.  usage: scan_lab.py [--docs N] [--batch B] [--rounds R] [--variants 0,1,2]
 Variants: an int = a production/lab scan variant (lab_scan); "f<frac>t<docs>" =
 the production B > 16 scan with that dynamic-tail split (lab_scan16x4), e.g.
 f0t128 (static), f0.1t128; a suffix k<kind> selects a lab kernel build of lab_scan16x4; a prefix "n:" runs the variant
@@ -20,7 +20,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from hybrid_rag_colbertv2_amd import synth  # noqa: E402
 from hybrid_rag_colbertv2_amd.index import ColbertIndex  # noqa: E402
-from oracle import oracle as orc  # noqa: E402
+
+
+def _dequant_mxfp8(q: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    """e4m3 bytes [..., 128] + E8M0 scales [..., 2] -> f32 (one scale per 64 dims)."""
+    v = q.contiguous().view(torch.float8_e4m3fn).float()
+    return v * torch.exp2(sc.float() - 127.0).repeat_interleave(64, dim=-1)
+
+
+def _maxsim_ref(Q: torch.Tensor, D: torch.Tensor, dl: torch.Tensor) -> torch.Tensor:
+    """Plain torch float64 MaxSim of queries [q, 32, 128] over docs [n, L, 128]
+    (rows >= doclens never score; empty docs -inf) -- the lab's check (the
+    oracle is test infrastructure: tests, smoke and the bench's CPU baseline)."""
+    sims = torch.einsum("qid,ntd->qnit", Q.double(), D.double())
+    mask = torch.arange(D.shape[1], device=D.device)[None, :] >= dl[:, None].long()
+    sims = sims.masked_fill(mask[None, :, None, :], float("-inf"))
+    return sims.max(dim=-1).values.sum(dim=-1).float()
 
 LAB = os.path.join(ROOT, "tools", "_build", "libscanlab.so")
 # "n:" variants run in a second build with the -D flags of ALT_DEFS (env
@@ -89,7 +104,7 @@ def main():
         qq, qs = quantize_mxfp8(Q)
         qbuf = torch.cat([qq.reshape(-1), qs.reshape(-1)])
         qptr = qbuf.data_ptr()
-        Qd = torch.from_numpy(orc.mxfp8_dequant(qq.cpu().numpy(), qs.cpu().numpy()))
+        Qd = _dequant_mxfp8(qq, qs)
     else:
         ix = ColbertIndex(tokens, doclens)
         Q = Qf.to(dev, torch.bfloat16)
@@ -130,15 +145,15 @@ def main():
             e1.record(st)
             e1.synchronize()
             times[v].append(e0.elapsed_time(e1) / a.chain)
-    # oracle on a slice (first 64 and last 200 docs, 8 queries)
+    # a float64 torch reference on a slice (first 64 and last 200 docs, 8 queries)
     sl = torch.cat([torch.arange(64), torch.arange(a.docs - 200, a.docs)]).to(dev)
     nq = min(8, a.batch)
-    qref = Qd[:nq].numpy() if fp8 else Q[:nq].float().cpu().numpy()
-    if fp8:   # the oracle scores the dequantized values of the slice
-        dsl = orc.mxfp8_dequant(ix.tokens[sl].cpu().numpy(), ix.scales[sl].cpu().numpy())
+    qref = Qd[:nq] if fp8 else Q[:nq].float()
+    if fp8:   # the dequantized values of the slice
+        dsl = _dequant_mxfp8(ix.tokens[sl], ix.scales[sl])
     else:
-        dsl = tokens[sl].float().cpu().numpy()
-    ref = orc.maxsim(qref, dsl, doclens[sl].cpu().numpy())
+        dsl = tokens[sl].float()
+    ref = _maxsim_ref(qref, dsl, doclens[sl]).cpu().numpy()
     flop = a.batch * a.docs * 2 * 32 * 128 * 128
     base = outs[variants[0]]
     for v in variants:
@@ -151,7 +166,7 @@ def main():
         gbs = a.docs * 32768 / med / 1e6
         print(f"B={a.batch} variant {v}: median {med:.3f} ms  min {min(times[v]):.3f}  {gbs:.0f} GB/s doc bytes  "
               f"{flop / med / 1e9:.1f} TFLOP/s "
-              f"({flop / med / 1e9 / (5000 if fp8 else 2500) * 100:.1f}% of {a.dtype} peak)  oracle_err {err:.2e} inf_ok {inf_ok} "
+              f"({flop / med / 1e9 / (5000 if fp8 else 2500) * 100:.1f}% of {a.dtype} peak)  ref_err {err:.2e} inf_ok {inf_ok} "
               f"max|d vs v{variants[0]}| {dv:.2e}", flush=True)
     for v in [x for x in a.stamps.split(",") if x] if not fp8 else []:
         outs.setdefault(v, torch.empty((a.batch, a.docs), device=dev))
