@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--docs", type=int, default=125_000)
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--cancel", type=float, default=0.0)
+    ap.add_argument("--busy-stage1", action="store_true",
+                    help="also a stage-1 callable that first runs a search on another shard (same stream)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     bmax = max(BATCHES)
@@ -92,7 +94,7 @@ def main():
                 b0 = int(rng.integers(0, bmax - B + 1))
                 Q = Qf[b0:b0 + B].to(dev, qdt).contiguous()
                 bm_i, bm_s = combos[b0, B]
-                mode = int(rng.integers(3))
+                mode = int(rng.integers(4 if a.busy_stage1 else 3))
                 if a.cancel > 0 and rng.random() < a.cancel:   # a stage 1 that fails mid-call
                     def boom():
                         raise Cancelled()
@@ -104,8 +106,16 @@ def main():
                         stats["cancelled"] += 1
                     prev = (name, B, "cancelled")
                     continue
-                lexical, lex_ids = (((lambda: (bm_i, bm_s)), bm_i) if mode == 0
-                                    else ((bm_i, bm_i) if mode == 1 else (None, None)))
+                if mode == 3:   # a stage 1 that runs GPU work of its own on the call's stream first
+                    other_ix, other_qdt = shards[list(shards)[rng.integers(len(shards))]]
+
+                    def busy(other_ix=other_ix, other_qdt=other_qdt, bm_i=bm_i, bm_s=bm_s):
+                        other_ix.search(Qf[:2].to(dev, other_qdt).contiguous(), 50)
+                        return bm_i, bm_s
+                    lexical, lex_ids = busy, bm_i
+                else:
+                    lexical, lex_ids = (((lambda: (bm_i, bm_s)), bm_i) if mode == 0
+                                        else ((bm_i, bm_i) if mode == 1 else (None, None)))
                 host = bool(rng.integers(2))
                 got = rets[name](Q, lexical, host=host)
                 with ref_lock[name]:
