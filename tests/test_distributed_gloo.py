@@ -188,6 +188,69 @@ def test_hybrid_exchange_equals_unsharded(world):
             assert misses == 0 and calls == {"all_gather": 1}, (kb, misses, calls)
 
 
+# randomized stage-1 width / k / C / final_k cases of the pooled stage 3 at
+# world 3 (ragged shards): (k, kb, C, final_k); kb 0 = no stage 1
+_POOL_CASES = [(40, 50, 20, 7), (5, 13, 7, 7), (100, 1, 20, 1), (17, 50, 64, 20), (40, 0, 20, 7),
+               (100, 50, 1, 1), (5, 50, 64, 20), (17, 13, 20, 20), (120, 7, 50, 10)]
+
+
+def _pool_cases_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hybrid_rag_colbertv2_amd import bm25
+        from hybrid_rag_colbertv2_amd.distributed import ShardedSearcher, shard_range
+        from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+        Q, docs, doclens, _ = _data()
+        terms, off, qt, qo, V = _bm25_data()
+        a, b = shard_range(len(docs), rank, world)
+        lex = bm25.sharded(terms[off[a]:off[b]], off[a:b + 1] - off[a], V, id_base=a)
+        ss = ShardedSearcher(OracleShard(Q, docs[a:b], doclens[a:b], a), ops=OracleOps())
+        out = []
+        for k, kb, C, fk in _POOL_CASES:
+            lexical = (lambda kb=kb: lex.search(qt, qo, kb)) if kb else None
+            s3, i3, li3, pool = ss.search_hybrid(Q, k, lexical, return_pool=True)
+            bm = li3.numpy() if li3 is not None else np.zeros((Q.shape[0], 0), np.int32)
+            cand = rrf_fuse(bm, i3.numpy(), rrf_k=60, C=C)
+            rs, ri, rp = ss.rerank(Q, torch.from_numpy(cand), fk, pool=pool)
+            out.append((cand, rs.numpy(), ri.numpy(), rp.numpy(), int(ss.last_pool_misses)))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pooled_stage3_cases_world3():
+    """The collective-free stage 3 over many (k, kb, C, final_k) shapes at
+    world 3: k above a shard's size (padding in the pool), kb = 1 and no
+    stage 1, C = 1 and C above the fused list, final_k = C -- every rank
+    equals the unsharded rerank of the same fused candidates, no misses."""
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pool_cases_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Q, docs, doclens, _ = _data()
+    full = orc.maxsim(Q.numpy(), docs, doclens)
+    terms, off, qt, qo, V = _bm25_data()
+    for _, out in res:
+        for (k, kb, C, fk), (cand, rs, ri, rp, misses) in zip(_POOL_CASES, out):
+            _, ei = orc.topk(full, k)
+            bk = orc.bm25_topk(terms, off, qt, qo, V, kb)[0] if kb else np.zeros((Q.shape[0], 0), np.int32)
+            assert np.array_equal(cand, rrf_fuse(bk, ei, rrf_k=60, C=C)), (k, kb, C)
+            ws, wi, wp = orc.rerank(Q.numpy(), docs, doclens, cand, fk)
+            assert np.array_equal(ri, wi) and np.array_equal(rp, wp), (k, kb, C, fk)
+            np.testing.assert_allclose(rs, ws, atol=1e-5)
+            assert misses == 0, (k, kb, C, fk, misses)
+
+
 _QUERIES = ["what is late interaction", "colbert maxsim on mi355x", "bm25 and rrf fusion",
             "hbm3e bandwidth", "rerank the top fifty chunks"]
 
