@@ -30,14 +30,15 @@ from hybrid_rag_colbertv2_amd.hybrid import OneTripRetriever, rrf_fuse  # noqa: 
 from hybrid_rag_colbertv2_amd.index import ColbertIndex  # noqa: E402
 
 K, KB, C, KF = 100, 100, 50, 10
+SHAPES = ((100, 50, 10), (10, 1, 1), (200, 100, 50), (100, 100, 100), (40, 20, 7))   # --shapes: (k, C, final_k)
 BATCHES = (1, 1, 1, 2, 2, 3, 5, 8, 17)
 
 
-def composed(index, Q, lex_ids):
-    _, ids = index.search(Q, K)
+def composed(index, Q, lex_ids, k=K, c=C, kf=KF):
+    _, ids = index.search(Q, k)
     bm = np.zeros((ids.shape[0], 0), np.int32) if lex_ids is None else lex_ids
-    cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=C)
-    return index.rerank(Q, torch.from_numpy(cand).to(index.device), KF)
+    cand = rrf_fuse(bm, ids.cpu().numpy(), rrf_k=60, C=c)
+    return index.rerank(Q, torch.from_numpy(cand).to(index.device), kf)
 
 
 def main():
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--docs", type=int, default=125_000)
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--cancel", type=float, default=0.0)
+    ap.add_argument("--shapes", action="store_true", help="random (k, C, final_k) per call (several layouts)")
     ap.add_argument("--busy-stage1", action="store_true",
                     help="also a stage-1 callable that first runs a search on another shard (same stream)")
     a = ap.parse_args()
@@ -81,7 +83,13 @@ def main():
         pass
 
     def worker(wid):
-        rets = {name: OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF) for name, (ix, _) in shards.items()}
+        rets = {}
+
+        def ret(name, shape):   # one retriever per (shard, k / C / final_k): their buffers' layouts differ
+            if (name, shape) not in rets:
+                rets[name, shape] = OneTripRetriever(shards[name][0], colbert_k=shape[0], fused=shape[1],
+                                                     final_k=shape[2])
+            return rets[name, shape]
         rng = np.random.default_rng(5 + wid)
         stream = torch.cuda.Stream() if a.threads > 1 else torch.cuda.current_stream()
         prev = None
@@ -99,7 +107,7 @@ def main():
                     def boom():
                         raise Cancelled()
                     try:
-                        rets[name](Q, boom, host=bool(rng.integers(2)))
+                        ret(name, (K, C, KF))(Q, boom, host=bool(rng.integers(2)))
                     except Cancelled:
                         pass
                     with lock:
@@ -117,9 +125,10 @@ def main():
                     lexical, lex_ids = (((lambda: (bm_i, bm_s)), bm_i) if mode == 0
                                         else ((bm_i, bm_i) if mode == 1 else (None, None)))
                 host = bool(rng.integers(2))
-                got = rets[name](Q, lexical, host=host)
+                shape = SHAPES[rng.integers(len(SHAPES))] if a.shapes else (K, C, KF)
+                got = ret(name, shape)(Q, lexical, host=host)
                 with ref_lock[name]:
-                    want = composed(ix, Q, lex_ids)
+                    want = composed(ix, Q, lex_ids, *shape)
                     stream.synchronize()
                 ok = all(np.array_equal(np.asarray(g if host else g.cpu()), w.cpu().numpy()) for g, w in zip(got, want))
                 with lock:
