@@ -51,11 +51,16 @@ def main():
     qmax = max(BATCHES)
     idx = {}
     for name, n, ragged, kind in (("bf16 dense 50k", 50_000, False, "bf16"), ("bf16 ragged 60k", 60_001, True, "bf16"),
-                                  ("fp8 dense 50k", 50_000, False, "fp8"), ("fp32 ragged 40k", 40_003, True, "fp32")):
+                                  ("fp8 dense 50k", 50_000, False, "fp8"), ("fp32 ragged 40k", 40_003, True, "fp32"),
+                                  ("bf16 ties 50k", 50_000, "ties", "bf16"), ("fp32 ties 40k", 40_003, "ties", "fp32")):
         Qf = synth.make_queries(qmax, seed=41)
         planted = synth.planted_ids(qmax, n, 10, seed=42)
         tok, dl = synth.make_shard(0, n, Qf, planted, dev, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
-        if ragged:
+        if ragged == "ties":   # every doc a copy of one of 200: exact ties between candidates
+            pick = torch.randint(0, 200, (n,), device=dev)
+            tok = tok[:200][pick].contiguous()
+            dl = dl[:200][pick].contiguous()
+        elif ragged:
             dl[::5] = torch.randint(0, 129, (len(dl[::5]),), device=dev, dtype=torch.int32)
             dl[::89] = 0
         ix = (ColbertIndex.faithful_f32(tok, dl, id_base=BASE) if kind == "fp32" else

@@ -47,11 +47,18 @@ def main():
                                   ("bf16 tiny 3k", 3_001, True, "bf16"),
                                   ("fp8 dense 70k", 70_000, False, "fp8"),
                                   ("fp32 dense 70k", 70_000, False, "fp32"),
-                                  ("fp32 ragged 90k", 90_001, True, "fp32")):
+                                  ("fp32 ragged 90k", 90_001, True, "fp32"),
+                                  ("bf16 ties 70k", 70_000, "ties", "bf16"),
+                                  ("fp32 ties 50k", 50_003, "ties", "fp32"),
+                                  ("fp8 ties 70k", 70_000, "ties", "fp8")):
         Qf = synth.make_queries(qmax, seed=31)
         planted = synth.planted_ids(qmax, n, 10, seed=32)
         tok, dl = synth.make_shard(0, n, Qf, planted, dev, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
-        if ragged:
+        if ragged == "ties":   # every doc a copy of one of 300: exact score ties across the whole index
+            pick = torch.randint(0, 300, (n,), device=dev)
+            tok = tok[:300][pick].contiguous()
+            dl = dl[:300][pick].contiguous()
+        elif ragged:
             dl[::5] = torch.randint(0, 129, (len(dl[::5]),), device=dev, dtype=torch.int32)
             dl[::97] = 0                                     # empty docs (-inf)
         ix = (ColbertIndex.faithful_f32(tok, dl, id_base=7) if kind == "fp32" else
