@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--cancel", type=float, default=0.0)
     ap.add_argument("--shapes", action="store_true", help="random (k, C, final_k) per call (several layouts)")
+    ap.add_argument("--ties", action="store_true", help="a corpus of copies of 300 docs (exact score ties)")
     ap.add_argument("--busy-stage1", action="store_true",
                     help="also a stage-1 callable that first runs a search on another shard (same stream)")
     a = ap.parse_args()
@@ -56,6 +57,10 @@ def main():
     Qf = synth.make_queries(bmax, seed=11)
     planted = synth.planted_ids(bmax, a.docs, 10, seed=12)
     tok32, dl = synth.make_shard(0, a.docs, Qf, planted, dev, dtype=torch.float32)
+    if a.ties:   # every doc a copy of one of 300: exact ties in stage 2, the fusion and stage 3
+        pick = torch.randint(0, 300, (a.docs,), device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+        tok32 = tok32[:300][pick].contiguous()
+        dl = dl[:300][pick].contiguous()
     tok16 = tok32.to(torch.bfloat16)
     dl_ragged = dl.clone()
     dl_ragged[::3] = torch.randint(0, 129, (len(dl_ragged[::3]),), device=dev, dtype=torch.int32)
