@@ -52,15 +52,26 @@ def main():
     idx = {}
     for name, n, ragged, kind in (("bf16 dense 50k", 50_000, False, "bf16"), ("bf16 ragged 60k", 60_001, True, "bf16"),
                                   ("fp8 dense 50k", 50_000, False, "fp8"), ("fp32 ragged 40k", 40_003, True, "fp32"),
-                                  ("bf16 ties 50k", 50_000, "ties", "bf16"), ("fp32 ties 40k", 40_003, "ties", "fp32")):
+                                  ("bf16 ties 50k", 50_000, "ties", "bf16"), ("fp32 ties 40k", 40_003, "ties", "fp32"),
+                                  ("bf16 long512 20k", 20_003, "long512", "bf16"),
+                                  ("fp32 long256 15k", 15_001, "long256", "fp32")):
         Qf = synth.make_queries(qmax, seed=41)
         planted = synth.planted_ids(qmax, n, 10, seed=42)
-        tok, dl = synth.make_shard(0, n, Qf, planted, dev, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+        if str(ragged).startswith("long"):   # long documents: ld token slots, random lengths up to ld
+            ld = int(str(ragged)[4:])
+            g = torch.Generator(device=dev).manual_seed(n)
+            tok = torch.randn(n, ld, 128, device=dev, generator=g)
+            tok = tok / tok.norm(dim=-1, keepdim=True)
+            tok = tok if kind == "fp32" else tok.to(torch.bfloat16)
+            dl = torch.randint(0, ld + 1, (n,), device=dev, generator=g, dtype=torch.int32)
+        else:
+            tok, dl = synth.make_shard(0, n, Qf, planted, dev,
+                                       dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
         if ragged == "ties":   # every doc a copy of one of 200: exact ties between candidates
             pick = torch.randint(0, 200, (n,), device=dev)
             tok = tok[:200][pick].contiguous()
             dl = dl[:200][pick].contiguous()
-        elif ragged:
+        elif ragged is True:
             dl[::5] = torch.randint(0, 129, (len(dl[::5]),), device=dev, dtype=torch.int32)
             dl[::89] = 0
         ix = (ColbertIndex.faithful_f32(tok, dl, id_base=BASE) if kind == "fp32" else

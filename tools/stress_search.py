@@ -50,15 +50,27 @@ def main():
                                   ("fp32 ragged 90k", 90_001, True, "fp32"),
                                   ("bf16 ties 70k", 70_000, "ties", "bf16"),
                                   ("fp32 ties 50k", 50_003, "ties", "fp32"),
-                                  ("fp8 ties 70k", 70_000, "ties", "fp8")):
+                                  ("fp8 ties 70k", 70_000, "ties", "fp8"),
+                                  ("bf16 long512 20k", 20_003, "long512", "bf16"),
+                                  ("fp8 long256 20k", 20_000, "long256", "fp8"),
+                                  ("fp32 long256 15k", 15_001, "long256", "fp32")):
         Qf = synth.make_queries(qmax, seed=31)
         planted = synth.planted_ids(qmax, n, 10, seed=32)
-        tok, dl = synth.make_shard(0, n, Qf, planted, dev, dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+        if str(ragged).startswith("long"):   # long documents: ld token slots, random lengths up to ld
+            ld = int(str(ragged)[4:])
+            g = torch.Generator(device=dev).manual_seed(n)
+            tok = torch.randn(n, ld, 128, device=dev, generator=g)
+            tok = tok / tok.norm(dim=-1, keepdim=True)
+            tok = tok if kind == "fp32" else tok.to(torch.bfloat16)
+            dl = torch.randint(0, ld + 1, (n,), device=dev, generator=g, dtype=torch.int32)
+        else:
+            tok, dl = synth.make_shard(0, n, Qf, planted, dev,
+                                       dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
         if ragged == "ties":   # every doc a copy of one of 300: exact score ties across the whole index
             pick = torch.randint(0, 300, (n,), device=dev)
             tok = tok[:300][pick].contiguous()
             dl = dl[:300][pick].contiguous()
-        elif ragged:
+        elif ragged is True:
             dl[::5] = torch.randint(0, 129, (len(dl[::5]),), device=dev, dtype=torch.int32)
             dl[::97] = 0                                     # empty docs (-inf)
         ix = (ColbertIndex.faithful_f32(tok, dl, id_base=7) if kind == "fp32" else
