@@ -35,14 +35,17 @@ struct cbv2_bm25 {
 
 extern "C" int cbv2_set_error(int code, const char* msg);  // defined in colbert_mi355x.hip
 
+// (doc_terms may be null when the docs hold no token at all: a shard of empty
+// chunks builds an index that matches nothing)
 static int check_corpus(const int32_t* doc_terms, const int64_t* doc_offsets, int64_t n_docs, int32_t vocab) {
-  if (n_docs < 0 || vocab < 1 || (n_docs > 0 && (!doc_terms || !doc_offsets)))
+  if (n_docs < 0 || vocab < 1 || (n_docs > 0 && !doc_offsets))
     return cbv2_set_error(CBV2_EINVAL, "bad bm25 corpus arguments");
   if (n_docs > 0x7fffffffLL) return cbv2_set_error(CBV2_EINVAL, "too many docs for int32 ids");
   for (int64_t d = 0; d < n_docs; ++d)
     if (doc_offsets[d + 1] < doc_offsets[d]) return cbv2_set_error(CBV2_EINVAL, "doc_offsets not ascending");
   const int64_t total = n_docs ? doc_offsets[n_docs] - doc_offsets[0] : 0;
-  const int32_t* t = n_docs ? doc_terms + doc_offsets[0] : nullptr;
+  if (total > 0 && !doc_terms) return cbv2_set_error(CBV2_EINVAL, "bad bm25 corpus arguments (null terms)");
+  const int32_t* t = total > 0 ? doc_terms + doc_offsets[0] : nullptr;
   for (int64_t i = 0; i < total; ++i)
     if (t[i] < 0 || t[i] >= vocab) return cbv2_set_error(CBV2_EINVAL, "term id out of range");
   return CBV2_OK;
@@ -50,6 +53,7 @@ static int check_corpus(const int32_t* doc_terms, const int64_t* doc_offsets, in
 
 // df of the distinct terms of each doc (sorting a scratch copy per doc)
 static void doc_freq(const int32_t* doc_terms, const int64_t* doc_offsets, int64_t n_docs, int64_t* df) {
+  if (doc_terms == nullptr) return;   // no tokens (check_corpus)
   std::vector<int32_t> scratch;
   for (int64_t d = 0; d < n_docs; ++d) {
     scratch.assign(doc_terms + doc_offsets[d], doc_terms + doc_offsets[d + 1]);
@@ -98,7 +102,7 @@ extern "C" int cbv2_bm25_build_shard(const int32_t* doc_terms, const int64_t* do
   // postings in doc order
   std::vector<int64_t> fill(ix->ptr.begin(), ix->ptr.end() - 1);
   std::vector<int32_t> scratch;
-  for (int64_t d = 0; d < n_docs; ++d) {
+  for (int64_t d = 0; d < n_docs && doc_terms != nullptr; ++d) {   // (no tokens: no postings)
     scratch.assign(doc_terms + doc_offsets[d], doc_terms + doc_offsets[d + 1]);
     std::sort(scratch.begin(), scratch.end());
     const double dl = (double)scratch.size();

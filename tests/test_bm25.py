@@ -170,3 +170,31 @@ def test_native_bm25_repeated_query_terms():
     wr = dict(zip(ir[0].tolist(), sr[0].tolist()))
     for d in holds3:
         assert wr[d] == np.float32(np.float32(w3[d] + w3[d]) + w3[d])
+
+
+def test_bm25_shard_of_empty_docs():
+    """A shard whose docs hold no token at all (empty chunks) builds -- no
+    terms pointer to pass -- and the merge of every shard's list still equals
+    the unsharded top-k (round-6 soak: the build used to refuse it, so one
+    rank of a sharded index would fail)."""
+    from hybrid_rag_colbertv2_amd.bm25 import NativeBM25
+    V = 7
+    empty = NativeBM25(np.zeros(0, np.int32), np.zeros(5, np.int64), V)               # 4 empty docs
+    ids, sc = empty.search(np.array([1, 2], np.int32), np.array([0, 2], np.int64), 6)
+    assert ids.tolist() == [[0, 1, 2, 3, -1, -1]] and sc.tolist() == [[0.0] * 6]
+    assert NativeBM25.doc_freq(np.zeros(0, np.int32), np.zeros(5, np.int64), V).tolist() == [0] * V
+    rng = np.random.default_rng(11)
+    N = 60
+    lens = rng.integers(1, 6, size=N)
+    lens[20:35] = 0                                                                    # shard 1: all empty
+    off = np.zeros(N + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    terms = rng.integers(0, V, size=int(off[-1])).astype(np.int32)
+    qt, qo = np.array([1, 3, 3, 5], np.int32), np.array([0, 2, 4], np.int64)
+    cuts = [0, 20, 35, N]
+    stats = (N, int(off[-1]), NativeBM25.doc_freq(terms, off, V))
+    res = [NativeBM25(terms[off[a]:off[b]], off[a:b + 1] - off[a], V, id_base=a, stats=stats).search(qt, qo, 40)
+           for a, b in zip(cuts[:-1], cuts[1:])]
+    ms, mi = orc.merge_topk(np.stack([r[1] for r in res]), np.stack([r[0] for r in res]), 40)
+    oi, os_ = orc.bm25_topk(terms, off, qt, qo, V, 40)
+    _same(mi, ms, oi, os_)
