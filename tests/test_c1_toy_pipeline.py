@@ -78,3 +78,34 @@ def test_retrieve_matches_reference():
         for g, r in zip(got, ref):
             assert {k: v for k, v in g.items() if k != "score"} == {k: v for k, v in r.items() if k != "score"}
             assert abs(g["score"] - r["score"]) < 1e-6
+
+
+def test_native_rrf_random_lists_match_reference():
+    """cbv2_rrf_fuse (host C++) against the reference's RRF restated in
+    oracle.rrf (LRC:960-978: float64 1/(k + rank) sums, BM25 list first,
+    stable descending sort -> equal sums keep first-insertion order) + [:C],
+    over random overlapping lists: small id ranges (many shared ids and exact
+    ties), empty lists, trailing -1 padding (as the searches pad), several
+    rrf_k and C."""
+    from hybrid_rag_colbertv2_amd.hybrid import rrf_fuse
+    rng = np.random.default_rng(17)
+    for case in range(300):
+        m = int(rng.integers(1, 200))
+        B = int(rng.integers(1, 4))
+        kb, kc = int(rng.integers(0, 121)), int(rng.integers(0, 121))
+        C = int(rng.choice([1, 10, 50, 250]))
+        rk = int(rng.choice([60, 1, 7]))
+        bm = np.full((B, kb), -1, np.int32)
+        cb = np.full((B, kc), -1, np.int32)
+        for b in range(B):
+            nb, nc = min(kb, int(rng.integers(0, m + 1))), min(kc, int(rng.integers(0, m + 1)))
+            bm[b, :nb] = rng.permutation(m)[:nb]
+            cb[b, :nc] = rng.permutation(m)[:nc]
+        got, sc, cnt = rrf_fuse(bm, cb, rrf_k=rk, C=C, return_scores=True)
+        for b in range(B):
+            full = orc.rrf([int(x) for x in bm[b] if x >= 0], [int(x) for x in cb[b] if x >= 0], k=rk)
+            want = full[:C]
+            ids = [cid for cid, _ in want]
+            assert got[b, :len(ids)].tolist() == ids, (case, b)
+            assert (got[b, len(ids):] == -1).all() and int(cnt[b]) == len(full), (case, b)   # count: distinct ids (before [:C], the header)
+            assert sc[b, :len(ids)].tolist() == [s for _, s in want], (case, b)
