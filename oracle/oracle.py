@@ -98,7 +98,7 @@ def mxfp8_quantize(x: np.ndarray):
     r = np.round(a / quantum) * quantum                  # numpy rounds half to even
     pos = {float(E4M3[v]): v for v in range(0x7F)}
     code = np.vectorize(lambda z: pos[float(z)])(r).astype(np.uint8)
-    code = np.where(y < 0, code | 0x80, code).astype(np.uint8)   # sign kept, also for -0 (as the hardware)
+    code = np.where(np.signbit(y), code | 0x80, code).astype(np.uint8)   # sign kept, also for -0 (as the hardware)
     return code.reshape(x.shape), (e + 127).astype(np.uint8)
 
 

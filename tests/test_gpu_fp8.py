@@ -48,6 +48,40 @@ def test_quantizer_matches_oracle(dev):
         assert (rel[np.abs(t.float().numpy()) > 2.0 ** -6 * np.exp2(es.repeat(64, -1).astype(float) - 127)] <= 2 ** -4 + 1e-9).all()
 
 
+def test_quantizer_rounding_boundaries_match_oracle(dev):
+    """Byte-exact at the quantizer's boundaries: block maxima exactly at powers
+    of two and at the e4m3 top (the E8M0 scale choice), elements at exact
+    midpoints between neighbouring e4m3 codes under the block's scale (ties
+    to even), in the e4m3 subnormal range, signed zeros, fp32 subnormals and
+    values near the fp32 top -- f32 and bf16 inputs."""
+    rng = np.random.default_rng(23)
+    rows = []
+    e4 = torch.arange(0, 127, dtype=torch.uint8).view(torch.float8_e4m3fn).float().numpy()   # e4m3 grid, >= 0
+    mids = (e4[1:] + e4[:-1]) / 2                                        # exact midpoints
+    for r in range(600):
+        E = int(rng.integers(-20, 21))
+        top = float(rng.choice([1.0, 1.5, 1.75, 1.875, 448.0 / 256.0])) * 2.0 ** E
+        row = np.zeros(128, np.float32)
+        for half in (0, 64):
+            scale = 2.0 ** (E - 8)
+            pick = rng.integers(0, len(mids), 64)
+            v = np.where(rng.random(64) < 0.5, mids[pick], e4[pick]) * scale
+            v *= np.where(rng.random(64) < 0.5, -1.0, 1.0)
+            v[0] = top * (1 if r % 2 else -1)
+            v[rng.random(64) < 0.05] = -0.0
+            row[half:half + 64] = v
+        rows.append(row)
+    x = np.stack(rows).astype(np.float32)
+    x[0, :5] = [1e-40, -1e-40, 3e38, -3e38, 1e-45]                       # fp32 subnormals, near the top
+    x[1, 64:] = 2.0 ** -140
+    for t in (torch.from_numpy(x), torch.from_numpy(x).bfloat16()):
+        q, sc = quantize_mxfp8(t.to(dev))
+        eq, es = orc.mxfp8_quantize(t.float().numpy())
+        assert np.array_equal(sc.cpu().numpy(), es), np.argwhere(sc.cpu().numpy() != es)[:5]
+        qb = q.cpu().numpy()
+        assert np.array_equal(qb, eq), (t.dtype, np.argwhere(qb != eq)[:5])
+
+
 @pytest.mark.parametrize("N,B,lq,ragged", [(300, 3, 32, True), (2000, 70, 32, True), (513, 1, 20, False),
                                            (1500, 9, 32, True)])
 def test_fp8_score_matches_oracle(dev, N, B, lq, ragged):
