@@ -54,7 +54,8 @@ def main():
                                   ("fp8 dense 50k", 50_000, False, "fp8"), ("fp32 ragged 40k", 40_003, True, "fp32"),
                                   ("bf16 ties 50k", 50_000, "ties", "bf16"), ("fp32 ties 40k", 40_003, "ties", "fp32"),
                                   ("bf16 long512 20k", 20_003, "long512", "bf16"),
-                                  ("fp32 long256 15k", 15_001, "long256", "fp32")):
+                                  ("fp32 long256 15k", 15_001, "long256", "fp32"),
+                                  ("fp32 wild 30k", 30_011, "wild", "fp32"), ("bf16 wild 30k", 30_011, "wild", "bf16")):
         Qf = synth.make_queries(qmax, seed=41)
         planted = synth.planted_ids(qmax, n, 10, seed=42)
         if str(ragged).startswith("long"):   # long documents: ld token slots, random lengths up to ld
@@ -67,6 +68,11 @@ def main():
         else:
             tok, dl = synth.make_shard(0, n, Qf, planted, dev,
                                        dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+        if ragged == "wild":   # token norms over ~6 orders of magnitude
+            g = torch.Generator(device=dev).manual_seed(n + 1)
+            scale = torch.exp(torch.randn(n, 128, 1, device=dev, generator=g) * 2.5)
+            tok = (tok.float() * scale).to(tok.dtype)
+            dl = torch.randint(0, 129, (n,), device=dev, generator=g, dtype=torch.int32)
         if ragged == "ties":   # every doc a copy of one of 200: exact ties between candidates
             pick = torch.randint(0, 200, (n,), device=dev)
             tok = tok[:200][pick].contiguous()
@@ -76,7 +82,10 @@ def main():
             dl[::89] = 0
         ix = (ColbertIndex.faithful_f32(tok, dl, id_base=BASE) if kind == "fp32" else
               ColbertIndex.mxfp8(tok, dl, id_base=BASE) if kind == "fp8" else ColbertIndex(tok, dl, id_base=BASE))
-        Q = Qf.to(dev, torch.float32 if kind == "fp32" else torch.bfloat16)
+        Qs = Qf.float()
+        if ragged == "wild":
+            Qs = Qs * torch.exp(torch.randn(Qs.shape[0], Qs.shape[1], 1, generator=torch.Generator().manual_seed(5)) * 2)
+        Q = Qs.to(dev, torch.float32 if kind == "fp32" else torch.bfloat16)
         idx[name] = (ix, Q, ix.score(Q).clone())     # every query's scores, once
         del tok
     rng = np.random.default_rng(4)
