@@ -291,10 +291,20 @@ bool take_pending(const void* ws, Pending* out) {
 // fusion done, [4] rerank enqueued, [5] exit (cbv2_retrieve_host_marks; the
 // latency lab lines them up with a kernel trace).
 thread_local int64_t t_marks[6] = {};
-inline void mark(int i) {
-  t_marks[i] = std::chrono::duration_cast<std::chrono::nanoseconds>(
-                   std::chrono::steady_clock::now().time_since_epoch()).count();
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
 }
+inline void mark(int i) { t_marks[i] = now_ns(); }
+
+// Lab probe of begin (cbv2_set_begin_probe / cbv2_retrieve_begin_marks,
+// internal; off by default): [0] begin entered, [1] the search returned
+// (every launch enqueued), [2] the host saw the search's ready flags (the
+// first kernel's last store: an upper bound, with no profiler attached, on
+// when the first kernel ran), 0 where not taken.  On, begin polls for the
+// flags before it returns -- a latency lab's knob, never the product's.
+thread_local int32_t t_begin_probe = 0;
+thread_local int64_t t_begin_marks[3] = {};
 
 // Selects the index's device for one call and restores the caller's.
 struct DevSel {
@@ -544,6 +554,12 @@ void cbv2_set_wait_lab(int64_t ticks, int32_t publish_delay_us) {
 }
 void cbv2_set_host_rerank(int32_t on) { g_host_rerank = on; }
 void cbv2_set_prearm(int32_t on) { g_prearm = on; }
+void cbv2_set_begin_probe(int32_t on) { t_begin_probe = on; }
+int cbv2_retrieve_begin_marks(int64_t* out, int32_t max) {
+  if (!out || max < 0) return err(CBV2_EINVAL, "null output");
+  for (int i = 0; i < 3 && i < max; ++i) out[i] = t_begin_marks[i];
+  return CBV2_OK;
+}
 
 int cbv2_retrieve_cancel(cbv2_index* ix, void* workspace, void* stream) {
   if (!ix) return err(CBV2_EINVAL, "null index");
@@ -577,6 +593,7 @@ size_t cbv2_retrieve_host_bytes(int32_t B, int32_t k, int32_t kb, int32_t C) {
 
 int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_dtype, int32_t B, int32_t lq,
                         int32_t k, int32_t kb, int32_t C, void* workspace, size_t workspace_bytes, void* stream) {
+  if (t_begin_probe) t_begin_marks[0] = now_ns(), t_begin_marks[1] = t_begin_marks[2] = 0;
   Kind kd;
   if (int rc = check_common(ix, &kd, c, Q, q_dtype, B, lq, k, kb)) return rc;
   if (C < 1) return err(CBV2_EINVAL, "C must be >= 1 (got %d)", C);
@@ -615,10 +632,14 @@ int cbv2_retrieve_begin(cbv2_index* ix, cbv2_comm* c, const void* Q, int32_t q_d
                          L.base, L.stage2, L.s, L.ids, L.status, stream);
   else
     rc = cbv2_search(ix, CBV2_SCORER_MAXSIM, Q, q_dtype, B, lq, k, L.base, L.stage2, L.s, L.ids, stream);
+  if (t_begin_probe) t_begin_marks[1] = now_ns();
   int64_t ld = 0;
   if (cbv2_last_ready_flag(&ld) != nullptr) {   // one flag per row (ld 1) or one for all (ld 0)
     pd.ready = (const int32_t*)((const uint64_t*)pd.mb.h + ready_word_off(pd.mb, B));
     pd.ready_n = ld != 0 ? B : 1;
+    if (t_begin_probe && rc == CBV2_OK &&
+        flags_seen(pd.ready, pd.ready_n, pd.ready_seq, std::chrono::microseconds(2000)))
+      t_begin_marks[2] = now_ns();
   } else {
     pd.ready_seq = 0;   // this search's path wrote no flag: the GPU rerank
   }
