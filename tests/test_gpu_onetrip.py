@@ -94,6 +94,43 @@ def test_one_trip_equals_composed(dev, kind, B):
         assert set(got[1][b].tolist()) == set(planted[b].tolist())
 
 
+@pytest.mark.parametrize("kind", ["bf16", "fp32"])
+def test_begin_probe_marks_and_results(dev, kind):
+    """The latency lab's begin probe (tools/launch_latency.py): with it on,
+    begin stamps entry <= search returned <= ready flags seen (the faithful
+    search's split kernel always publishes them; a small bf16 shard's scan
+    path may publish none: 0) and the results equal the probe-off call's;
+    off again, begin stamps nothing."""
+    L = _lib.lib()
+    L.cbv2_set_begin_probe.argtypes = [ctypes.c_int32]
+    L.cbv2_set_begin_probe.restype = None
+    L.cbv2_retrieve_begin_marks.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    N, B = 5000, 1
+    Qf, _, tokens, doclens, (terms, off, V) = _corpus(dev, N, B, seed=77,
+                                                      dtype=torch.float32 if kind == "fp32" else torch.bfloat16)
+    ix = ColbertIndex.faithful_f32(tokens, doclens) if kind == "fp32" else ColbertIndex(tokens, doclens)
+    Q = Qf.to(dev, torch.float32 if kind == "fp32" else torch.bfloat16)
+    lex = NativeBM25(terms, off, V)
+    qt, qo = synth.bm25_queries(B)
+    bm = lambda: lex.search(qt, qo, KB)   # noqa: E731
+    one = OneTripRetriever(ix, colbert_k=K, fused=C, final_k=KF)
+    want = one(Q, bm, host=True)
+    marks = (ctypes.c_int64 * 3)()
+    L.cbv2_set_begin_probe(1)
+    try:
+        got = one(Q, bm, host=True)
+        assert L.cbv2_retrieve_begin_marks(marks, 3) == 0
+    finally:
+        L.cbv2_set_begin_probe(0)
+    assert all(np.array_equal(g, w) for g, w in zip(got, want))
+    assert 0 < marks[0] <= marks[1], list(marks)
+    assert marks[1] <= marks[2] or (kind == "bf16" and marks[2] == 0), list(marks)
+    one(Q, bm, host=True)
+    again = (ctypes.c_int64 * 3)()
+    L.cbv2_retrieve_begin_marks(again, 3)
+    assert list(again) == list(marks)          # probe off: begin left the last probe's marks alone
+
+
 def test_one_trip_long_queries_and_bad_input(dev):
     N = 300
     Qf, _, tokens, doclens, _ = _corpus(dev, N, 2, seed=5)
