@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--dtype", default="both", choices=["bf16", "fp32", "both"])
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--label", default="bare", help="names the run in the output (bare / traced)")
+    ap.add_argument("--idle", default="sleep", choices=["sleep", "spin"],
+                    help="how the host waits out the 2 ms between calls: sleep (the bench's latency loop) or "
+                         "spin (the CPU stays awake)")
     a = ap.parse_args()
     import torch
     sys.path.insert(0, ROOT)
@@ -71,7 +74,12 @@ def main():
             for name, (one, Q1) in legs.items():
                 Q1 = Q1.contiguous()
                 torch.cuda.synchronize()
-                time.sleep(0.002)
+                if a.idle == "sleep":
+                    time.sleep(0.002)
+                else:
+                    t_end = time.perf_counter() + 0.002
+                    while time.perf_counter() < t_end:
+                        pass
                 one(Q1, bm_one, host=True)
                 L.cbv2_retrieve_begin_marks(bm, 3)
                 m = one.marks
@@ -83,7 +91,7 @@ def main():
     finally:
         L.cbv2_set_begin_probe(0)
     for name, rs in rows.items():
-        out = {"leg": name, "docs": n, "calls": len(rs), "run": a.label}
+        out = {"leg": name, "docs": n, "calls": len(rs), "run": a.label, "idle": a.idle}
         for key in (rs[0] if rs else {}):
             v = sorted(r[key] for r in rs)
             out[key + "_us"] = {"p50": round(statistics.median(v) / 1e3, 2), "p10": round(v[len(v) // 10] / 1e3, 2),
